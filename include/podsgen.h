@@ -1,0 +1,153 @@
+/*
+ * podsgen.h -- C ABI of libpodsgen.so, the MI355X (gfx950) engine behind the
+ * digital-filter + PODFS hot path of sidbannet/PODS-digital-filter.
+ *
+ * The reference has no FFI: its "operator API" is a set of Python functions that
+ * mutate numpy arrays.  Each entry point below replaces one of them;
+ * the Python drop-in modules (pods-digital-filter_amd/digitalfilters.py, PODFS.py)
+ * keep the reference signatures and call these through ctypes.
+ *
+ * Conventions
+ *   - every function returns int: PODS_OK (0) or a negative PODS_ERR_* code; the
+ *     message of the last failure on the calling thread is pods_last_error().
+ *   - no C++ exception crosses the ABI; HIP errors map to PODS_ERR_HIP.
+ *   - the caller owns every output buffer.  "_dev" pointers are device pointers on the
+ *     context's device (e.g. torch tensor data_ptr()); "_host" pointers are host memory.
+ *   - a context is bound to one device and one HIP stream (pods_set_stream); it is not
+ *     thread-safe.  Calls enqueue on that stream; functions that return host data
+ *     synchronise the stream before returning.
+ *   - plain pointers and sizes only, no torch types.
+ */
+#ifndef PODSGEN_H
+#define PODSGEN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PODS_ABI_VERSION 1
+
+enum {
+  PODS_OK = 0,
+  PODS_ERR_ARG = -1,         /* bad argument / shape                        */
+  PODS_ERR_HIP = -2,         /* HIP runtime error                           */
+  PODS_ERR_STATE = -3,       /* call order (e.g. generate before configure) */
+  PODS_ERR_NOMEM = -4,       /* device allocation failed                    */
+  PODS_ERR_INTERNAL = -5,
+  PODS_ERR_UNSUPPORTED = -6
+};
+
+/* Lund transform variants (digitalfilters.py:143-178 adapt1d, :180-231 adapt2prf). */
+enum { PODS_LUND_1D = 0, PODS_LUND_PRF = 1, PODS_LUND_NONE = -1 };
+
+typedef struct pods_ctx pods_ctx;
+
+/* Digital-filter problem description (digitalfilters.py main(), :1244-1397). */
+typedef struct pods_df_params {
+  int32_t jma, kma;      /* inlet grid: J spanwise rows, K wall-normal columns      */
+  int32_t ns;            /* snapshots (time steps)                                  */
+  int32_t nfx, nfy, nfz; /* half filter widths: taps = 2*nf+1                       */
+  int32_t j0, j1;        /* row slab owned by this context, 0 <= j0 < j1 <= jma     */
+  int32_t lund_mode;     /* PODS_LUND_1D | PODS_LUND_PRF | PODS_LUND_NONE           */
+  int32_t rotate;        /* 0: rotation is the identity (skipped); 1: apply rot[9]  */
+  uint32_t seed;         /* numpy legacy RandomState / np.random.seed value         */
+  int32_t reserved;
+  double rng_low;        /* uniform low   (-sqrt(3), digitalfilters.py:1340)        */
+  double rng_range;      /* high - low    (2*sqrt(3))                               */
+} pods_df_params;
+
+const char* pods_last_error(void);
+int pods_abi_version(void);
+
+/* Context lifetime.  Replaces nothing in the reference (single Python process). */
+int pods_create(pods_ctx** out, int device);
+int pods_destroy(pods_ctx* ctx);
+/* Enqueue all work on this hipStream_t (NULL = legacy default stream). */
+int pods_set_stream(pods_ctx* ctx, void* hip_stream);
+int pods_synchronize(pods_ctx* ctx);
+
+/* ---- generation: digitalfilters.py main() step loop :1403-1477 --------------------
+ * bx/by/bz: filter taps (calccoeff, :73-89), lengths 2nf+1, host.
+ * lund_host: 9 x P_local SoA rows a00,a10,a11,a20,a21,a22,U,V,W for the slab's points
+ *            (P-index j*K + k, j relative to j0), host.
+ * rot_host:  3x3 row-major rotation (prof_rotation_matrix, :1064-1116), host, used
+ *            when params->rotate != 0.
+ * Allocates the device buffers of the run (random stream slab, x-filtered planes,
+ * snapshot matrix). */
+int pods_df_configure(pods_ctx* ctx, const pods_df_params* params, const double* bx,
+                      const double* by, const double* bz, const double* lund_host,
+                      const double* rot_host);
+/* RNG + 3 separable filter passes + Lund + rotation for all ns steps
+ * (filter3DSciPy1D :100-140 x3, adapt1d/adapt2prf, rotate_velocity, A[:,i] = ... :1471).
+ * The snapshot matrix stays on the device, snapshot-major: A_T[i][c*P_local + p]. */
+int pods_df_generate(pods_ctx* ctx);
+/* Device pointer and row length (= 3*P_local) of the snapshot matrix A_T (ns rows). */
+int pods_df_snapshots(pods_ctx* ctx, double** a_dev, int64_t* row_len);
+
+/* Load an existing snapshot matrix instead of generating one (PODFS.POD called on a
+ * user array, PODFS.py:1294).  at_host: snapshot-major ns x row_len (row i = A[:, i]). */
+int pods_set_snapshots(pods_ctx* ctx, const double* at_host, int ns, int64_t row_len);
+
+/* Stream-ordered copy between host/device buffers of this context's device
+ * (kind: 0 = host->device, 1 = device->host, 2 = device->device).  device->host
+ * synchronises the stream before returning. */
+int pods_copy(pods_ctx* ctx, void* dst, const void* src, size_t bytes, int kind);
+
+/* mean over snapshots with numpy's pairwise order, np.mean(A,1) (:1492).  The context
+ * keeps the mean for pods_corr / pods_spatial_modes (A - mean, :1493-1495);
+ * mean_out (3*P_local doubles) may be NULL. */
+int pods_mean(pods_ctx* ctx, double* mean_out, int out_is_device);
+
+/* Correlation C = (A-m)^T (A-m) [/ns] (PODFS.py:1451-1455).  C_dev: ns x ns row-major,
+ * full symmetric.  divide = 1 divides by ns (single device); multi-device callers pass 0,
+ * all-reduce the partials, then call pods_divide_inplace(C, ns*ns, ns). */
+int pods_corr(pods_ctx* ctx, double* C_dev, int divide);
+/* x[i] = x[i] / divisor for n doubles on the device. */
+int pods_divide_inplace(pods_ctx* ctx, double* x_dev, int64_t n, double divisor);
+
+/* Temporal modes after sort_eigenvalues + scaling (PODFS.py:1310, :1323-1325).
+ * V_dev: eigenvectors from a symmetric solver in ASCENDING eigenvalue order, element
+ * (i, j) at V_dev[i*v_rs + j*v_cs].  Output T_dev (ns x ncols, row-major) holds column j
+ * = V[:, ns-1-j] (descending order) scaled by sqrt(lambda_j / (sum_i V_ij^2 / ns)) for
+ * j < nvalid (sequential sum, Python builtin).  lambda_desc_host: ncols eigenvalues in
+ * descending order. */
+int pods_temporal_modes(pods_ctx* ctx, const double* V_dev, int64_t v_rs, int64_t v_cs,
+                        const double* lambda_desc_host, int nvalid, int ncols, double* T_dev);
+
+/* Spatial modes Phi = ((A-m) T[:, :nm]) * (1/lambda) / ns (PODFS.py:1330-1333).
+ * T_dev: ns x ldT row-major.  phi_dev: 3*P_local x nm row-major (reference layout). */
+int pods_spatial_modes(pods_ctx* ctx, const double* T_dev, int ldT, const double* lambda_host,
+                       int nm, double* phi_dev);
+
+/* Shifted direct DFT of the temporal modes (PODFS.py:1562-1571):
+ * c[n][i] = sum_m T[m][i] exp(-1j 2 k pi t_m / period) / ns,  k = n - ns//2,
+ * complex64 interleaved (re, im), row-major ns x nm.  t_host: ns sample times. */
+int pods_fourier(pods_ctx* ctx, const double* T_dev, int ldT, int nm, int ns,
+                 const double* t_host, double period, float* c_dev);
+
+/* ---- unit-level entry points (reference operator API, one call each) ------------- */
+/* filter3DSciPy1D(x, y, ...) (:100-140) on one host block x of shape
+ * (2nfx+1, 2nfy+J, 2nfz+K) C-order -> y (J, K). */
+int pods_filter_block(pods_ctx* ctx, const double* x_host, int nfx, int nfy, int nfz, int jma,
+                      int kma, const double* bx, const double* by, const double* bz,
+                      double* y_host);
+/* The first n doubles of np.random.RandomState(seed).uniform(low, low+range) computed
+ * on the device with jump-ahead substreams; out_dev: n doubles. */
+int pods_rng_uniform(pods_ctx* ctx, uint32_t seed, int64_t n, double low, double range,
+                     double* out_dev);
+
+/* ---- host-only self checks (no GPU needed) ------------------------------------------ */
+/* MT19937 jump-ahead math check: jumps mt^(1) of `seed` by 624*(nblocks-1) words with the
+ * GF(2) polynomial machinery on the host and compares with sequential twisting.
+ * Returns PODS_OK when equal. */
+int pods_host_mt_jump_check(uint32_t seed, int64_t nblocks);
+/* Characteristic polynomial degree found by Berlekamp-Massey (expect 19937). */
+int pods_host_mt_charpoly_degree(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PODSGEN_H */

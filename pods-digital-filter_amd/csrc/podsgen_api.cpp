@@ -1,0 +1,601 @@
+// C ABI of libpodsgen.so (include/podsgen.h): context, buffers, call sequencing.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <exception>
+#include <string>
+#include <vector>
+
+#include "mt_host.h"
+#include "podsgen.h"
+#include "podsgen_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define PODS_HIP(expr)                                                                  \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess)                                                               \
+      return fail(PODS_ERR_HIP, std::string(#expr) + " failed: " + hipGetErrorString(_e)); \
+  } while (0)
+
+#define PODS_TRY try {
+#define PODS_CATCH                                          \
+  }                                                         \
+  catch (const std::exception& e) {                         \
+    return fail(PODS_ERR_INTERNAL, std::string("exception: ") + e.what()); \
+  }                                                         \
+  catch (...) {                                             \
+    return fail(PODS_ERR_INTERNAL, "unknown exception");   \
+  }
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+hipError_t ensure(DevBuf& b, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (b.bytes >= bytes) return hipSuccess;
+  if (b.p) {
+    hipError_t e = hipFree(b.p);
+    if (e != hipSuccess) return e;
+    b.p = nullptr;
+    b.bytes = 0;
+  }
+  hipError_t e = hipMalloc(&b.p, bytes);
+  if (e != hipSuccess) {
+    b.p = nullptr;
+    return e;
+  }
+  b.bytes = bytes;
+  return hipSuccess;
+}
+
+void release(DevBuf& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+}
+
+// numpy pairwise-sum programs (oracle/pods_oracle.py pairwise_program / cpairwise_program)
+constexpr int PW_BLOCKSIZE = 128;
+constexpr int NPY_BUFSIZE = 8192;
+
+void pw_rec(std::vector<int>& prog, int start, int m) {
+  if (m <= PW_BLOCKSIZE) {
+    prog.push_back(start);
+    prog.push_back(m);
+    return;
+  }
+  int m2 = m / 2;
+  m2 -= m2 % 8;
+  pw_rec(prog, start, m2);
+  pw_rec(prog, start + m2, m - m2);
+  prog.push_back(-1);
+  prog.push_back(0);
+}
+
+std::vector<int> pairwise_program(int n) {
+  std::vector<int> prog;
+  for (int s = 0; s < n; s += NPY_BUFSIZE) {
+    pw_rec(prog, s, std::min(NPY_BUFSIZE, n - s));
+    if (s) {
+      prog.push_back(-1);
+      prog.push_back(0);
+    }
+  }
+  return prog;
+}
+
+void cpw_rec(std::vector<int>& prog, int start, int m) {
+  if (2 * m <= PW_BLOCKSIZE) {
+    prog.push_back(start);
+    prog.push_back(m);
+    return;
+  }
+  int h = m - m % 8;
+  int m2 = h / 2;
+  cpw_rec(prog, start, m2);
+  cpw_rec(prog, start + m2, m - m2);
+  prog.push_back(-1);
+  prog.push_back(0);
+}
+
+std::vector<int> cpairwise_program(int n) {
+  std::vector<int> prog;
+  for (int s = 0; s < n; s += NPY_BUFSIZE) {
+    cpw_rec(prog, s, std::min(NPY_BUFSIZE, n - s));
+    if (s) {
+      prog.push_back(-1);
+      prog.push_back(0);
+    }
+  }
+  return prog;
+}
+
+// Substream layout of an MT19937 stream of `ntot` doubles (312 per 624-word block).
+struct RngLayout {
+  int64_t ntot = 0, Bs = 0;
+  int G = 0, G1 = 0, G2 = 64;
+  std::vector<int> j1_src, j1_poly, j1_dst, j2_src, j2_poly, j2_dst;
+};
+
+RngLayout make_layout(int64_t ntot) {
+  RngLayout L;
+  L.ntot = ntot;
+  const int64_t blocks = (ntot + 311) / 312;
+  int64_t want = (blocks + 2047) / 2048;
+  int64_t Bs = 1024;
+  while (Bs < want) Bs *= 2;
+  L.Bs = Bs;
+  L.G = (int)std::max<int64_t>(1, (blocks + Bs - 1) / Bs);
+  L.G1 = L.G >= 2 ? (L.G - 1 + L.G2 - 1) / L.G2 : 1;
+  for (int g1 = 1; g1 < L.G1; ++g1) {
+    L.j1_src.push_back(0);
+    L.j1_poly.push_back(g1);
+    L.j1_dst.push_back(g1);
+  }
+  for (int g = 1; g < L.G; ++g) {
+    L.j2_src.push_back((g - 1) / L.G2);
+    L.j2_poly.push_back((g - 1) % L.G2 + 1);
+    L.j2_dst.push_back(g);
+  }
+  return L;
+}
+
+struct RngBuffers {
+  DevBuf states, bases, poly1, poly2, j1, j2;
+  int64_t Bs_loaded = 0;
+  int G1_loaded = 0;
+  std::vector<uint32_t> seed_host;  // 2 x 624 staging (mt^(0), mt^(1))
+  void free_all() {
+    release(states); release(bases); release(poly1); release(poly2); release(j1); release(j2);
+    Bs_loaded = 0;
+    G1_loaded = 0;
+  }
+};
+
+}  // namespace
+
+struct pods_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool configured = false;
+  pods_df_params p{};
+  int NX = 0, NY = 0, NZ = 0, Kp = 0, jl = 0;
+  int64_t S = 0, Sl = 0, Pl = 0, rowlen = 0;
+  RngLayout layout;
+  RngBuffers rng;
+  DevBuf R, T1, A, mean, lund, taps, rot, prog_mean, prog_dft, tbuf, mag, lam;
+  int nprog_mean = 0;
+  bool mean_valid = false;
+  bool have_snapshots = false;  // A holds ns x rowlen snapshots (generated or loaded)
+  std::vector<double> stage;  // host staging for small uploads
+};
+
+namespace {
+
+int upload_rng(pods_ctx* c, const RngLayout& L, uint32_t seed, RngBuffers& rb) {
+  using namespace pods::mt;
+  const JumpTables& jt = jump_tables(L.Bs, L.G2, std::max(L.G1, 1));
+  PODS_HIP(ensure(rb.states, (size_t)L.G * N * 4));
+  PODS_HIP(ensure(rb.bases, (size_t)std::max(L.G1, 1) * N * 4));
+  if (rb.Bs_loaded != L.Bs || rb.G1_loaded < L.G1) {
+    PODS_HIP(ensure(rb.poly1, (size_t)std::max(L.G1, 1) * N * 4));
+    PODS_HIP(ensure(rb.poly2, (size_t)(L.G2 + 1) * N * 4));
+    PODS_HIP(hipMemcpy(rb.poly1.p, jt.level1.data(), (size_t)std::max(L.G1, 1) * N * 4,
+                       hipMemcpyHostToDevice));
+    PODS_HIP(hipMemcpy(rb.poly2.p, jt.level2.data(), (size_t)(L.G2 + 1) * N * 4,
+                       hipMemcpyHostToDevice));
+    rb.Bs_loaded = L.Bs;
+    rb.G1_loaded = L.G1;
+  }
+  const size_t n1 = L.j1_src.size(), n2 = L.j2_src.size();
+  std::vector<int> jobs;
+  jobs.insert(jobs.end(), L.j1_src.begin(), L.j1_src.end());
+  jobs.insert(jobs.end(), L.j1_poly.begin(), L.j1_poly.end());
+  jobs.insert(jobs.end(), L.j1_dst.begin(), L.j1_dst.end());
+  jobs.insert(jobs.end(), L.j2_src.begin(), L.j2_src.end());
+  jobs.insert(jobs.end(), L.j2_poly.begin(), L.j2_poly.end());
+  jobs.insert(jobs.end(), L.j2_dst.begin(), L.j2_dst.end());
+  PODS_HIP(ensure(rb.j1, jobs.size() * sizeof(int) + 16));
+  PODS_HIP(hipMemcpy(rb.j1.p, jobs.data(), jobs.size() * sizeof(int), hipMemcpyHostToDevice));
+  (void)n1;
+  (void)n2;
+  rb.seed_host.assign(2 * N, 0);
+  seed_state(seed, rb.seed_host.data());
+  std::memcpy(rb.seed_host.data() + N, rb.seed_host.data(), N * 4);
+  twist(rb.seed_host.data() + N);
+  return PODS_OK;
+}
+
+// Enqueue: seed states, level-1 and level-2 jumps (stream-ordered after the uploads).
+int run_jumps(pods_ctx* c, const RngLayout& L, RngBuffers& rb) {
+  using namespace pods::mt;
+  PODS_HIP(hipMemcpyAsync(rb.states.p, rb.seed_host.data(), N * 4, hipMemcpyHostToDevice, c->stream));
+  PODS_HIP(hipMemcpyAsync(rb.bases.p, rb.seed_host.data() + N, N * 4, hipMemcpyHostToDevice,
+                          c->stream));
+  const int n1 = (int)L.j1_src.size(), n2 = (int)L.j2_src.size();
+  const int* jb = rb.j1.as<int>();
+  PODS_HIP(pods::launch_mt_jump(rb.bases.as<uint32_t>(), jb, rb.poly1.as<uint32_t>(), jb + n1,
+                                rb.bases.as<uint32_t>(), jb + 2 * n1, n1, c->stream));
+  const int* j2 = jb + 3 * n1;
+  PODS_HIP(pods::launch_mt_jump(rb.bases.as<uint32_t>(), j2, rb.poly2.as<uint32_t>(), j2 + n2,
+                                rb.states.as<uint32_t>(), j2 + 2 * n2, n2, c->stream));
+  return PODS_OK;
+}
+
+int check_ctx(pods_ctx* c) {
+  if (!c) return fail(PODS_ERR_ARG, "null context");
+  return PODS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* pods_last_error(void) { return g_err.c_str(); }
+int pods_abi_version(void) { return PODS_ABI_VERSION; }
+
+int pods_create(pods_ctx** out, int device) {
+  PODS_TRY
+  if (!out) return fail(PODS_ERR_ARG, "out is null");
+  *out = nullptr;
+  int n = 0;
+  PODS_HIP(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n)
+    return fail(PODS_ERR_ARG, "device " + std::to_string(device) + " out of range (" +
+                                  std::to_string(n) + " devices)");
+  PODS_HIP(hipSetDevice(device));
+  pods_ctx* c = new pods_ctx();
+  c->device = device;
+  *out = c;
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_destroy(pods_ctx* c) {
+  PODS_TRY
+  if (!c) return PODS_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (DevBuf* b : {&c->R, &c->T1, &c->A, &c->mean, &c->lund, &c->taps, &c->rot, &c->prog_mean,
+                    &c->prog_dft, &c->tbuf, &c->mag, &c->lam})
+    release(*b);
+  c->rng.free_all();
+  delete c;
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_set_stream(pods_ctx* c, void* stream) {
+  if (int e = check_ctx(c)) return e;
+  c->stream = static_cast<hipStream_t>(stream);
+  return PODS_OK;
+}
+
+int pods_synchronize(pods_ctx* c) {
+  if (int e = check_ctx(c)) return e;
+  PODS_HIP(hipStreamSynchronize(c->stream));
+  return PODS_OK;
+}
+
+int pods_df_configure(pods_ctx* c, const pods_df_params* prm, const double* bx, const double* by,
+                      const double* bz, const double* lund_host, const double* rot_host) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!prm || !bx || !by || !bz) return fail(PODS_ERR_ARG, "null params/taps");
+  const pods_df_params& p = *prm;
+  if (p.jma <= 0 || p.kma <= 0 || p.ns <= 0) return fail(PODS_ERR_ARG, "jma, kma, ns must be > 0");
+  if (p.nfx < 0 || p.nfy < 0 || p.nfz < 0) return fail(PODS_ERR_ARG, "negative filter width");
+  if (2 * p.nfx + 1 > 49) return fail(PODS_ERR_UNSUPPORTED, "2*nfx+1 > 49 taps");
+  if (2 * p.nfy + 1 > 25) return fail(PODS_ERR_UNSUPPORTED, "2*nfy+1 > 25 taps");
+  if (p.j0 < 0 || p.j1 > p.jma || p.j0 >= p.j1) return fail(PODS_ERR_ARG, "bad row slab [j0, j1)");
+  if (p.lund_mode != PODS_LUND_1D && p.lund_mode != PODS_LUND_PRF && p.lund_mode != PODS_LUND_NONE)
+    return fail(PODS_ERR_ARG, "bad lund_mode");
+  if (p.lund_mode != PODS_LUND_NONE && !lund_host) return fail(PODS_ERR_ARG, "lund_host is null");
+  if (p.rotate && !rot_host) return fail(PODS_ERR_ARG, "rot_host is null");
+  PODS_HIP(hipSetDevice(c->device));
+  c->p = p;
+  c->NX = 2 * p.nfx + 1;
+  c->NY = 2 * p.nfy + 1;
+  c->NZ = 2 * p.nfz + 1;
+  c->Kp = p.kma + 2 * p.nfz;
+  c->jl = p.j1 - p.j0;
+  c->S = (int64_t)(p.jma + 2 * p.nfy) * c->Kp;
+  c->Sl = (int64_t)(c->jl + 2 * p.nfy) * c->Kp;
+  c->Pl = (int64_t)c->jl * p.kma;
+  c->rowlen = 3 * c->Pl;
+  if (p.kma > pods::filter_yz_max_K(c->Kp))
+    return fail(PODS_ERR_UNSUPPORTED, "kma too large for the y/z filter kernel");
+  const int64_t nplanes = 3 * (int64_t)(c->NX + p.ns - 1);
+  const int64_t ntot = nplanes * c->S;  // doubles of the stream that reach A
+  c->layout = make_layout(ntot);
+  PODS_HIP(ensure(c->R, (size_t)nplanes * c->Sl * sizeof(double)));
+  PODS_HIP(ensure(c->T1, (size_t)3 * p.ns * c->Sl * sizeof(double)));
+  PODS_HIP(ensure(c->A, (size_t)p.ns * c->rowlen * sizeof(double)));
+  PODS_HIP(ensure(c->mean, (size_t)c->rowlen * sizeof(double)));
+  PODS_HIP(ensure(c->lund, (size_t)9 * c->Pl * sizeof(double)));
+  PODS_HIP(ensure(c->taps, (size_t)(c->NX + c->NY + c->NZ) * sizeof(double)));
+  PODS_HIP(ensure(c->rot, 9 * sizeof(double)));
+  std::vector<double> taps(c->NX + c->NY + c->NZ);
+  std::copy(bx, bx + c->NX, taps.begin());
+  std::copy(by, by + c->NY, taps.begin() + c->NX);
+  std::copy(bz, bz + c->NZ, taps.begin() + c->NX + c->NY);
+  PODS_HIP(hipMemcpy(c->taps.p, taps.data(), taps.size() * sizeof(double), hipMemcpyHostToDevice));
+  if (lund_host)
+    PODS_HIP(hipMemcpy(c->lund.p, lund_host, (size_t)9 * c->Pl * sizeof(double), hipMemcpyHostToDevice));
+  double r9[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+  if (p.rotate) std::memcpy(r9, rot_host, sizeof(r9));
+  PODS_HIP(hipMemcpy(c->rot.p, r9, sizeof(r9), hipMemcpyHostToDevice));
+  std::vector<int> prog = pairwise_program(p.ns);
+  c->nprog_mean = (int)prog.size() / 2;
+  PODS_HIP(ensure(c->prog_mean, prog.size() * sizeof(int)));
+  PODS_HIP(hipMemcpy(c->prog_mean.p, prog.data(), prog.size() * sizeof(int), hipMemcpyHostToDevice));
+  if (int e = upload_rng(c, c->layout, p.seed, c->rng)) return e;
+  c->configured = true;
+  c->have_snapshots = false;
+  c->mean_valid = false;
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_df_generate(pods_ctx* c) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!c->configured) return fail(PODS_ERR_STATE, "pods_df_generate before pods_df_configure");
+  PODS_HIP(hipSetDevice(c->device));
+  const pods_df_params& p = c->p;
+  const RngLayout& L = c->layout;
+  if (int e = run_jumps(c, L, c->rng)) return e;
+  PODS_HIP(pods::launch_mt_generate(c->rng.states.as<uint32_t>(), L.G, L.Bs, L.ntot, c->S, c->Kp, p.j0,
+                                    p.j1 + 2 * p.nfy, c->Sl, p.rng_low, p.rng_range, c->R.as<double>(),
+                                    c->stream));
+  // x pass: enough (component, point, step-chunk) threads to fill the chip
+  const int64_t pts = 3 * c->Sl;
+  int64_t nch = (256LL * 2048 + pts - 1) / pts;
+  nch = std::max<int64_t>(1, std::min<int64_t>(nch, std::max(1, p.ns / 16)));
+  const int chunk = (int)((p.ns + nch - 1) / nch);
+  const double* taps = c->taps.as<double>();
+  PODS_HIP(pods::launch_filter_x(c->NX, c->R.as<double>(), taps, p.ns, c->Sl, 3, chunk,
+                                 c->T1.as<double>(), c->stream));
+  PODS_HIP(pods::launch_filter_yz(c->NY, c->T1.as<double>(), taps + c->NX, taps + c->NX + c->NY,
+                                  c->NZ, p.ns, c->jl, p.kma, c->Kp, c->Sl, 3, c->lund.as<double>(),
+                                  p.lund_mode, c->rot.as<double>(), p.rotate, c->A.as<double>(),
+                                  c->rowlen, c->stream));
+  c->have_snapshots = true;
+  c->mean_valid = false;
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_df_snapshots(pods_ctx* c, double** a_dev, int64_t* row_len) {
+  if (int e = check_ctx(c)) return e;
+  if (!c->configured && !c->have_snapshots) return fail(PODS_ERR_STATE, "no snapshot buffer");
+  if (a_dev) *a_dev = c->A.as<double>();
+  if (row_len) *row_len = c->rowlen;
+  return PODS_OK;
+}
+
+int pods_set_snapshots(pods_ctx* c, const double* at, int ns, int64_t rowlen) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!at || ns <= 0 || rowlen <= 0) return fail(PODS_ERR_ARG, "bad snapshot matrix");
+  PODS_HIP(hipSetDevice(c->device));
+  PODS_HIP(ensure(c->A, (size_t)ns * rowlen * sizeof(double)));
+  PODS_HIP(ensure(c->mean, (size_t)rowlen * sizeof(double)));
+  PODS_HIP(hipMemcpy(c->A.p, at, (size_t)ns * rowlen * sizeof(double), hipMemcpyHostToDevice));
+  std::vector<int> prog = pairwise_program(ns);
+  c->nprog_mean = (int)prog.size() / 2;
+  PODS_HIP(ensure(c->prog_mean, prog.size() * sizeof(int)));
+  PODS_HIP(hipMemcpy(c->prog_mean.p, prog.data(), prog.size() * sizeof(int), hipMemcpyHostToDevice));
+  c->p = pods_df_params{};
+  c->p.ns = ns;
+  c->rowlen = rowlen;
+  c->configured = false;
+  c->have_snapshots = true;
+  c->mean_valid = false;
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_copy(pods_ctx* c, void* dst, const void* src, size_t bytes, int kind) {
+  if (int e = check_ctx(c)) return e;
+  if (!dst || !src) return fail(PODS_ERR_ARG, "null pointer");
+  if (bytes == 0) return PODS_OK;
+  const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice
+                          : kind == 1 ? hipMemcpyDeviceToHost
+                                      : hipMemcpyDeviceToDevice;
+  if (kind < 0 || kind > 2) return fail(PODS_ERR_ARG, "bad copy kind");
+  PODS_HIP(hipMemcpyAsync(dst, src, bytes, k, c->stream));
+  if (kind != 2) PODS_HIP(hipStreamSynchronize(c->stream));
+  return PODS_OK;
+}
+
+int pods_mean(pods_ctx* c, double* mean_out, int out_is_device) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!c->have_snapshots) return fail(PODS_ERR_STATE, "pods_mean before snapshots exist");
+  PODS_HIP(hipSetDevice(c->device));
+  PODS_HIP(pods::launch_mean(c->A.as<double>(), c->rowlen, c->p.ns, c->prog_mean.as<int>(),
+                             c->nprog_mean, c->mean.as<double>(), c->stream));
+  c->mean_valid = true;
+  if (mean_out) {
+    const size_t bytes = (size_t)c->rowlen * sizeof(double);
+    if (out_is_device) {
+      PODS_HIP(hipMemcpyAsync(mean_out, c->mean.p, bytes, hipMemcpyDeviceToDevice, c->stream));
+    } else {
+      PODS_HIP(hipMemcpyAsync(mean_out, c->mean.p, bytes, hipMemcpyDeviceToHost, c->stream));
+      PODS_HIP(hipStreamSynchronize(c->stream));
+    }
+  }
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_corr(pods_ctx* c, double* C_dev, int divide) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!c->have_snapshots || !c->mean_valid) return fail(PODS_ERR_STATE, "pods_corr needs pods_mean first");
+  if (!C_dev) return fail(PODS_ERR_ARG, "C_dev is null");
+  PODS_HIP(hipSetDevice(c->device));
+  PODS_HIP(pods::launch_syrk(c->A.as<double>(), c->rowlen, c->p.ns, c->rowlen, c->mean.as<double>(),
+                             C_dev, c->p.ns, divide, c->stream));
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_divide_inplace(pods_ctx* c, double* x, int64_t n, double d) {
+  if (int e = check_ctx(c)) return e;
+  PODS_HIP(pods::launch_divide(x, n, d, c->stream));
+  return PODS_OK;
+}
+
+int pods_temporal_modes(pods_ctx* c, const double* V, int64_t v_rs, int64_t v_cs,
+                        const double* lam_desc, int nvalid, int ncols, double* T) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!V || !T || !lam_desc) return fail(PODS_ERR_ARG, "null pointer");
+  const int ns = c->have_snapshots ? c->p.ns : 0;
+  if (ns <= 0) return fail(PODS_ERR_STATE, "no snapshots");
+  if (ncols <= 0 || ncols > ns || nvalid > ncols) return fail(PODS_ERR_ARG, "bad ncols/nvalid");
+  PODS_HIP(ensure(c->lam, (size_t)ncols * sizeof(double)));
+  PODS_HIP(ensure(c->mag, (size_t)ncols * sizeof(double)));
+  c->stage.assign(lam_desc, lam_desc + ncols);
+  PODS_HIP(hipMemcpyAsync(c->lam.p, c->stage.data(), (size_t)ncols * sizeof(double),
+                          hipMemcpyHostToDevice, c->stream));
+  PODS_HIP(pods::launch_temporal(V, v_rs, v_cs, ns, ncols, std::max(nvalid, 0), c->lam.as<double>(),
+                                 c->mag.as<double>(), T, c->stream));
+  PODS_HIP(hipStreamSynchronize(c->stream));  // staging buffer reuse
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_spatial_modes(pods_ctx* c, const double* T, int ldT, const double* lam, int nm, double* phi) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!c->have_snapshots || !c->mean_valid) return fail(PODS_ERR_STATE, "pods_spatial_modes needs pods_mean");
+  if (!T || !lam || !phi || nm <= 0 || ldT < nm) return fail(PODS_ERR_ARG, "bad arguments");
+  PODS_HIP(ensure(c->lam, (size_t)nm * sizeof(double)));
+  c->stage.resize(nm);
+  for (int m = 0; m < nm; ++m) c->stage[m] = 1.0 / lam[m];  // np.ones(nm)/energy (PODFS.py:1331)
+  PODS_HIP(hipMemcpyAsync(c->lam.p, c->stage.data(), (size_t)nm * sizeof(double), hipMemcpyHostToDevice,
+                          c->stream));
+  PODS_HIP(pods::launch_spatial(c->A.as<double>(), c->rowlen, c->p.ns, c->mean.as<double>(), T, ldT, nm,
+                                c->lam.as<double>(), phi, c->stream));
+  PODS_HIP(hipStreamSynchronize(c->stream));
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_fourier(pods_ctx* c, const double* T, int ldT, int nm, int ns, const double* t_host,
+                 double period, float* c_dev) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!T || !t_host || !c_dev || nm <= 0 || ns <= 0 || ldT < nm) return fail(PODS_ERR_ARG, "bad arguments");
+  PODS_HIP(hipSetDevice(c->device));
+  std::vector<int> prog = cpairwise_program(ns);
+  PODS_HIP(ensure(c->prog_dft, prog.size() * sizeof(int)));
+  PODS_HIP(ensure(c->tbuf, (size_t)ns * sizeof(double)));
+  PODS_HIP(hipMemcpyAsync(c->prog_dft.p, prog.data(), prog.size() * sizeof(int), hipMemcpyHostToDevice,
+                          c->stream));
+  PODS_HIP(hipMemcpyAsync(c->tbuf.p, t_host, (size_t)ns * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  PODS_HIP(pods::launch_dft(T, ldT, nm, ns, c->tbuf.as<double>(), 1.0 / period, 1.0 / (double)ns,
+                            c->prog_dft.as<int>(), (int)prog.size() / 2,
+                            reinterpret_cast<float2*>(c_dev), c->stream));
+  PODS_HIP(hipStreamSynchronize(c->stream));  // host vectors above go out of scope
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_filter_block(pods_ctx* c, const double* x, int nfx, int nfy, int nfz, int jma, int kma,
+                      const double* bx, const double* by, const double* bz, double* y) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!x || !y || !bx || !by || !bz || jma <= 0 || kma <= 0 || nfx < 0 || nfy < 0 || nfz < 0)
+    return fail(PODS_ERR_ARG, "bad arguments");
+  const int NX = 2 * nfx + 1, NY = 2 * nfy + 1, NZ = 2 * nfz + 1;
+  if (NX > 49 || NY > 25) return fail(PODS_ERR_UNSUPPORTED, "filter too wide");
+  const int Kp = kma + 2 * nfz;
+  if (kma > pods::filter_yz_max_K(Kp)) return fail(PODS_ERR_UNSUPPORTED, "kma too large");
+  PODS_HIP(hipSetDevice(c->device));
+  const int64_t S = (int64_t)(jma + 2 * nfy) * Kp;
+  DevBuf dx, dt1, dy, dtap;
+  auto cleanup = [&] { release(dx); release(dt1); release(dy); release(dtap); };
+  hipError_t e1 = ensure(dx, (size_t)NX * S * 8), e2 = ensure(dt1, (size_t)S * 8),
+             e3 = ensure(dy, (size_t)jma * kma * 8), e4 = ensure(dtap, (size_t)(NX + NY + NZ) * 8);
+  if (e1 || e2 || e3 || e4) {
+    cleanup();
+    return fail(PODS_ERR_NOMEM, "device allocation failed");
+  }
+  std::vector<double> taps(NX + NY + NZ);
+  std::copy(bx, bx + NX, taps.begin());
+  std::copy(by, by + NY, taps.begin() + NX);
+  std::copy(bz, bz + NZ, taps.begin() + NX + NY);
+  hipError_t e = hipMemcpy(dx.p, x, (size_t)NX * S * 8, hipMemcpyHostToDevice);
+  if (!e) e = hipMemcpy(dtap.p, taps.data(), taps.size() * 8, hipMemcpyHostToDevice);
+  const double* tp = dtap.as<double>();
+  if (!e) e = pods::launch_filter_x(NX, dx.as<double>(), tp, 1, S, 1, 1, dt1.as<double>(), c->stream);
+  if (!e)
+    e = pods::launch_filter_yz(NY, dt1.as<double>(), tp + NX, tp + NX + NY, NZ, 1, jma, kma, Kp, S, 1,
+                               nullptr, PODS_LUND_NONE, nullptr, 0, dy.as<double>(), (int64_t)jma * kma,
+                               c->stream);
+  if (!e) e = hipMemcpyAsync(y, dy.p, (size_t)jma * kma * 8, hipMemcpyDeviceToHost, c->stream);
+  if (!e) e = hipStreamSynchronize(c->stream);
+  cleanup();
+  if (e) return fail(PODS_ERR_HIP, std::string("filter_block: ") + hipGetErrorString(e));
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_rng_uniform(pods_ctx* c, uint32_t seed, int64_t n, double low, double range, double* out) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!out || n <= 0 || n > 0x7fffffffLL) return fail(PODS_ERR_ARG, "bad n/out");
+  PODS_HIP(hipSetDevice(c->device));
+  RngLayout L = make_layout(n);
+  RngBuffers rb;
+  int rc = upload_rng(c, L, seed, rb);
+  if (!rc) rc = run_jumps(c, L, rb);
+  if (!rc) {
+    hipError_t e = pods::launch_mt_generate(rb.states.as<uint32_t>(), L.G, L.Bs, n, n, (int)n, 0, 1, n,
+                                            low, range, out, c->stream);
+    if (!e) e = hipStreamSynchronize(c->stream);
+    if (e) rc = fail(PODS_ERR_HIP, std::string("rng: ") + hipGetErrorString(e));
+  }
+  rb.free_all();
+  return rc;
+  PODS_CATCH
+}
+
+int pods_host_mt_jump_check(uint32_t seed, int64_t nblocks) {
+  PODS_TRY
+  using namespace pods::mt;
+  if (nblocks < 1) return fail(PODS_ERR_ARG, "nblocks >= 1");
+  std::vector<uint32_t> s1(N), ref(N), got(N);
+  seed_state(seed, s1.data());
+  twist(s1.data());  // mt^(1)
+  ref = s1;
+  for (int64_t b = 1; b < nblocks; ++b) twist(ref.data());  // mt^(nblocks)
+  Poly g = powmod_t((uint64_t)N * (uint64_t)(nblocks - 1));
+  apply_poly(g, s1.data(), got.data());
+  if (got != ref) return fail(PODS_ERR_INTERNAL, "jump-ahead mismatch");
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_host_mt_charpoly_degree(void) { return pods::mt::charpoly_degree(); }
+
+}  // extern "C"

@@ -1,0 +1,35 @@
+// Launchers of the gfx950 kernels (podsgen_kernels.hip).  All enqueue on `st`.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace pods {
+
+hipError_t launch_mt_jump(const uint32_t* src, const int* src_idx, const uint32_t* polys,
+                          const int* poly_idx, uint32_t* dst, const int* dst_idx, int njobs,
+                          hipStream_t st);
+hipError_t launch_mt_generate(const uint32_t* states, int G, int64_t Bs, int64_t ntot, int64_t S,
+                              int Kp, int rlo, int rhi, int64_t Sl, double low, double range,
+                              double* out, hipStream_t st);
+hipError_t launch_filter_x(int NX, const double* R, const double* bx, int ns, int64_t Sl, int ncomp,
+                           int chunk, double* T1, hipStream_t st);
+hipError_t launch_filter_yz(int NY, const double* T1, const double* by, const double* bz, int NZ,
+                            int ns, int jl, int K, int Kp, int64_t Sl, int ncomp,
+                            const double* lund, int lund_mode, const double* rot, int rotate,
+                            double* AT, int64_t rowlen, hipStream_t st);
+int filter_yz_max_K(int Kp);
+hipError_t launch_mean(const double* AT, int64_t rowlen, int ns, const int* prog, int nprog,
+                       double* mean, hipStream_t st);
+hipError_t launch_syrk(const double* AT, int64_t ld, int ns, int64_t Kdim, const double* mean,
+                       double* C, int64_t ldc, int divide, hipStream_t st);
+hipError_t launch_divide(double* x, int64_t n, double d, hipStream_t st);
+hipError_t launch_temporal(const double* V, int64_t v_rs, int64_t v_cs, int ns, int ncols,
+                           int nvalid, const double* lam, double* mag, double* T, hipStream_t st);
+hipError_t launch_spatial(const double* AT, int64_t rowlen, int ns, const double* mean,
+                          const double* T, int ldT, int nm, const double* inv_lam, double* phi,
+                          hipStream_t st);
+hipError_t launch_dft(const double* T, int ldT, int nm, int ns, const double* t, double inv_period,
+                      double inv_n, const int* prog, int nprog, float2* c, hipStream_t st);
+
+}  // namespace pods

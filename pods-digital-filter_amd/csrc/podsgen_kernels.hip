@@ -1,0 +1,783 @@
+// gfx950 kernels of the digital-filter + PODFS hot path.
+//
+// Numerics contract (compiled with -ffp-contract=off):
+//   * k_mt_*          reproduce numpy's legacy MT19937 stream bit-for-bit
+//   * k_filter_x/yz   reproduce scipy.signal.convolve(method='direct') x->y->z order and
+//                     the adapt1d / adapt2prf expressions bit-for-bit
+//   * k_mean          reproduces np.mean's pairwise order bit-for-bit
+//   * k_syrk / k_spatial_modes use fp64 FMA (MFMA) -- tolerance-level parity
+//   * k_dft           replicates numpy's complex expression; sin/cos from OCML
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "podsgen_kernels.h"
+
+namespace pods {
+
+// -----------------------------------------------------------------------------------------
+// MT19937
+// -----------------------------------------------------------------------------------------
+static constexpr int MTN = 624;
+static constexpr uint32_t MT_A = 0x9908b0dfu;
+
+__device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c) {
+  const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+  return c ^ (y >> 1) ^ ((y & 1u) ? MT_A : 0u);
+}
+
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// One full twist of an LDS state by a 256-thread workgroup (three dependency phases:
+// [0,227) reads old words, [227,454) and [454,623) read words written one phase earlier).
+__device__ void twist_block256(uint32_t* st) {
+  const int t = threadIdx.x;
+  uint32_t v = 0;
+  if (t < 227) v = mt_mix(st[t], st[t + 1], st[t + 397]);
+  __syncthreads();
+  if (t < 227) st[t] = v;
+  __syncthreads();
+  if (t < 227) v = mt_mix(st[227 + t], st[228 + t], st[t]);
+  __syncthreads();
+  if (t < 227) st[227 + t] = v;
+  __syncthreads();
+  if (t < 169) v = mt_mix(st[454 + t], st[455 + t], st[227 + t]);
+  __syncthreads();
+  if (t < 169) st[454 + t] = v;
+  __syncthreads();
+  if (t == 0) st[623] = mt_mix(st[623], st[0], st[396]);
+  __syncthreads();
+}
+
+// The same twist by one wavefront (64 lanes): read everything of a phase, then write.
+__device__ void twist_wave(uint32_t* st, int lane) {
+  uint32_t v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = lane + 64 * r;
+    if (i < 227) v[r] = mt_mix(st[i], st[i + 1], st[i + 397]);
+  }
+  wave_sync();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = lane + 64 * r;
+    if (i < 227) st[i] = v[r];
+  }
+  wave_sync();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = 227 + lane + 64 * r;
+    if (i < 454) v[r] = mt_mix(st[i], st[i + 1], st[i - 227]);
+  }
+  wave_sync();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = 227 + lane + 64 * r;
+    if (i < 454) st[i] = v[r];
+  }
+  wave_sync();
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const int i = 454 + lane + 64 * r;
+    if (i < 623) v[r] = mt_mix(st[i], st[i + 1], st[i - 227]);
+  }
+  wave_sync();
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const int i = 454 + lane + 64 * r;
+    if (i < 623) st[i] = v[r];
+  }
+  wave_sync();
+  if (lane == 0) st[623] = mt_mix(st[623], st[0], st[396]);
+  wave_sync();
+}
+
+// Jump-ahead: dst = g(F) src by block Horner over 32 blocks of 624 coefficients:
+//   acc <- twist(acc) ^ sum_r c_{624q+r} window_r(x),  x = (src, twist(src)).
+__global__ __launch_bounds__(256) void k_mt_jump(const uint32_t* __restrict__ src_base,
+                                                 const int* __restrict__ src_idx,
+                                                 const uint32_t* __restrict__ polys,
+                                                 const int* __restrict__ poly_idx,
+                                                 uint32_t* __restrict__ dst_base,
+                                                 const int* __restrict__ dst_idx, int njobs) {
+  __shared__ uint32_t x[2 * MTN];
+  __shared__ uint32_t acc[MTN];
+  const int job = blockIdx.x;
+  if (job >= njobs) return;
+  const uint32_t* s = src_base + (size_t)src_idx[job] * MTN;
+  const uint32_t* g = polys + (size_t)poly_idx[job] * MTN;
+  for (int i = threadIdx.x; i < MTN; i += 256) {
+    const uint32_t v = s[i];
+    x[i] = v;
+    x[MTN + i] = v;
+    acc[i] = 0u;
+  }
+  __syncthreads();
+  twist_block256(x + MTN);
+  const int w0 = threadIdx.x, w1 = threadIdx.x + 256, w2 = threadIdx.x + 512;
+  const bool has2 = w2 < MTN;
+  for (int q = 31; q >= 0; --q) {
+    if (q != 31) twist_block256(acc);
+    uint32_t v0 = 0, v1 = 0, v2 = 0;
+    for (int rb = 0; rb < MTN; rb += 32) {
+      const int off = q * MTN + rb;
+      const int wi = off >> 5, sh = off & 31;
+      uint32_t bits = g[wi] >> sh;
+      if (sh && wi + 1 < MTN) bits |= g[wi + 1] << (32 - sh);
+      if (rb + 32 > MTN) bits &= (1u << (MTN - rb)) - 1u;
+      bits = __builtin_amdgcn_readfirstlane(bits);
+      while (bits) {
+        const int b = __builtin_ctz(bits);
+        bits &= bits - 1u;
+        const int r = rb + b;
+        v0 ^= x[r + w0];
+        v1 ^= x[r + w1];
+        if (has2) v2 ^= x[r + w2];
+      }
+    }
+    acc[w0] ^= v0;
+    acc[w1] ^= v1;
+    if (has2) acc[w2] ^= v2;
+    __syncthreads();
+  }
+  uint32_t* d = dst_base + (size_t)dst_idx[job] * MTN;
+  for (int i = threadIdx.x; i < MTN; i += 256) d[i] = acc[i];
+}
+
+// Substream generator: one wavefront per substream g, Bs blocks of 624 words from state
+// mt^(g*Bs).  Double D of the stream (2 words) -> uniform(low, low+range), written to the
+// slab buffer when its padded row lies in [rlo, rhi) of its plane.
+__global__ __launch_bounds__(256) void k_mt_generate(const uint32_t* __restrict__ states, int G,
+                                                     int64_t Bs, int64_t ntot, int64_t S, int Kp,
+                                                     int rlo, int rhi, int64_t Sl, double low,
+                                                     double range, double* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t mts[4][MTN];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = blockIdx.x * 4 + wave;
+  if (g >= G) return;
+  uint32_t* mt = mts[wave];
+  const uint32_t* src = states + (size_t)g * MTN;
+  for (int i = lane; i < MTN; i += 64) mt[i] = src[i];
+  wave_sync();
+  const int64_t D0 = (int64_t)g * Bs * 312;
+  // per-lane position of double D0 + lane within (plane, offset)
+  int64_t q = (D0 + lane) / S;
+  int64_t o = (D0 + lane) - q * S;
+  for (int64_t b = 0; b < Bs; ++b) {
+    const int64_t Db = D0 + b * 312;
+    if (Db >= ntot) break;
+    twist_wave(mt, lane);
+    int64_t qq = q, oo = o;
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const int d = lane + 64 * r;
+      if (d < 312 && Db + d < ntot) {
+        const uint2 w = reinterpret_cast<const uint2*>(mt)[d];
+        const uint32_t a = mt_temper(w.x) >> 5, bb = mt_temper(w.y) >> 6;
+        const double u = ((double)a * 67108864.0 + (double)bb) / 9007199254740992.0;
+        const double val = low + range * u;
+        const int row = (int)(oo / Kp);
+        if (row >= rlo && row < rhi) {
+          const int col = (int)(oo - (int64_t)row * Kp);
+          out[qq * Sl + (int64_t)(row - rlo) * Kp + col] = val;
+        }
+      }
+      oo += 64;
+      while (oo >= S) {
+        oo -= S;
+        ++qq;
+      }
+    }
+    wave_sync();
+    o += 312;
+    while (o >= S) {
+      o -= S;
+      ++q;
+    }
+  }
+}
+
+// -----------------------------------------------------------------------------------------
+// separable filter
+// -----------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t stream_plane(int c, int p, int NX) {
+  return p < NX ? (int64_t)c * NX + p : (int64_t)3 * NX + 3 * (int64_t)(p - NX) + c;
+}
+
+// x pass: t1[c][i][pt] = sum_a x[c][plane i+a][pt] * bx[NX-1-a], a ascending, acc from 0.
+// One thread per (component, padded slab point), sliding register window over the steps.
+template <int NX>
+__global__ __launch_bounds__(256) void k_filter_x(const double* __restrict__ R,
+                                                  const double* __restrict__ bx, int ns,
+                                                  int64_t Sl, int steps_per_chunk,
+                                                  double* __restrict__ T1) {
+  const int64_t pt = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c = blockIdx.y;
+  if (pt >= Sl) return;
+  const int i0 = blockIdx.z * steps_per_chunk;
+  const int i1 = min(ns, i0 + steps_per_chunk);
+  if (i0 >= i1) return;
+  double b[NX];
+#pragma unroll
+  for (int a = 0; a < NX; ++a) b[a] = bx[NX - 1 - a];
+  double w[NX];
+#pragma unroll
+  for (int a = 0; a < NX - 1; ++a) w[a] = R[stream_plane(c, i0 + a, NX) * Sl + pt];
+  for (int i = i0; i < i1; ++i) {
+    w[NX - 1] = R[stream_plane(c, i + NX - 1, NX) * Sl + pt];
+    double acc = 0.0;
+#pragma unroll
+    for (int a = 0; a < NX; ++a) acc = acc + w[a] * b[a];
+    T1[((int64_t)c * ns + i) * Sl + pt] = acc;
+#pragma unroll
+    for (int a = 0; a < NX - 1; ++a) w[a] = w[a + 1];
+  }
+}
+
+// y + z passes, Lund transform, rotation, snapshot store.
+// Block = (row tile of TJ output rows, step i).  y pass streams the TJ+NY-1 padded rows of
+// one column through registers (t2 order b ascending), z pass reads t2 from LDS.
+template <int TJ, int NY>
+__global__ __launch_bounds__(512) void k_filter_yz(
+    const double* __restrict__ T1, const double* __restrict__ by, const double* __restrict__ bz,
+    int NZ, int ns, int jl, int K, int Kp, int64_t Sl, int ncomp,
+    const double* __restrict__ lund, int lund_mode, const double* __restrict__ rot, int rotate,
+    double* __restrict__ AT, int64_t rowlen) {
+  extern __shared__ __attribute__((aligned(16))) double t2[];  // TJ x Kp
+  constexpr int MAXO = 8;
+  const int jt = blockIdx.x * TJ;
+  const int i = blockIdx.y;
+  const int nthr = blockDim.x;
+  const int tid = threadIdx.x;
+  const int rows = min(TJ, jl - jt);
+  const int64_t Pl = (int64_t)jl * K;
+  double byr[NY];
+#pragma unroll
+  for (int b = 0; b < NY; ++b) byr[b] = by[NY - 1 - b];
+  double res[3][MAXO];
+  for (int c = 0; c < ncomp; ++c) {
+    const double* src = T1 + ((int64_t)c * ns + i) * Sl + (int64_t)jt * Kp;
+    for (int col = tid; col < Kp; col += nthr) {
+      double acc[TJ];
+#pragma unroll
+      for (int jj = 0; jj < TJ; ++jj) acc[jj] = 0.0;
+#pragma unroll
+      for (int r = 0; r < TJ + NY - 1; ++r) {
+        if (r < rows + NY - 1) {
+          const double v = src[(int64_t)r * Kp + col];
+#pragma unroll
+          for (int jj = 0; jj < TJ; ++jj) {
+            const int b = r - jj;
+            if (b >= 0 && b < NY) acc[jj] = acc[jj] + v * byr[b];
+          }
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < TJ; ++jj)
+        if (jj < rows) t2[jj * Kp + col] = acc[jj];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < MAXO; ++m) {
+      const int o = tid + m * nthr;
+      const int jj = o / K, k = o - jj * K;
+      double acc = 0.0;
+      if (jj < rows) {
+        const double* rowp = t2 + jj * Kp + k;
+        for (int cc = 0; cc < NZ; ++cc) acc = acc + rowp[cc] * bz[NZ - 1 - cc];
+      }
+      res[c][m] = acc;
+    }
+    __syncthreads();
+  }
+  double R9[9];
+  if (rotate) {
+#pragma unroll
+    for (int e = 0; e < 9; ++e) R9[e] = rot[e];
+  }
+  double* dst = AT + (int64_t)i * rowlen;
+#pragma unroll
+  for (int m = 0; m < MAXO; ++m) {
+    const int o = tid + m * nthr;
+    const int jj = o / K, k = o - jj * K;
+    if (jj >= rows) continue;
+    const int64_t p = (int64_t)(jt + jj) * K + k;
+    if (lund_mode < 0) {
+      for (int c = 0; c < ncomp; ++c) dst[c * Pl + p] = res[c][m];
+      continue;
+    }
+    const double xu = res[0][m], xv = res[1][m], xw = res[2][m];
+    const double a00 = lund[0 * Pl + p], a10 = lund[1 * Pl + p], a11 = lund[2 * Pl + p];
+    const double a20 = lund[3 * Pl + p], a21 = lund[4 * Pl + p], a22 = lund[5 * Pl + p];
+    // digitalfilters.py:174-176 (adapt1d) / :227-229 (adapt2prf), left to right, zero terms kept
+    double u = ((a00 * xu + 0.0 * xv) + 0.0 * xw) + lund[6 * Pl + p];
+    double v = (a10 * xu + a11 * xv) + 0.0 * xw;
+    double w = (a20 * xu + a21 * xv) + a22 * xw;
+    if (lund_mode == 1) {
+      v = v + lund[7 * Pl + p];
+      w = w + lund[8 * Pl + p];
+    }
+    if (rotate) {  // rotate_velocity :1119-1131 (R.dot(V))
+      const double ur = (R9[0] * u + R9[1] * v) + R9[2] * w;
+      const double vr = (R9[3] * u + R9[4] * v) + R9[5] * w;
+      const double wr = (R9[6] * u + R9[7] * v) + R9[8] * w;
+      u = ur;
+      v = vr;
+      w = wr;
+    }
+    dst[p] = u;
+    dst[Pl + p] = v;
+    dst[2 * Pl + p] = w;
+  }
+}
+
+// -----------------------------------------------------------------------------------------
+// mean over snapshots: numpy pairwise program (leaf = (start,len), add = (-1, 0))
+// -----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_mean(const double* __restrict__ AT, int64_t rowlen,
+                                              int ns, const int* __restrict__ prog, int nprog,
+                                              double* __restrict__ mean) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= rowlen) return;
+  double stk[40];
+  int sp = 0;
+  for (int op = 0; op < nprog; ++op) {
+    const int s = prog[2 * op], n = prog[2 * op + 1];
+    if (s < 0) {
+      const double bsum = stk[--sp];
+      stk[sp - 1] = stk[sp - 1] + bsum;
+      continue;
+    }
+    const double* a = AT + (int64_t)s * rowlen + r;
+    double res;
+    if (n < 8) {
+      res = 0.0;
+      for (int i = 0; i < n; ++i) res = res + a[(int64_t)i * rowlen];
+    } else {
+      double r0 = a[0], r1 = a[rowlen], r2 = a[2 * rowlen], r3 = a[3 * rowlen];
+      double r4 = a[4 * rowlen], r5 = a[5 * rowlen], r6 = a[6 * rowlen], r7 = a[7 * rowlen];
+      int i = 8;
+      for (; i < n - (n % 8); i += 8) {
+        const double* b = a + (int64_t)i * rowlen;
+        r0 = r0 + b[0];
+        r1 = r1 + b[rowlen];
+        r2 = r2 + b[2 * rowlen];
+        r3 = r3 + b[3 * rowlen];
+        r4 = r4 + b[4 * rowlen];
+        r5 = r5 + b[5 * rowlen];
+        r6 = r6 + b[6 * rowlen];
+        r7 = r7 + b[7 * rowlen];
+      }
+      res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+      for (; i < n; ++i) res = res + a[(int64_t)i * rowlen];
+    }
+    stk[sp++] = res;
+  }
+  mean[r] = (0.0 + stk[0]) / (double)ns;
+}
+
+// -----------------------------------------------------------------------------------------
+// correlation SYRK on fp64 MFMA (v_mfma_f64_16x16x4_f64)
+// C[i][j] = sum_r (A_T[i][r]-m[r]) (A_T[j][r]-m[r]), lower-triangle tiles, mirrored.
+// -----------------------------------------------------------------------------------------
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+template <int BT, int KT>
+__global__ __launch_bounds__(256) void k_syrk(const double* __restrict__ AT, int64_t ld, int ns,
+                                              int64_t Kdim, const double* __restrict__ mean,
+                                              int nb, double* __restrict__ C, int64_t ldc,
+                                              int divide) {
+  // BT x BT output tile; 4 waves as 2x2, each wave (BT/2)x(BT/2) = MB x MB 16x16 blocks
+  constexpr int MB = BT / 32;
+  __shared__ double Xs[BT][KT + 1];
+  __shared__ double Ys[BT][KT + 1];
+  // lower-triangle tile id -> (bi, bj), bi >= bj
+  const int t = blockIdx.x;
+  int bi = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+  while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
+  while (bi * (bi + 1) / 2 > t) --bi;
+  const int bj = t - bi * (bi + 1) / 2;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int i0 = bi * BT, j0 = bj * BT;
+  f64x4 acc[MB][MB];
+#pragma unroll
+  for (int m = 0; m < MB; ++m)
+#pragma unroll
+    for (int n = 0; n < MB; ++n) acc[m][n] = (f64x4){0.0, 0.0, 0.0, 0.0};
+  constexpr int ELEMS = BT * KT / 256;  // per thread per operand
+  for (int64_t k0 = 0; k0 < Kdim; k0 += KT) {
+#pragma unroll
+    for (int e = 0; e < ELEMS; ++e) {
+      const int idx = tid + e * 256;
+      const int row = idx / KT, kk = idx % KT;
+      const int64_t k = k0 + kk;
+      double xv = 0.0, yv = 0.0;
+      if (k < Kdim) {
+        const double mk = mean[k];
+        if (i0 + row < ns) xv = AT[(int64_t)(i0 + row) * ld + k] - mk;
+        if (j0 + row < ns) yv = AT[(int64_t)(j0 + row) * ld + k] - mk;
+      }
+      Xs[row][kk] = xv;
+      Ys[row][kk] = yv;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < KT; kk += 4) {
+      double a[MB], b[MB];
+#pragma unroll
+      for (int m = 0; m < MB; ++m) a[m] = Xs[wr * (BT / 2) + m * 16 + (lane & 15)][kk + (lane >> 4)];
+#pragma unroll
+      for (int n = 0; n < MB; ++n) b[n] = Ys[wc * (BT / 2) + n * 16 + (lane & 15)][kk + (lane >> 4)];
+#pragma unroll
+      for (int m = 0; m < MB; ++m)
+#pragma unroll
+        for (int n = 0; n < MB; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b[n], acc[m][n], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  const double dn = (double)ns;
+#pragma unroll
+  for (int m = 0; m < MB; ++m)
+#pragma unroll
+    for (int n = 0; n < MB; ++n)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int gi = i0 + wr * (BT / 2) + m * 16 + (lane >> 4) + 4 * reg;
+        const int gj = j0 + wc * (BT / 2) + n * 16 + (lane & 15);
+        if (gi < ns && gj < ns) {
+          double v = acc[m][n][reg];
+          if (divide) v = v / dn;
+          C[(int64_t)gi * ldc + gj] = v;
+          if (bi != bj) C[(int64_t)gj * ldc + gi] = v;
+        }
+      }
+}
+
+__global__ void k_divide(double* __restrict__ x, int64_t n, double d) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = x[i] / d;
+}
+
+// -----------------------------------------------------------------------------------------
+// temporal modes: descending reorder + PODFS.py:1323-1325 scaling
+// -----------------------------------------------------------------------------------------
+__global__ void k_temporal_mag(const double* __restrict__ V, int64_t v_rs, int64_t v_cs, int ns,
+                               int ncols, double* __restrict__ mag) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= ncols) return;
+  const double* col = V + (int64_t)(ns - 1 - j) * v_cs;
+  double s = 0.0;
+  for (int i = 0; i < ns; ++i) {
+    const double x = col[(int64_t)i * v_rs];
+    s = s + x * x;
+  }
+  mag[j] = s / (double)ns;
+}
+
+__global__ void k_temporal_scale(const double* __restrict__ V, int64_t v_rs, int64_t v_cs, int ns,
+                                 int ncols, int nvalid, const double* __restrict__ lam,
+                                 const double* __restrict__ mag, double* __restrict__ T) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = blockIdx.y;
+  if (j >= ncols) return;
+  double x = V[(int64_t)i * v_rs + (int64_t)(ns - 1 - j) * v_cs];
+  if (j < nvalid) x = x * sqrt(lam[j] / mag[j]);
+  T[(int64_t)i * ncols + j] = x;
+}
+
+// -----------------------------------------------------------------------------------------
+// spatial modes Phi[r][m] = ((sum_i (A_T[i][r]-m_r) T[i][m]) * (1/lambda_m)) / ns
+// -----------------------------------------------------------------------------------------
+template <int NMB>
+__global__ __launch_bounds__(256) void k_spatial_modes(const double* __restrict__ AT, int64_t rowlen,
+                                                       int ns, const double* __restrict__ mean,
+                                                       const double* __restrict__ T, int ldT, int col0,
+                                                       int nm, const double* __restrict__ inv_lam,
+                                                       double* __restrict__ phi, int ldphi) {
+  constexpr int CH = 128;
+  __shared__ __attribute__((aligned(16))) double Ts[CH][NMB];
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool valid = r < rowlen;
+  const double mr = valid ? mean[r] : 0.0;
+  double acc[NMB];
+#pragma unroll
+  for (int m = 0; m < NMB; ++m) acc[m] = 0.0;
+  for (int i0 = 0; i0 < ns; i0 += CH) {
+    for (int e = threadIdx.x; e < CH * NMB; e += 256) {
+      const int ii = e / NMB, m = e % NMB;
+      Ts[ii][m] = (i0 + ii < ns && m < nm) ? T[(int64_t)(i0 + ii) * ldT + col0 + m] : 0.0;
+    }
+    __syncthreads();
+    if (valid) {
+      const int lim = min(CH, ns - i0);
+      for (int ii = 0; ii < lim; ++ii) {
+        const double a = AT[(int64_t)(i0 + ii) * rowlen + r] - mr;
+#pragma unroll
+        for (int m = 0; m < NMB; ++m) acc[m] = __builtin_fma(a, Ts[ii][m], acc[m]);
+      }
+    }
+    __syncthreads();
+  }
+  if (!valid) return;
+  const double dn = (double)ns;
+#pragma unroll
+  for (int m = 0; m < NMB; ++m)
+    if (m < nm) phi[r * ldphi + col0 + m] = (acc[m] * inv_lam[col0 + m]) / dn;
+}
+
+// -----------------------------------------------------------------------------------------
+// shifted direct DFT (PODFS.py:1562-1571) with numpy's complex pairwise summation
+// job j < nk: k = j (k >= 0), writes n = h+k and the exact conjugate at n = h-k;
+// job j == nk (even ns): k = -ns/2 (n = 0).
+// -----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_dft(const double* __restrict__ T, int ldT, int nm, int ns,
+                                             const double* __restrict__ t, double inv_period,
+                                             double inv_n, const int* __restrict__ prog, int nprog,
+                                             int nk, int njobs, float2* __restrict__ cout) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int mode = gid % nm;
+  const int job = gid / nm;
+  if (job >= njobs) return;
+  const int h = ns / 2;
+  const int k = (job < nk) ? job : -h;
+  const double zi = (-2.0 * (double)k) * 3.141592653589793;
+  const double* y = T + mode;
+  double sr_stk[24], si_stk[24];
+  int sp = 0;
+  for (int op = 0; op < nprog; ++op) {
+    const int s = prog[2 * op], n = prog[2 * op + 1];
+    if (s < 0) {
+      const double br = sr_stk[--sp], bi = si_stk[sp];
+      sr_stk[sp - 1] = sr_stk[sp - 1] + br;
+      si_stk[sp - 1] = si_stk[sp - 1] + bi;
+      continue;
+    }
+    double rr, ri;
+    if (n < 4) {
+      rr = -0.0;
+      ri = -0.0;
+      for (int m = s; m < s + n; ++m) {
+        double sv, cv;
+        sincos((zi * t[m]) * inv_period, &sv, &cv);
+        const double yv = y[(int64_t)m * ldT];
+        rr = rr + (yv * cv - 0.0 * sv);
+        ri = ri + (yv * sv + 0.0 * cv);
+      }
+    } else {
+      double r[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        double sv, cv;
+        const int m = s + e;
+        sincos((zi * t[m]) * inv_period, &sv, &cv);
+        const double yv = y[(int64_t)m * ldT];
+        r[2 * e] = yv * cv - 0.0 * sv;
+        r[2 * e + 1] = yv * sv + 0.0 * cv;
+      }
+      int i = 4;
+      for (; i < n - (n % 4); i += 4) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          double sv, cv;
+          const int m = s + i + e;
+          sincos((zi * t[m]) * inv_period, &sv, &cv);
+          const double yv = y[(int64_t)m * ldT];
+          r[2 * e] = r[2 * e] + (yv * cv - 0.0 * sv);
+          r[2 * e + 1] = r[2 * e + 1] + (yv * sv + 0.0 * cv);
+        }
+      }
+      rr = (r[0] + r[2]) + (r[4] + r[6]);
+      ri = (r[1] + r[3]) + (r[5] + r[7]);
+      for (; i < n; ++i) {
+        double sv, cv;
+        const int m = s + i;
+        sincos((zi * t[m]) * inv_period, &sv, &cv);
+        const double yv = y[(int64_t)m * ldT];
+        rr = rr + (yv * cv - 0.0 * sv);
+        ri = ri + (yv * sv + 0.0 * cv);
+      }
+    }
+    sr_stk[sp] = rr;
+    si_stk[sp] = ri;
+    ++sp;
+  }
+  const double cr = (0.0 + sr_stk[0]) * inv_n;
+  const double ci = (0.0 + si_stk[0]) * inv_n;
+  const float2 val = make_float2((float)cr, (float)ci);
+  if (job < nk) {
+    cout[(int64_t)(h + k) * nm + mode] = val;
+    if (k > 0 && h - k >= 0) cout[(int64_t)(h - k) * nm + mode] = make_float2(val.x, -val.y);
+  } else {
+    cout[mode] = val;  // n = 0, k = -ns/2
+  }
+}
+
+// -----------------------------------------------------------------------------------------
+// launchers
+// -----------------------------------------------------------------------------------------
+hipError_t launch_mt_jump(const uint32_t* src, const int* src_idx, const uint32_t* polys,
+                          const int* poly_idx, uint32_t* dst, const int* dst_idx, int njobs,
+                          hipStream_t st) {
+  if (njobs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_mt_jump, dim3(njobs), dim3(256), 0, st, src, src_idx, polys, poly_idx, dst,
+                     dst_idx, njobs);
+  return hipGetLastError();
+}
+
+hipError_t launch_mt_generate(const uint32_t* states, int G, int64_t Bs, int64_t ntot, int64_t S,
+                              int Kp, int rlo, int rhi, int64_t Sl, double low, double range,
+                              double* out, hipStream_t st) {
+  if (G <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_mt_generate, dim3((G + 3) / 4), dim3(256), 0, st, states, G, Bs, ntot, S, Kp,
+                     rlo, rhi, Sl, low, range, out);
+  return hipGetLastError();
+}
+
+template <int NX>
+static hipError_t launch_fx(const double* R, const double* bx, int ns, int64_t Sl, int ncomp,
+                            int chunk, double* T1, hipStream_t st) {
+  const int nch = (ns + chunk - 1) / chunk;
+  dim3 grid((unsigned)((Sl + 255) / 256), (unsigned)ncomp, (unsigned)nch);
+  hipLaunchKernelGGL(k_filter_x<NX>, grid, dim3(256), 0, st, R, bx, ns, Sl, chunk, T1);
+  return hipGetLastError();
+}
+
+hipError_t launch_filter_x(int NX, const double* R, const double* bx, int ns, int64_t Sl, int ncomp,
+                           int chunk, double* T1, hipStream_t st) {
+  switch (NX) {
+#define PODS_FX(n) \
+  case n:          \
+    return launch_fx<n>(R, bx, ns, Sl, ncomp, chunk, T1, st);
+    PODS_FX(1) PODS_FX(3) PODS_FX(5) PODS_FX(7) PODS_FX(9) PODS_FX(11) PODS_FX(13) PODS_FX(15)
+    PODS_FX(17) PODS_FX(19) PODS_FX(21) PODS_FX(23) PODS_FX(25) PODS_FX(27) PODS_FX(29)
+    PODS_FX(31) PODS_FX(33) PODS_FX(35) PODS_FX(37) PODS_FX(39) PODS_FX(41) PODS_FX(43)
+    PODS_FX(45) PODS_FX(47) PODS_FX(49)
+#undef PODS_FX
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+static constexpr int YZ_TJ = 8;
+
+template <int NY>
+static hipError_t launch_fyz(const double* T1, const double* by, const double* bz, int NZ, int ns,
+                             int jl, int K, int Kp, int64_t Sl, int ncomp, const double* lund,
+                             int lund_mode, const double* rot, int rotate, double* AT,
+                             int64_t rowlen, hipStream_t st) {
+  int nthr = ((Kp + 63) / 64) * 64;
+  if (nthr > 512) nthr = 512;
+  // MAXO = 8 outputs per thread per component
+  if ((int64_t)YZ_TJ * K > (int64_t)8 * nthr) return hipErrorInvalidConfiguration;
+  dim3 grid((unsigned)((jl + YZ_TJ - 1) / YZ_TJ), (unsigned)ns);
+  const size_t lds = (size_t)YZ_TJ * Kp * sizeof(double);
+  hipLaunchKernelGGL((k_filter_yz<YZ_TJ, NY>), grid, dim3(nthr), lds, st, T1, by, bz, NZ, ns, jl, K,
+                     Kp, Sl, ncomp, lund, lund_mode, rot, rotate, AT, rowlen);
+  return hipGetLastError();
+}
+
+hipError_t launch_filter_yz(int NY, const double* T1, const double* by, const double* bz, int NZ,
+                            int ns, int jl, int K, int Kp, int64_t Sl, int ncomp,
+                            const double* lund, int lund_mode, const double* rot, int rotate,
+                            double* AT, int64_t rowlen, hipStream_t st) {
+  switch (NY) {
+#define PODS_FYZ(n) \
+  case n:           \
+    return launch_fyz<n>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_mode, rot, rotate, AT, rowlen, st);
+    PODS_FYZ(1) PODS_FYZ(3) PODS_FYZ(5) PODS_FYZ(7) PODS_FYZ(9) PODS_FYZ(11) PODS_FYZ(13)
+    PODS_FYZ(15) PODS_FYZ(17) PODS_FYZ(19) PODS_FYZ(21) PODS_FYZ(23) PODS_FYZ(25)
+#undef PODS_FYZ
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+int filter_yz_max_K(int Kp) {
+  int nthr = ((Kp + 63) / 64) * 64;
+  if (nthr > 512) nthr = 512;
+  return 8 * nthr / YZ_TJ;
+}
+
+hipError_t launch_mean(const double* AT, int64_t rowlen, int ns, const int* prog, int nprog,
+                       double* mean, hipStream_t st) {
+  hipLaunchKernelGGL(k_mean, dim3((unsigned)((rowlen + 255) / 256)), dim3(256), 0, st, AT, rowlen, ns,
+                     prog, nprog, mean);
+  return hipGetLastError();
+}
+
+hipError_t launch_syrk(const double* AT, int64_t ld, int ns, int64_t Kdim, const double* mean,
+                       double* C, int64_t ldc, int divide, hipStream_t st) {
+  constexpr int BT = 64, KT = 16;
+  const int nb = (ns + BT - 1) / BT;
+  const int tiles = nb * (nb + 1) / 2;
+  hipLaunchKernelGGL((k_syrk<BT, KT>), dim3(tiles), dim3(256), 0, st, AT, ld, ns, Kdim, mean, nb, C,
+                     ldc, divide);
+  return hipGetLastError();
+}
+
+hipError_t launch_divide(double* x, int64_t n, double d, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_divide, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, n, d);
+  return hipGetLastError();
+}
+
+hipError_t launch_temporal(const double* V, int64_t v_rs, int64_t v_cs, int ns, int ncols,
+                           int nvalid, const double* lam, double* mag, double* T, hipStream_t st) {
+  hipLaunchKernelGGL(k_temporal_mag, dim3((ncols + 63) / 64), dim3(64), 0, st, V, v_rs, v_cs, ns,
+                     ncols, mag);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_temporal_scale, dim3((ncols + 255) / 256, ns), dim3(256), 0, st, V, v_rs, v_cs,
+                     ns, ncols, nvalid, lam, mag, T);
+  return hipGetLastError();
+}
+
+hipError_t launch_spatial(const double* AT, int64_t rowlen, int ns, const double* mean,
+                          const double* T, int ldT, int nm, const double* inv_lam, double* phi,
+                          hipStream_t st) {
+  const dim3 grid((unsigned)((rowlen + 255) / 256));
+  for (int col0 = 0; col0 < nm; col0 += 32) {
+    const int nb = nm - col0 < 32 ? nm - col0 : 32;
+    if (nb <= 8)
+      hipLaunchKernelGGL(k_spatial_modes<8>, grid, dim3(256), 0, st, AT, rowlen, ns, mean, T, ldT, col0,
+                         nb, inv_lam, phi, nm);
+    else if (nb <= 16)
+      hipLaunchKernelGGL(k_spatial_modes<16>, grid, dim3(256), 0, st, AT, rowlen, ns, mean, T, ldT, col0,
+                         nb, inv_lam, phi, nm);
+    else if (nb <= 20)
+      hipLaunchKernelGGL(k_spatial_modes<20>, grid, dim3(256), 0, st, AT, rowlen, ns, mean, T, ldT, col0,
+                         nb, inv_lam, phi, nm);
+    else
+      hipLaunchKernelGGL(k_spatial_modes<32>, grid, dim3(256), 0, st, AT, rowlen, ns, mean, T, ldT, col0,
+                         nb, inv_lam, phi, nm);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_dft(const double* T, int ldT, int nm, int ns, const double* t, double inv_period,
+                      double inv_n, const int* prog, int nprog, float2* c, hipStream_t st) {
+  const int h = ns / 2;
+  const int nk = (ns % 2 == 0) ? h : h + 1;  // k = 0..nk-1
+  const int njobs = nk + ((ns % 2 == 0) ? 1 : 0);
+  const int64_t total = (int64_t)njobs * nm;
+  hipLaunchKernelGGL(k_dft, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, T, ldT, nm, ns, t,
+                     inv_period, inv_n, prog, nprog, nk, njobs, c);
+  return hipGetLastError();
+}
+
+}  // namespace pods

@@ -1,0 +1,101 @@
+"""ctypes binding of libpodsgen.so (C ABI declared in include/podsgen.h).
+
+The library is the product: there is no CPU fallback.  If the shared object is missing
+or a call fails, a RuntimeError carrying pods_last_error() is raised.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PODSGEN_LIB", os.path.join(_HERE, "libpodsgen.so"))
+
+PODS_OK = 0
+PODS_LUND_1D = 0
+PODS_LUND_PRF = 1
+PODS_LUND_NONE = -1
+
+c_int = ctypes.c_int
+c_i64 = ctypes.c_int64
+c_u32 = ctypes.c_uint32
+c_dbl = ctypes.c_double
+c_void_p = ctypes.c_void_p
+P_dbl = ctypes.POINTER(ctypes.c_double)
+
+
+class DFParams(ctypes.Structure):
+    """pods_df_params (include/podsgen.h)."""
+    _fields_ = [("jma", ctypes.c_int32), ("kma", ctypes.c_int32), ("ns", ctypes.c_int32),
+                ("nfx", ctypes.c_int32), ("nfy", ctypes.c_int32), ("nfz", ctypes.c_int32),
+                ("j0", ctypes.c_int32), ("j1", ctypes.c_int32), ("lund_mode", ctypes.c_int32),
+                ("rotate", ctypes.c_int32), ("seed", ctypes.c_uint32), ("reserved", ctypes.c_int32),
+                ("rng_low", ctypes.c_double), ("rng_range", ctypes.c_double)]
+
+
+# name -> (restype, argtypes); every entry point of include/podsgen.h
+SIGNATURES = {
+    "pods_last_error": (ctypes.c_char_p, []),
+    "pods_abi_version": (c_int, []),
+    "pods_create": (c_int, [ctypes.POINTER(c_void_p), c_int]),
+    "pods_destroy": (c_int, [c_void_p]),
+    "pods_set_stream": (c_int, [c_void_p, c_void_p]),
+    "pods_synchronize": (c_int, [c_void_p]),
+    "pods_df_configure": (c_int, [c_void_p, ctypes.POINTER(DFParams), c_void_p, c_void_p, c_void_p,
+                                  c_void_p, c_void_p]),
+    "pods_df_generate": (c_int, [c_void_p]),
+    "pods_df_snapshots": (c_int, [c_void_p, ctypes.POINTER(c_void_p), ctypes.POINTER(c_i64)]),
+    "pods_set_snapshots": (c_int, [c_void_p, c_void_p, c_int, c_i64]),
+    "pods_copy": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_size_t, c_int]),
+    "pods_mean": (c_int, [c_void_p, c_void_p, c_int]),
+    "pods_corr": (c_int, [c_void_p, c_void_p, c_int]),
+    "pods_divide_inplace": (c_int, [c_void_p, c_void_p, c_i64, c_dbl]),
+    "pods_temporal_modes": (c_int, [c_void_p, c_void_p, c_i64, c_i64, c_void_p, c_int, c_int, c_void_p]),
+    "pods_spatial_modes": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
+    "pods_fourier": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_dbl, c_void_p]),
+    "pods_filter_block": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                                  c_void_p, c_void_p, c_void_p]),
+    "pods_rng_uniform": (c_int, [c_void_p, c_u32, c_i64, c_dbl, c_dbl, c_void_p]),
+    "pods_host_mt_jump_check": (c_int, [c_u32, c_i64]),
+    "pods_host_mt_charpoly_degree": (c_int, []),
+}
+
+_lib = None
+
+
+def load():
+    """Load libpodsgen.so once; raise loudly if it is missing (no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("libpodsgen.so not found at %s -- build it with "
+                           "`python -c 'import __graft_entry__ as g; g.build()'` or "
+                           "`make -C pods-digital-filter_amd/csrc`" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.pods_abi_version() != 1:
+        raise RuntimeError("libpodsgen ABI mismatch")
+    _lib = lib
+    return lib
+
+
+def check(rc, what=""):
+    if rc != PODS_OK:
+        msg = load().pods_last_error()
+        raise RuntimeError("%s failed (%d): %s" % (what or "podsgen call", rc,
+                                                    msg.decode() if msg else "?"))
+
+
+def ptr(a):
+    """Address of a numpy array / torch tensor / int, as c_void_p."""
+    if a is None:
+        return None
+    if isinstance(a, int):
+        return c_void_p(a)
+    if hasattr(a, "data_ptr"):
+        return c_void_p(a.data_ptr())
+    if hasattr(a, "ctypes"):
+        return c_void_p(a.ctypes.data)
+    raise TypeError(type(a))

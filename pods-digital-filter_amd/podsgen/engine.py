@@ -1,0 +1,313 @@
+"""Device-resident pipeline of the digital-filter + PODFS hot path.
+
+    DFSetup (host, tiny) -> Generator.generate()          RNG + x/y/z filters + Lund + rotation
+                         -> run_pod()                     mean, C = A'^T A'/ns (+ RCCL all-reduce),
+                                                          eigensolve, temporal + spatial modes
+                         -> run_fourier()                 shifted DFT on the GPU, ranking/count on host
+
+Multi-GPU: one process per GPU.  Each rank owns a contiguous slab of inlet rows
+(host.row_slab); its partial correlation is summed with ONE torch.distributed
+all_reduce (RCCL over xGMI with the "nccl" backend).  Rank 0 solves the eigenproblem
+and broadcasts lambda and T[:, :nm]; every rank then forms its slab of the spatial modes.
+
+PyTorch is used for device memory, the stream, torch.distributed and
+torch.linalg.eigh (the POD eigensolve) -- nothing else.
+"""
+import ctypes
+import time
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import DFParams, check, ptr
+from .host import DFSetup, num_valid_modes, rank_and_count, row_slab, time_axis  # noqa: F401
+
+try:
+    import torch
+except Exception:  # pragma: no cover
+    torch = None
+
+
+def _require_gpu():
+    if torch is None or not torch.cuda.is_available():
+        raise RuntimeError("podsgen needs a ROCm GPU (torch.cuda.is_available() is False); "
+                           "there is no CPU fallback")
+
+
+class Context:
+    """One pods_ctx bound to a device and to torch's current stream on it."""
+
+    def __init__(self, device=0):
+        _require_gpu()
+        self.lib = _lib.load()
+        self.device = int(device)
+        torch.cuda.set_device(self.device)
+        self.stream = torch.cuda.current_stream(self.device)
+        h = ctypes.c_void_p()
+        check(self.lib.pods_create(ctypes.byref(h), self.device), "pods_create")
+        self.h = h
+        check(self.lib.pods_set_stream(self.h, ctypes.c_void_p(self.stream.cuda_stream)), "pods_set_stream")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.pods_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class DeviceSnapshots:
+    """Handle on the device snapshot matrix A_T (ns x 3*P_local, snapshot-major).
+    The reference's A is (3P, ns) with rows [u(P); v(P); w(P)] (digitalfilters.py:1397)."""
+    ctx: Context
+    ns: int
+    rowlen: int
+    j0: int = 0
+    j1: int = 0
+    kma: int = 0
+
+    def data_ptr(self):
+        p = ctypes.c_void_p()
+        n = ctypes.c_int64()
+        check(self.ctx.lib.pods_df_snapshots(self.ctx.h, ctypes.byref(p), ctypes.byref(n)), "pods_df_snapshots")
+        return p.value
+
+    def to_host_T(self):
+        """A_T as a host (ns, 3*P_local) array."""
+        out = np.empty((self.ns, self.rowlen), dtype=np.float64)
+        check(self.ctx.lib.pods_copy(self.ctx.h, ptr(out), ctypes.c_void_p(self.data_ptr()),
+                                     out.nbytes, 1), "pods_copy")
+        return out
+
+    def to_host(self):
+        """The reference layout A (3*P_local, ns)."""
+        return np.ascontiguousarray(self.to_host_T().T)
+
+
+class Generator:
+    """digitalfilters.py main() step loop (:1403-1477) on one GPU / row slab."""
+
+    def __init__(self, setup: DFSetup, device=0, rank=0, world=1, ctx: Optional[Context] = None):
+        self.setup = setup
+        self.ctx = ctx or Context(device)
+        self.rank, self.world = rank, world
+        self.j0, self.j1 = row_slab(setup.jma, rank, world)
+        bx, by, bz = setup.taps()
+        rot = setup.rotation()
+        rotate = bool(setup.rotated and not np.array_equal(rot, np.eye(3)))
+        self._keep = [np.ascontiguousarray(bx), np.ascontiguousarray(by), np.ascontiguousarray(bz),
+                      setup.lund_rows(self.j0, self.j1), np.ascontiguousarray(rot, dtype=np.float64)]
+        p = DFParams(jma=setup.jma, kma=setup.kma, ns=setup.ns, nfx=setup.nfx, nfy=setup.nfy,
+                     nfz=setup.nfz, j0=self.j0, j1=self.j1, lund_mode=setup.lund_mode(),
+                     rotate=int(rotate), seed=int(setup.seed) & 0xffffffff, reserved=0,
+                     rng_low=-np.sqrt(3.0), rng_range=np.sqrt(3.0) - (-np.sqrt(3.0)))
+        self.params = p
+        k = self._keep
+        check(self.ctx.lib.pods_df_configure(self.ctx.h, ctypes.byref(p), ptr(k[0]), ptr(k[1]), ptr(k[2]),
+                                             ptr(k[3]), ptr(k[4])), "pods_df_configure")
+        self.rowlen = 3 * (self.j1 - self.j0) * setup.kma
+
+    def generate(self):
+        check(self.ctx.lib.pods_df_generate(self.ctx.h), "pods_df_generate")
+        return self.snapshots()
+
+    def snapshots(self):
+        return DeviceSnapshots(self.ctx, self.setup.ns, self.rowlen, self.j0, self.j1, self.setup.kma)
+
+
+def load_snapshots(A, ctx: Optional[Context] = None, device=0):
+    """Upload a reference-layout host A (3P, ns) for PODFS.POD(A, ...)."""
+    ctx = ctx or Context(device)
+    A = np.asarray(A, dtype=np.float64)
+    AT = np.ascontiguousarray(A.T)
+    check(ctx.lib.pods_set_snapshots(ctx.h, ptr(AT), AT.shape[0], AT.shape[1]), "pods_set_snapshots")
+    return DeviceSnapshots(ctx, AT.shape[0], AT.shape[1])
+
+
+@dataclass
+class PODResult:
+    energy: np.ndarray            # all ns eigenvalues, descending (host)
+    num_valid: int
+    nm: int
+    mean: "torch.Tensor"          # (3P_local,)
+    T: Optional["torch.Tensor"]   # (ns, ncols) scaled temporal modes (rank 0; others: T[:, :nm])
+    phi: "torch.Tensor"           # (3P_local, nm) spatial modes
+    C: Optional["torch.Tensor"] = None
+    timings: dict = field(default_factory=dict)
+
+
+def _dist_info(dist):
+    if dist is None or not dist.is_available() or not dist.is_initialized():
+        return None, 0, 1
+    return dist, dist.get_rank(), dist.get_world_size()
+
+
+def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=True,
+            keep_C=False, timer=None):
+    """PODFS.POD (PODFS.py:1294-1393) with correct_for_cell_volumes='false'."""
+    ctx, lib = snap.ctx, snap.ctx.lib
+    ns = snap.ns
+    dist, rank, world = _dist_info(dist)
+    dev = torch.device("cuda", ctx.device)
+    tm = timer or (lambda name: _NullCtx())
+    mean = torch.empty(snap.rowlen, dtype=torch.float64, device=dev)
+    with tm("mean"):
+        check(lib.pods_mean(ctx.h, ptr(mean), 1), "pods_mean")
+    C = torch.empty((ns, ns), dtype=torch.float64, device=dev)
+    with tm("corr"):
+        check(lib.pods_corr(ctx.h, ptr(C), 1 if world == 1 else 0), "pods_corr")
+    if world > 1:
+        with tm("allreduce"):
+            dist.all_reduce(C)
+            check(lib.pods_divide_inplace(ctx.h, ptr(C), ns * ns, float(ns)), "pods_divide_inplace")
+    meta = torch.zeros(4, dtype=torch.int64, device=dev)
+    lam_desc_t = torch.empty(ns, dtype=torch.float64, device=dev)
+    T = None
+    if rank == 0:
+        with tm("eigh"):
+            lam, V = torch.linalg.eigh(C)
+            lam_desc_t.copy_(torch.flip(lam, dims=(0,)))
+            lam_desc = lam_desc_t.cpu().numpy()
+        nvalid = num_valid_modes(lam_desc, ns, tol_CN)
+        nmt = nm if (0 <= nm <= nvalid) else nvalid
+        ncols = ns if full_temporal else max(nmt, 1)
+        T = torch.empty((ns, ncols), dtype=torch.float64, device=dev)
+        with tm("temporal"):
+            check(lib.pods_temporal_modes(ctx.h, ptr(V), V.stride(0), V.stride(1), ptr(lam_desc),
+                                          nvalid, ncols, ptr(T)), "pods_temporal_modes")
+        del V
+        meta[0], meta[1] = nvalid, nmt
+    if world > 1:
+        dist.broadcast(meta, 0)
+        dist.broadcast(lam_desc_t, 0)
+        nvalid, nmt = int(meta[0]), int(meta[1])
+        lam_desc = lam_desc_t.cpu().numpy()
+        Tn = torch.empty((ns, max(nmt, 1)), dtype=torch.float64, device=dev)
+        if rank == 0:
+            Tn.copy_(T[:, :max(nmt, 1)])
+        dist.broadcast(Tn, 0)
+        if rank != 0:
+            T = Tn
+        Tsel, ldT = Tn, Tn.shape[1]
+    else:
+        Tsel, ldT = T, T.shape[1]
+    phi = torch.empty((snap.rowlen, max(nmt, 1)), dtype=torch.float64, device=dev)
+    if nmt > 0:
+        with tm("spatial"):
+            check(lib.pods_spatial_modes(ctx.h, ptr(Tsel), ldT, ptr(np.ascontiguousarray(lam_desc[:nmt])),
+                                         nmt, ptr(phi)), "pods_spatial_modes")
+    return PODResult(energy=lam_desc, num_valid=nvalid, nm=nmt, mean=mean, T=T, phi=phi[:, :nmt],
+                     C=C if keep_C else None)
+
+
+@dataclass
+class FourierResult:
+    c: np.ndarray          # (ns, nm) complex64
+    c_ind: np.ndarray      # (nm, ns) int32
+    c_count: np.ndarray    # (nm,) int64
+    FC: np.ndarray         # (sum c_count, 3) float64
+    period: float
+    time: np.ndarray
+
+
+def host_rank_and_count(c, et):
+    ns, nm = c.shape
+    c_ind = np.zeros((nm, ns), dtype=np.int32)
+    c_count = np.zeros(nm, dtype=np.int64)
+    rows = []
+    for i in range(nm):
+        c_ind[i], c_count[i] = rank_and_count(c[:, i], et)
+        idx = c_ind[i, :c_count[i]]
+        blk = np.empty((len(idx), 3), dtype=np.float64)
+        blk[:, 0] = idx - ns // 2
+        blk[:, 1] = c[idx, i].real
+        blk[:, 2] = c[idx, i].imag
+        rows.append(blk)
+    FC = np.concatenate(rows) if rows else np.zeros((0, 3))
+    return c_ind, c_count, FC
+
+
+def run_fourier(ctx: Context, T, nm, ns, dt, et, timer=None):
+    """fourier_coefficients (PODFS.py:1523-1659): DFT on the GPU, ranking/count on host."""
+    tm = timer or (lambda name: _NullCtx())
+    time_, period = time_axis(ns, dt)
+    dev = torch.device("cuda", ctx.device)
+    nm = int(nm)
+    if nm == 0:
+        return FourierResult(np.zeros((ns, 0), np.complex64), np.zeros((0, ns), np.int32),
+                             np.zeros(0, np.int64), np.zeros((0, 3)), period, time_)
+    cbuf = torch.empty((ns, nm, 2), dtype=torch.float32, device=dev)
+    with tm("dft"):
+        check(ctx.lib.pods_fourier(ctx.h, ptr(T), T.stride(0), nm, ns, ptr(np.ascontiguousarray(time_)),
+                                   float(period), ptr(cbuf)), "pods_fourier")
+    with tm("rank"):
+        c = cbuf.cpu().numpy().view(np.complex64).reshape(ns, nm)
+        c_ind, c_count, FC = host_rank_and_count(c, et)
+    return FourierResult(c=c, c_ind=c_ind, c_count=c_count, FC=FC, period=period, time=time_)
+
+
+class _NullCtx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+class StageTimer:
+    """Per-stage GPU time with HIP events on the pipeline's stream (torch events wrap
+    hipEvent_t on the current stream, which is the stream the kernels run on)."""
+
+    def __init__(self, enabled=True):
+        self.enabled = enabled
+        self.events = []
+
+    def __call__(self, name):
+        timer = self
+
+        class _C:
+            def __enter__(self):
+                if timer.enabled:
+                    self.a = torch.cuda.Event(enable_timing=True)
+                    self.a.record()
+                return self
+
+            def __exit__(self, *exc):
+                if timer.enabled:
+                    b = torch.cuda.Event(enable_timing=True)
+                    b.record()
+                    timer.events.append((name, self.a, b))
+                return False
+        return _C()
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, a, b in self.events:
+            out[name] = out.get(name, 0.0) + a.elapsed_time(b)
+        return out
+
+
+def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=True, timer=None, gen=None):
+    """The whole hot path; returns (Generator, PODResult, FourierResult | None)."""
+    dist_, rank, world = _dist_info(dist)
+    tm = timer or (lambda name: _NullCtx())
+    gen = gen or Generator(setup, device=device, rank=rank, world=world)
+    with tm("generate"):
+        snap = gen.generate()
+    pod = run_pod(snap, setup.nm, dist=dist_, full_temporal=full_temporal, timer=timer)
+    fo = None
+    if rank == 0:
+        fo = run_fourier(gen.ctx, pod.T, pod.nm, setup.ns, setup.dt_eff, setup.et, timer=timer)
+    return gen, pod, fo
+
+
+def wall():
+    return time.perf_counter()

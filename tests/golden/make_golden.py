@@ -1,0 +1,315 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ by RUNNING THE REFERENCE'S OWN CODE.
+
+This script is test infrastructure.  It runs only in the build container (it needs
+/root/reference, which never exists on the GPU box) and its outputs are plain data
+(.npz arrays and the reference's own text output files).  Nothing from the reference
+is copied into the repository: the source text is read at run time, translated in
+memory and discarded.
+
+How the reference is executed
+-----------------------------
+The reference (sidbannet/PODS-digital-filter) is Python 2 and cannot be imported by
+this interpreter (mixed tabs, print statements).  We therefore
+
+  1. read digitalfilters.py / PODFS.py as text and apply Python 2's tab rule
+     (expandtabs(8));
+  2. run lib2to3 over the module text (print/except/zip/... fixers);
+  3. parse the result with `ast` and pull out ONLY the pure numpy/scipy functions on
+     the hot path -- no module-level imports of vtk/h5py/matplotlib are executed, and
+     no stand-ins for those libraries are written;
+  4. apply the Python-2 / numpy-1.x semantic patches listed in SEMANTIC_PATCHES
+     (integer division, np.int, numpy-1.x float32->float64 promotion);
+  5. exec those functions in a namespace holding numpy, scipy.signal and math.
+
+Functions executed from the reference (file:line):
+  digitalfilters.py:73-89    calccoeff
+  digitalfilters.py:100-140  filter3DSciPy1D
+  digitalfilters.py:143-178  adapt1d
+  digitalfilters.py:180-231  adapt2prf
+  digitalfilters.py:1038-1062 build_profile
+  digitalfilters.py:1064-1131 prof_rotation_matrix / rotate_velocity
+  PODFS.py:1409-1427          write_eigenvalues
+  PODFS.py:1430-1447          sort_eigenvalues
+  PODFS.py:1451-1464          calculate_correlation_matrix
+  PODFS.py:1523-1659          fourier_coefficients (writes PODFS/PODFS.dat)
+
+main() (digitalfilters.py:1134-1510) and POD() (PODFS.py:1294-1393) are monolithic and
+reach VTK (make_inflow_plane, write_mean_field2); their glue lines (RNG draws, roll,
+snapshot assembly, mean subtraction, valid-mode count, temporal scaling, spatial modes)
+are replayed below line by line with the same numpy calls, each citing its line.
+
+Run:  python tests/golden/make_golden.py      (writes tests/golden/*.npz, *.dat)
+"""
+import ast
+import io
+import math
+import os
+import shutil
+import sys
+import tempfile
+import warnings
+
+import numpy as np
+import scipy.signal as scSig
+
+REF = os.environ.get("PODS_REFERENCE", "/root/reference")
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+# (function name) -> list of (old, new) text patches, each must apply exactly as listed.
+SEMANTIC_PATCHES = {
+    # Python 2 integer division (PODFS.py:1565,1607,1636,1657)
+    "fourier_coefficients": [
+        ("num_fcs/2", "num_fcs//2"),
+        # numpy-1.x promotion: np.float32 (*|+) python float -> float64 (PODFS.py:1588-1593)
+        ("energy_sum = np.sum(np.abs(c[:,i]))", "energy_sum = np.float64(np.sum(np.abs(c[:,i])))"),
+        ("energy += np.abs(c[c_ind[i,c_count[i]],i])", "energy += np.float64(np.abs(c[c_ind[i,c_count[i]],i]))"),
+    ],
+    # np.int was removed in numpy 1.24 (PODFS.py:1432)
+    "sort_eigenvalues": [("dtype=np.int)", "dtype=int)")],
+    # Python 2 integer division (digitalfilters.py:1121)
+    "rotate_velocity": [("len(A)/3", "len(A)//3")],
+}
+
+DF_FUNCS = ["calccoeff", "filter3DSciPy1D", "adapt1d", "adapt2prf", "build_profile",
+            "prof_rotation_matrix", "rotate_velocity"]
+POD_FUNCS = ["write_eigenvalues", "sort_eigenvalues", "calculate_correlation_matrix",
+             "fourier_coefficients"]
+
+
+def _translate(path):
+    from lib2to3 import refactor
+    with open(path, "r") as f:
+        src = f.read().expandtabs(8)
+    if not src.endswith("\n"):
+        src += "\n"
+    fixers = refactor.get_fixers_from_package("lib2to3.fixes")
+    tool = refactor.RefactoringTool(fixers)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        return str(tool.refactor_string(src, os.path.basename(path)))
+
+
+def _extract(src, names):
+    tree = ast.parse(src)
+    lines = src.splitlines(keepends=True)
+    out = {}
+    for node in tree.body:
+        if isinstance(node, ast.FunctionDef) and node.name in names:
+            out[node.name] = "".join(lines[node.lineno - 1:node.end_lineno])
+    missing = set(names) - set(out)
+    assert not missing, missing
+    return out
+
+
+def load_reference():
+    ns = {"np": np, "scSig": scSig, "math": math, "Pi": np.pi, "linalg": np.linalg}
+    for path, names in ((os.path.join(REF, "digitalfilters.py"), DF_FUNCS),
+                        (os.path.join(REF, "PODFS.py"), POD_FUNCS)):
+        funcs = _extract(_translate(path), names)
+        for name, text in funcs.items():
+            for old, new in SEMANTIC_PATCHES.get(name, []):
+                assert old in text, (name, old)
+                text = text.replace(old, new)
+            exec(compile(text, "<reference:%s>" % name, "exec"), ns)
+    return ns
+
+
+class Obj(object):
+    pass
+
+
+def run_reference_pipeline(ref, *, jma, kma, ns, seed, lengthscale=3.0, fwidth=2.0, dt=0.0,
+                           res=0.1, bulk_velocity=1.0, u_dash=0.02, nm=20, et=0.9,
+                           normal=(1.0, 0.0, 0.0), prf=None, workdir=None):
+    """Replay digitalfilters.py main() (:1244-1510) + PODFS.POD (:1294-1393) with the
+    reference's own functions.  prf=None -> built profile (adapt1d + rotation);
+    prf=dict(U,V,W,uu,vv,ww,uv,uw,vw) of (jma,kma) arrays -> adapt2prf path (no rotation)."""
+    out = {}
+    np.random.seed(seed)                                  # extension: reference never seeds
+    lnx = lny = lnz = lengthscale                         # :1262-1264
+    nf = int(math.ceil(fwidth * lengthscale))             # :1267
+    nfx = nfy = nfz = nf
+    n1 = np.asarray(normal, dtype=np.float64)
+    nx = n1[0] / np.sqrt(n1[0]**2 + n1[1]**2 + n1[2]**2)  # :1276-1278
+    ny = n1[1] / np.sqrt(n1[0]**2 + n1[1]**2 + n1[2]**2)
+    nz = n1[2] / np.sqrt(n1[0]**2 + n1[1]**2 + n1[2]**2)
+    V = W = 0
+    if prf is None:
+        U, uu, vv, ww, uw = ref["build_profile"]("hyperbolic-tangent", "top-hat",
+                                                 bulk_velocity, u_dash, kma)      # :1305
+    else:
+        U, V, W = prf["U"], prf["V"], prf["W"]
+        uu, vv, ww, uv, uw, vw = (prf[k] for k in ("uu", "vv", "ww", "uv", "uw", "vw"))
+    if dt == 0.:                                          # :1306-1309
+        flag = np.where(U**2 + V**2 + W**2 != 0)
+        dt = res / np.mean(U[flag])
+    else:                                                 # :1310-1317
+        flag = np.where(U**2 + V**2 + W**2 != 0)
+        dt1 = res / np.mean(U[flag])
+        factor = dt1 / dt
+        lnx = factor * lnx
+        nfx = int(math.ceil(float(fwidth) * lnx))
+    pdfr = np.sqrt(3.0)                                   # :1340
+    if prf is None:                                       # :1343-1350
+        for k in range(0, kma):
+            if uu[k] < 0.0: uu[k] = 0.0
+            if vv[k] < 0.0: vv[k] = 0.0
+            if ww[k] < 0.0: ww[k] = 0.0
+    a = np.zeros((1, nfx * 2 + 1, nfy * 2 + 1, nfz * 2 + 1))
+    xu = np.random.uniform(low=-pdfr, high=pdfr, size=(nfx*2+1, nfy*2+jma, nfz*2+kma))  # :1361
+    xv = np.random.uniform(low=-pdfr, high=pdfr, size=(nfx*2+1, nfy*2+jma, nfz*2+kma))
+    xw = np.random.uniform(low=-pdfr, high=pdfr, size=(nfx*2+1, nfy*2+jma, nfz*2+kma))
+    yu = np.zeros((jma, kma)); yv = np.zeros((jma, kma)); yw = np.zeros((jma, kma))
+    A = np.zeros((jma * kma * 3, ns), dtype=np.float64)   # :1397
+    filt = []
+    for i in range(ns):                                   # :1403
+        ref["filter3DSciPy1D"](xu, yu, a, jma, kma, lnx, lny, lnz, nfx, nfy, nfz)   # :1440
+        ref["filter3DSciPy1D"](xv, yv, a, jma, kma, lnx, lny, lnz, nfx, nfy, nfz)
+        ref["filter3DSciPy1D"](xw, yw, a, jma, kma, lnx, lny, lnz, nfx, nfy, nfz)
+        if i < 3:
+            filt.append(np.stack([yu.copy(), yv.copy(), yw.copy()]))
+        if prf is not None:                               # :1445-1451
+            ref["adapt2prf"](yu, yv, yw, U, V, W, uu, vv, ww, uv, uw, vw, jma, kma)
+        else:
+            ref["adapt1d"](yu, yv, yw, U, uu, vv, ww, uw, jma, kma)
+        xu = np.roll(xu, -1, axis=0); xv = np.roll(xv, -1, axis=0); xw = np.roll(xw, -1, axis=0)
+        xu[nfx*2, :, :] = np.random.uniform(low=-pdfr, high=pdfr, size=(nfy*2+jma, nfz*2+kma))
+        xv[nfx*2, :, :] = np.random.uniform(low=-pdfr, high=pdfr, size=(nfy*2+jma, nfz*2+kma))
+        xw[nfx*2, :, :] = np.random.uniform(low=-pdfr, high=pdfr, size=(nfy*2+jma, nfz*2+kma))
+        A[0:jma*kma, i] = yu.reshape(jma*kma)             # :1471-1473
+        A[jma*kma:2*jma*kma, i] = yv.reshape(jma*kma)
+        A[2*jma*kma:3*jma*kma, i] = yw.reshape(jma*kma)
+        if prf is None:                                   # :1476-1477
+            A[:, i] = ref["rotate_velocity"](A[:, i], nx, ny, nz)
+    out["A_raw"] = A.copy()
+    out["filtered_first_steps"] = np.stack(filt)
+    mean_field = np.mean(A, 1)                            # :1492
+    for j in range(0, ns):
+        A[:, j] = A[:, j] - mean_field[:]
+    out["mean_field"] = mean_field
+    # ---- PODFS.POD (:1294-1393), correct_for_cell_volumes='false', tol_CN=1e-15 --------------
+    num_points = jma * kma
+    C = np.array(np.zeros((ns, ns), dtype=np.float64))
+    ref["calculate_correlation_matrix"](ns, num_points, 3, "false", [], A, C)    # :1303
+    out["C"] = C.copy()
+    energy, temporal_modes = np.linalg.eig(C)             # :1309
+    out["eig_is_real"] = np.array(np.isrealobj(energy))
+    ref["sort_eigenvalues"](ns, energy, temporal_modes)   # :1310
+    tol_CN = 1.0e-15
+    num_valid_modes = 0                                   # :1312-1317
+    while ((energy[num_valid_modes].real / energy[0].real > pow(tol_CN, 2.0)) and
+           (num_valid_modes < ns - 2) and (energy[num_valid_modes].real > 0.0)):
+        num_valid_modes += 1
+        if ((energy[num_valid_modes].real / energy[0].real > pow(tol_CN, 2.0)) and
+                (energy[num_valid_modes].real > 0.0)):
+            num_valid_modes += 1
+    num_modes_trunc = nm
+    if (num_modes_trunc < 0) or (num_modes_trunc > num_valid_modes):           # :1319
+        num_modes_trunc = num_valid_modes
+    for j in range(0, num_valid_modes):                   # :1323-1325
+        temporal_mode_mag = sum(temporal_modes[:, j].real * temporal_modes[:, j].real) / ns
+        temporal_modes[:, j] = temporal_modes[:, j] * np.sqrt(energy[j].real / temporal_mode_mag)
+    energy_trunc_inv = np.diag(np.ones(num_modes_trunc) / energy[0:num_modes_trunc].real, 0)   # :1331
+    spatial = np.dot(np.dot(A[:, 0:ns], temporal_modes[:, 0:num_modes_trunc].real),
+                     energy_trunc_inv) / ns              # :1333
+    out.update(energy=np.asarray(energy), num_valid_modes=np.array(num_valid_modes),
+               nm=np.array(num_modes_trunc), temporal_modes=np.asarray(temporal_modes)[:, :num_modes_trunc],
+               spatial_modes=spatial, dt=np.array(dt), nfx=np.array(nfx), nfy=np.array(nfy),
+               nfz=np.array(nfz), lnx=np.array(lnx), lny=np.array(lny), lnz=np.array(lnz),
+               taps_x=ref["calccoeff"](np.zeros(2*nfx+1), nfx, lnx),
+               taps_y=ref["calccoeff"](np.zeros(2*nfy+1), nfy, lny),
+               taps_z=ref["calccoeff"](np.zeros(2*nfz+1), nfz, lnz))
+    # ---- fourier_coefficients (:1523-1659), run in a scratch dir (writes ./PODFS/PODFS.dat) ----
+    i_d = Obj()
+    i_d.hdf5 = True; i_d.ns = ns; i_d.dt = dt; i_d.nm = num_modes_trunc; i_d.et = et
+    i_d.temporal_modes = temporal_modes; i_d.verbose = False
+    cwd = os.getcwd()
+    tmp = workdir or tempfile.mkdtemp(prefix="pods_golden_")
+    os.makedirs(os.path.join(tmp, "PODFS"), exist_ok=True)
+    try:
+        os.chdir(tmp)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            _stdout = sys.stdout
+            sys.stdout = io.StringIO()
+            try:
+                ref["fourier_coefficients"](i_d)
+                ref["write_eigenvalues"](num_valid_modes, ns, energy, "PODFS/POD.eigenvalues.dat")
+            finally:
+                sys.stdout = _stdout
+        with open("PODFS/PODFS.dat") as f:
+            out["podfs_dat"] = np.array(f.read())
+        with open("PODFS/POD.eigenvalues.dat") as f:
+            out["eigenvalues_dat"] = np.array(f.read())
+    finally:
+        os.chdir(cwd)
+        if workdir is None:
+            shutil.rmtree(tmp, ignore_errors=True)
+    out.update(period=np.array(i_d.period), N_FC=np.asarray(i_d.N_FC), FC=np.asarray(i_d.FC))
+    return out
+
+
+def synthetic_prf(jma, kma, seed):
+    """Deterministic inhomogeneous profile for the adapt2prf path (SURVEY.md 8(d) C5 style)."""
+    r = np.random.RandomState(seed)
+    y = np.linspace(-0.5, 0.5, jma)[:, None]
+    z = np.linspace(-0.5, 0.5, kma)[None, :]
+    U = 0.5 * (1.0 + np.tanh(10.0 * (0.5 - np.sqrt(y**2 + z**2)))) + 0.05
+    V = 0.01 * np.sin(3.0 * y) * np.ones_like(z)
+    W = 0.01 * np.cos(2.0 * z) * np.ones_like(y)
+    s = (0.02 * U)**2
+    rho = 0.4 * np.sin(2.0 * y + 3.0 * z) * np.ones_like(U)
+    uu = s.copy(); vv = 1.1 * s; ww = 0.9 * s
+    uv = rho * np.sqrt(uu * vv); uw = -0.5 * rho * np.sqrt(uu * ww); vw = 0.3 * rho * np.sqrt(vv * ww)
+    uu[0, 0] = 0.0                                        # exercise the a00<=0 guard
+    vv[1, 1] = 0.25 * uv[1, 1] ** 2 / max(uu[1, 1], 1e-300)  # exercise a10^2>R11 clamp
+    del r
+    return dict(U=U, V=V, W=W, uu=uu, vv=vv, ww=ww, uv=uv, uw=uw, vw=vw)
+
+
+CASES = {
+    # name: kwargs                                                            (why)
+    "c1_32x32x64": dict(jma=32, kma=32, ns=64, seed=12345),                  # BASELINE config 1
+    "cli_10x11x5": dict(jma=10, kma=11, ns=5, seed=7),                       # quickstart -n 5, CLI default grid
+    "odd_12x9x17_aniso": dict(jma=12, kma=9, ns=17, seed=3, dt=0.05),        # odd ns, -t => nfx != nfy
+    "prf_8x12x9": dict(jma=8, kma=12, ns=9, seed=11, prf="synthetic"),       # adapt2prf path
+    "rot_6x7x6": dict(jma=6, kma=7, ns=6, seed=5, normal=(1.0, 1.0, 0.5)),   # non-identity rotation
+}
+
+
+def main():
+    ref = load_reference()
+    # unit fixtures for the filter on a raw random block (anisotropic taps) -----------------------
+    rs = np.random.RandomState(2024)
+    x = rs.uniform(-np.sqrt(3), np.sqrt(3), (2*9+1, 2*6+7, 2*4+5))
+    y = np.zeros((7, 5))
+    ref["filter3DSciPy1D"](x, y, None, 7, 5, 4.5, 3.0, 2.0, 9, 6, 4)
+    taps = [ref["calccoeff"](np.zeros(2*n+1), n, l) for n, l in ((9, 4.5), (6, 3.0), (4, 2.0), (12, 6.0))]
+    np.savez_compressed(os.path.join(HERE, "unit_filter.npz"), x=x, y=y, taps_9=taps[0],
+                        taps_6=taps[1], taps_4=taps[2], taps_12=taps[3])
+    # rotation matrices for a few normals
+    normals = np.array([[1, 0, 0], [0, 1, 0], [0, 0, 1], [1, 1, 0], [-1, 0, 0], [0.3, -0.5, 0.8]], float)
+    Rs = []
+    for n in normals:
+        n = n / np.linalg.norm(n)
+        Rs.append(ref["prof_rotation_matrix"](n[0], n[1], n[2]))
+    np.savez_compressed(os.path.join(HERE, "unit_rotation.npz"), normals=normals, R=np.array(Rs))
+    for name, kw in CASES.items():
+        kw = dict(kw)
+        if kw.get("prf") == "synthetic":
+            kw["prf"] = synthetic_prf(kw["jma"], kw["kma"], kw["seed"])
+            extra = {"prf_" + k: v for k, v in kw["prf"].items()}
+        else:
+            extra = {}
+        res = run_reference_pipeline(ref, **kw)
+        meta = {k: np.array(v) for k, v in kw.items() if k != "prf"}
+        res.update({"cfg_" + k: v for k, v in meta.items()})
+        res.update(extra)
+        path = os.path.join(HERE, "%s.npz" % name)
+        np.savez_compressed(path, **res)
+        print("wrote", path, "nm=%d valid=%d" % (res["nm"], res["num_valid_modes"]))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,122 @@
+"""The oracle is pinned against fixtures produced by the reference's own code
+(tests/golden/make_golden.py).  Everything here is bit-exact unless stated."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import pods_oracle as O
+
+CASES = ["c1_32x32x64", "cli_10x11x5", "odd_12x9x17_aniso", "prf_8x12x9", "rot_6x7x6"]
+
+
+def load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name + ".npz"))
+
+
+def cfg_from(g):
+    kw = dict(jma=int(g["cfg_jma"]), kma=int(g["cfg_kma"]), ns=int(g["cfg_ns"]), seed=int(g["cfg_seed"]))
+    if "cfg_dt" in g.files:
+        kw["dt"] = float(g["cfg_dt"])
+    if "cfg_normal" in g.files:
+        kw["normal"] = tuple(g["cfg_normal"])
+    if "prf_U" in g.files:
+        kw["prf"] = {k[4:]: np.array(g[k]) for k in g.files if k.startswith("prf_")}
+    return O.DFConfig(**kw)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_generation_bit_exact(golden_dir, name):
+    g = load(golden_dir, name)
+    cfg = cfg_from(g)
+    assert cfg.nfx == int(g["nfx"]) and cfg.nfy == int(g["nfy"])
+    assert cfg.dt_eff == float(g["dt"])
+    A = O.generate(cfg)
+    assert np.array_equal(A, g["A_raw"])
+    mean, Ac = O.mean_and_center(A)
+    assert np.array_equal(mean, g["mean_field"])
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_pod_and_fourier_bit_exact(golden_dir, name):
+    g = load(golden_dir, name)
+    cfg = cfg_from(g)
+    Ac = g["A_raw"] - g["mean_field"][:, None]
+    res = O.pod(Ac, cfg.ns, cfg.nm)
+    assert np.array_equal(res["C"], g["C"])
+    assert np.array_equal(res["energy"], g["energy"].real)
+    assert res["num_valid"] == int(g["num_valid_modes"]) and res["nm"] == int(g["nm"])
+    assert np.array_equal(res["T"][:, :res["nm"]], g["temporal_modes"].real)
+    assert np.array_equal(res["spatial"], g["spatial_modes"])
+    fo = O.fourier(res["T"], cfg.ns, cfg.dt_eff, res["nm"], cfg.et)
+    assert fo["period"] == float(g["period"])
+    assert np.array_equal(fo["c_count"], g["N_FC"])
+    assert np.array_equal(fo["FC"], g["FC"])
+    txt = O.podfs_dat_text(res["nm"], fo["period"], fo["c"], fo["c_ind"], fo["c_count"], cfg.ns)
+    assert txt == str(g["podfs_dat"])
+    assert O.eigenvalues_text(res["num_valid"], cfg.ns, res["energy"]) == str(g["eigenvalues_dat"])
+
+
+def test_unit_filter_and_taps(golden_dir):
+    g = np.load(os.path.join(golden_dir, "unit_filter.npz"))
+    for n, l, key in ((9, 4.5, "taps_9"), (6, 3.0, "taps_6"), (4, 2.0, "taps_4"), (12, 6.0, "taps_12")):
+        assert np.array_equal(O.calccoeff(n, l), g[key])
+    y = O.filter_block(g["x"], g["taps_9"], g["taps_6"], g["taps_4"])
+    assert np.array_equal(y, g["y"])
+    assert np.array_equal(O.filter_block_scipy(g["x"], g["taps_9"], g["taps_6"], g["taps_4"]), g["y"])
+
+
+def test_unit_rotation(golden_dir):
+    g = np.load(os.path.join(golden_dir, "unit_rotation.npz"))
+    for n, R in zip(g["normals"], g["R"]):
+        n = n / np.linalg.norm(n)
+        assert np.array_equal(O.rotation_matrix(*n), R)
+
+
+def test_loops_form_matches_vectorised(golden_dir):
+    g = load(golden_dir, "cli_10x11x5")
+    cfg = cfg_from(g)
+    assert np.array_equal(O.generate(cfg, loops=True), g["A_raw"])
+
+
+@pytest.mark.parametrize("n", [1, 5, 7, 8, 9, 64, 127, 128, 129, 200, 1000, 4096, 4097, 8193, 9000, 16384, 20000, 50000])
+def test_pairwise_restatement(n):
+    a = np.random.default_rng(n).standard_normal(n) + 1.0
+    assert O.pairwise_sum(a) == np.add.reduce(a)
+    A = np.stack([a, a[::-1]])
+    assert np.array_equal(np.mean(A, 1), np.array([O.pairwise_sum(a), O.pairwise_sum(a[::-1])]) / n)
+
+
+@pytest.mark.parametrize("n", [1, 3, 4, 5, 63, 64, 65, 100, 129, 1000, 4096, 8193, 9000, 16384, 20000])
+def test_complex_pairwise_restatement(n):
+    r = np.random.default_rng(n)
+    z = r.standard_normal(n) + 1j * r.standard_normal(n)
+    sr, si = O.cpairwise_sum(z.real, z.imag)
+    assert complex(sr, si) == z.sum()
+
+
+@pytest.mark.parametrize("ns", [5, 17, 64, 65, 130])
+def test_dft_explicit_equals_reference_expression(ns):
+    y = np.random.default_rng(ns).standard_normal(ns)
+    time, period = O.time_axis(ns, 0.0731)
+    assert np.array_equal(O.dft_explicit(y, time, period), O.dft_reference(y, time, period))
+
+
+def test_dft_conjugate_symmetry():
+    ns = 64
+    y = np.random.default_rng(0).standard_normal(ns)
+    time, period = O.time_axis(ns, 0.05)
+    c = O.dft_reference(y, time, period)
+    h = ns // 2
+    for k in range(1, h):
+        assert c[h + k] == np.conj(c[h - k])
+
+
+def test_prf_row_geometry_doc_example():
+    """docs/usage/CFDCodeIntegration.rst:53 -- first .prf data row for the default
+    10 x 11 grid at res 0.1 (geometry + '%0.12f')."""
+    from nsigproclib import str as fmt  # product helper (sp.str restatement)
+    import PODFS
+    pts = PODFS.cell_centres(10, 11, 0.1, (1.0, 0.0, 0.0), 0.0, (0.0, 0.0, 0.0))
+    row = ",".join(fmt(v) for v in pts[0])
+    assert row == "0.000000000000,-0.500000000000,0.550000011921"
