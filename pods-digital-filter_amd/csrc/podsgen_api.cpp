@@ -178,7 +178,7 @@ struct pods_ctx {
   int64_t S = 0, Sl = 0, Pl = 0, rowlen = 0;
   RngLayout layout;
   RngBuffers rng;
-  DevBuf R, T1, A, mean, lund, taps, rot, prog_mean, prog_dft, tbuf, mag, lam;
+  DevBuf R, T1, A, mean, lund, taps, rot, prog_mean, prog_dft, tbuf, mag, lam, cwork;
   int nprog_mean = 0;
   bool mean_valid = false;
   bool have_snapshots = false;  // A holds ns x rowlen snapshots (generated or loaded)
@@ -272,7 +272,7 @@ int pods_destroy(pods_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->R, &c->T1, &c->A, &c->mean, &c->lund, &c->taps, &c->rot, &c->prog_mean,
-                    &c->prog_dft, &c->tbuf, &c->mag, &c->lam})
+                    &c->prog_dft, &c->tbuf, &c->mag, &c->lam, &c->cwork})
     release(*b);
   c->rng.free_all();
   delete c;
@@ -451,8 +451,11 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
   if (!c->have_snapshots || !c->mean_valid) return fail(PODS_ERR_STATE, "pods_corr needs pods_mean first");
   if (!C_dev) return fail(PODS_ERR_ARG, "C_dev is null");
   PODS_HIP(hipSetDevice(c->device));
+  int64_t ksplit = 0;
+  const int nsplit = pods::syrk_plan(c->p.ns, c->rowlen, &ksplit);
+  if (nsplit > 1) PODS_HIP(ensure(c->cwork, (size_t)nsplit * c->p.ns * c->p.ns * sizeof(double)));
   PODS_HIP(pods::launch_syrk(c->A.as<double>(), c->rowlen, c->p.ns, c->rowlen, c->mean.as<double>(),
-                             C_dev, c->p.ns, divide, c->stream));
+                             C_dev, c->p.ns, divide, c->cwork.as<double>(), c->stream));
   return PODS_OK;
   PODS_CATCH
 }

@@ -21,8 +21,10 @@ hipError_t launch_filter_yz(int NY, const double* T1, const double* by, const do
 int filter_yz_max_K(int Kp);
 hipError_t launch_mean(const double* AT, int64_t rowlen, int ns, const int* prog, int nprog,
                        double* mean, hipStream_t st);
+// Split-K plan: returns the number of K splits (work slabs of ns*ns doubles needed when > 1).
+int syrk_plan(int ns, int64_t Kdim, int64_t* ksplit);
 hipError_t launch_syrk(const double* AT, int64_t ld, int ns, int64_t Kdim, const double* mean,
-                       double* C, int64_t ldc, int divide, hipStream_t st);
+                       double* C, int64_t ldc, int divide, double* work, hipStream_t st);
 hipError_t launch_divide(double* x, int64_t n, double d, hipStream_t st);
 hipError_t launch_temporal(const double* V, int64_t v_rs, int64_t v_cs, int ns, int ncols,
                            int nvalid, const double* lam, double* mag, double* T, hipStream_t st);

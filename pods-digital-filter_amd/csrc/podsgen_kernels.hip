@@ -9,6 +9,7 @@
 //   * k_dft           replicates numpy's complex expression; sin/cos from OCML
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "podsgen_kernels.h"
@@ -328,10 +329,11 @@ __global__ __launch_bounds__(512) void k_filter_yz(
       v = v + lund[7 * Pl + p];
       w = w + lund[8 * Pl + p];
     }
-    if (rotate) {  // rotate_velocity :1119-1131 (R.dot(V))
-      const double ur = (R9[0] * u + R9[1] * v) + R9[2] * w;
-      const double vr = (R9[3] * u + R9[4] * v) + R9[5] * w;
-      const double wr = (R9[6] * u + R9[7] * v) + R9[8] * w;
+    if (rotate) {  // rotate_velocity :1119-1131: numpy R.dot(V) -> OpenBLAS dgemv, whose
+                   // 3-term row dot is fma(R2, w, fma(R0, u, R1*v)) (pinned by golden rot case)
+      const double ur = __builtin_fma(R9[2], w, __builtin_fma(R9[0], u, R9[1] * v));
+      const double vr = __builtin_fma(R9[5], w, __builtin_fma(R9[3], u, R9[4] * v));
+      const double wr = __builtin_fma(R9[8], w, __builtin_fma(R9[6], u, R9[7] * v));
       u = ur;
       v = vr;
       w = wr;
@@ -464,6 +466,134 @@ __global__ __launch_bounds__(256) void k_syrk(const double* __restrict__ AT, int
           if (bi != bj) C[(int64_t)gj * ldc + gi] = v;
         }
       }
+}
+
+// Split-K SYRK, 128x128 tiles.  Work item = (lower-triangle tile, K split), dealt so that the
+// items one XCD runs back to back are neighbouring tiles of one split (T1 remap, bijective).
+// 4 waves as 2x2, each wave 64x64 = 4x4 MFMA 16x16 blocks; next K-tile prefetched into
+// registers while the current one is on the matrix cores.  Partials go to slab `s` of Cout
+// (deterministic: the sum over splits is done by k_syrk_reduce in split order).
+template <int BT, int KT>
+__global__ __launch_bounds__(256, 2) void k_syrk_split(const double* __restrict__ AT, int64_t ld,
+                                                       int ns, int64_t Kdim,
+                                                       const double* __restrict__ mean, int ntiles,
+                                                       int nsplit, int64_t ksplit,
+                                                       double* __restrict__ Cout, int64_t ldc,
+                                                       int64_t slab, int final_write, int divide) {
+  constexpr int MB = BT / 32;            // 16x16 blocks per wave per dim
+  constexpr int PAIRS = BT * KT / 2;     // double2 per operand per K-tile
+  constexpr int PPT = PAIRS / 256;       // per thread
+  __shared__ __attribute__((aligned(16))) double Xs[BT][KT + 1];
+  __shared__ __attribute__((aligned(16))) double Ys[BT][KT + 1];
+  const int nitems = ntiles * nsplit;
+  const int b = blockIdx.x;
+  const int xcd = b & 7, qq = nitems >> 3, rr = nitems & 7;
+  const int logical = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
+  const int sp = logical / ntiles, t = logical - sp * ntiles;
+  int bi = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+  while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
+  while (bi * (bi + 1) / 2 > t) --bi;
+  const int bj = t - bi * (bi + 1) / 2;
+  const int64_t kb = (int64_t)sp * ksplit;
+  const int64_t ke = min(Kdim, kb + ksplit);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int i0 = bi * BT, j0 = bj * BT;
+  f64x4 acc[MB][MB];
+#pragma unroll
+  for (int m = 0; m < MB; ++m)
+#pragma unroll
+    for (int n = 0; n < MB; ++n) acc[m][n] = (f64x4){0.0, 0.0, 0.0, 0.0};
+  double2 xr[PPT], yr[PPT];
+  auto load = [&](int64_t k0) {
+#pragma unroll
+    for (int e = 0; e < PPT; ++e) {
+      const int pidx = tid + e * 256;
+      const int row = pidx / (KT / 2), kk = (pidx % (KT / 2)) * 2;
+      const int64_t k = k0 + kk;
+      double2 xv = make_double2(0.0, 0.0), yv = make_double2(0.0, 0.0);
+      if (k + 1 < ke) {
+        const double2 m2 = *reinterpret_cast<const double2*>(mean + k);
+        if (i0 + row < ns) {
+          const double2 a = *reinterpret_cast<const double2*>(AT + (int64_t)(i0 + row) * ld + k);
+          xv = make_double2(a.x - m2.x, a.y - m2.y);
+        }
+        if (j0 + row < ns) {
+          const double2 a = *reinterpret_cast<const double2*>(AT + (int64_t)(j0 + row) * ld + k);
+          yv = make_double2(a.x - m2.x, a.y - m2.y);
+        }
+      } else if (k < ke) {
+        const double mk = mean[k];
+        if (i0 + row < ns) xv.x = AT[(int64_t)(i0 + row) * ld + k] - mk;
+        if (j0 + row < ns) yv.x = AT[(int64_t)(j0 + row) * ld + k] - mk;
+      }
+      xr[e] = xv;
+      yr[e] = yv;
+    }
+  };
+  load(kb);
+  for (int64_t k0 = kb; k0 < ke; k0 += KT) {
+#pragma unroll
+    for (int e = 0; e < PPT; ++e) {
+      const int pidx = tid + e * 256;
+      const int row = pidx / (KT / 2), kk = (pidx % (KT / 2)) * 2;
+      Xs[row][kk] = xr[e].x;
+      Xs[row][kk + 1] = xr[e].y;
+      Ys[row][kk] = yr[e].x;
+      Ys[row][kk + 1] = yr[e].y;
+    }
+    __syncthreads();
+    if (k0 + KT < ke) load(k0 + KT);
+#pragma unroll
+    for (int kk = 0; kk < KT; kk += 4) {
+      double a[MB], bv[MB];
+#pragma unroll
+      for (int m = 0; m < MB; ++m) a[m] = Xs[wr * (BT / 2) + m * 16 + (lane & 15)][kk + (lane >> 4)];
+#pragma unroll
+      for (int n = 0; n < MB; ++n) bv[n] = Ys[wc * (BT / 2) + n * 16 + (lane & 15)][kk + (lane >> 4)];
+#pragma unroll
+      for (int m = 0; m < MB; ++m)
+#pragma unroll
+        for (int n = 0; n < MB; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], bv[n], acc[m][n], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  double* dst = final_write ? Cout : Cout + (int64_t)sp * slab;
+  const double dn = (double)ns;
+#pragma unroll
+  for (int m = 0; m < MB; ++m)
+#pragma unroll
+    for (int n = 0; n < MB; ++n)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int gi = i0 + wr * (BT / 2) + m * 16 + (lane >> 4) + 4 * reg;
+        const int gj = j0 + wc * (BT / 2) + n * 16 + (lane & 15);
+        if (gi < ns && gj < ns) {
+          double v = acc[m][n][reg];
+          if (final_write) {
+            if (divide) v = v / dn;
+            dst[(int64_t)gi * ldc + gj] = v;
+            if (bi != bj) dst[(int64_t)gj * ldc + gi] = v;
+          } else if (gi >= gj) {
+            dst[(int64_t)gi * ldc + gj] = v;
+          }
+        }
+      }
+}
+
+// C[i][j] = (sum_s part_s[max][min]) [/ ns], splits summed in order.
+__global__ void k_syrk_reduce(const double* __restrict__ part, int nsplit, int64_t slab, int ns,
+                              int64_t ldc, double* __restrict__ C, int divide) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = blockIdx.y;
+  if (j >= ns) return;
+  const int a = i >= j ? i : j, b = i >= j ? j : i;
+  const int64_t off = (int64_t)a * ldc + b;
+  double v = part[off];
+  for (int s = 1; s < nsplit; ++s) v = v + part[(int64_t)s * slab + off];
+  if (divide) v = v / (double)ns;
+  C[(int64_t)i * ldc + j] = v;
 }
 
 __global__ void k_divide(double* __restrict__ x, int64_t n, double d) {
@@ -718,13 +848,37 @@ hipError_t launch_mean(const double* AT, int64_t rowlen, int ns, const int* prog
   return hipGetLastError();
 }
 
-hipError_t launch_syrk(const double* AT, int64_t ld, int ns, int64_t Kdim, const double* mean,
-                       double* C, int64_t ldc, int divide, hipStream_t st) {
-  constexpr int BT = 64, KT = 16;
+int syrk_plan(int ns, int64_t Kdim, int64_t* ksplit) {
+  constexpr int BT = 128, KT = 16;
   const int nb = (ns + BT - 1) / BT;
   const int tiles = nb * (nb + 1) / 2;
-  hipLaunchKernelGGL((k_syrk<BT, KT>), dim3(tiles), dim3(256), 0, st, AT, ld, ns, Kdim, mean, nb, C,
-                     ldc, divide);
+  const int slots = 512;  // 256 CUs x 2 workgroups
+  int64_t nsplit = (4LL * slots + tiles - 1) / tiles;
+  const int64_t maxsplit = std::max<int64_t>(1, Kdim / (KT * 64));
+  nsplit = std::min(nsplit, maxsplit);
+  int64_t ks = (Kdim + nsplit - 1) / nsplit;
+  ks = ((ks + KT - 1) / KT) * KT;
+  nsplit = (Kdim + ks - 1) / ks;
+  *ksplit = ks;
+  return (int)std::max<int64_t>(1, nsplit);
+}
+
+hipError_t launch_syrk(const double* AT, int64_t ld, int ns, int64_t Kdim, const double* mean,
+                       double* C, int64_t ldc, int divide, double* work, hipStream_t st) {
+  constexpr int BT = 128, KT = 16;
+  const int nb = (ns + BT - 1) / BT;
+  const int tiles = nb * (nb + 1) / 2;
+  int64_t ksplit = 0;
+  const int nsplit = syrk_plan(ns, Kdim, &ksplit);
+  const int64_t slab = (int64_t)ns * ldc;
+  const int final_write = nsplit == 1;
+  hipLaunchKernelGGL((k_syrk_split<BT, KT>), dim3(tiles * nsplit), dim3(256), 0, st, AT, ld, ns, Kdim,
+                     mean, tiles, nsplit, ksplit, final_write ? C : work, ldc, slab, final_write,
+                     divide);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || final_write) return e;
+  hipLaunchKernelGGL(k_syrk_reduce, dim3((ns + 255) / 256, ns), dim3(256), 0, st, work, nsplit, slab,
+                     ns, ldc, C, divide);
   return hipGetLastError();
 }
 
