@@ -167,6 +167,29 @@ struct RngBuffers {
   }
 };
 
+// SYRK work items {bi, bj, split, 0}: split-major, then 8x8 super-blocks of 128x128 tiles
+// in the lower triangle, tiles row-major inside a super-block.  Consecutive items go to one
+// XCD, so the 64 workgroups an XCD holds at once cover one super-block: 16 panels, one K range.
+std::vector<int> syrk_items(int ns, int nsplit) {
+  const int T = pods::syrk_tile();
+  const int nb = (ns + T - 1) / T;
+  const int SB = 8;
+  const int nsb = (nb + SB - 1) / SB;
+  std::vector<int> it;
+  for (int s = 0; s < nsplit; ++s)
+    for (int I = 0; I < nsb; ++I)
+      for (int Jb = 0; Jb <= I; ++Jb)
+        for (int bi = I * SB; bi < std::min(nb, (I + 1) * SB); ++bi)
+          for (int bj = Jb * SB; bj < std::min(nb, (Jb + 1) * SB); ++bj)
+            if (bj <= bi) {
+              it.push_back(bi);
+              it.push_back(bj);
+              it.push_back(s);
+              it.push_back(0);
+            }
+  return it;
+}
+
 }  // namespace
 
 struct pods_ctx {
@@ -178,7 +201,9 @@ struct pods_ctx {
   int64_t S = 0, Sl = 0, Pl = 0, rowlen = 0;
   RngLayout layout;
   RngBuffers rng;
-  DevBuf R, T1, A, mean, lund, taps, rot, prog_mean, prog_dft, tbuf, mag, lam, cwork;
+  DevBuf R, T1, A, mean, lund, taps, rot, prog_mean, prog_dft, tbuf, mag, lam, cwork, items;
+  int nitems = 0;
+  int64_t items_key = -1;
   int nprog_mean = 0;
   bool mean_valid = false;
   bool have_snapshots = false;  // A holds ns x rowlen snapshots (generated or loaded)
@@ -272,7 +297,7 @@ int pods_destroy(pods_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->R, &c->T1, &c->A, &c->mean, &c->lund, &c->taps, &c->rot, &c->prog_mean,
-                    &c->prog_dft, &c->tbuf, &c->mag, &c->lam, &c->cwork})
+                    &c->prog_dft, &c->tbuf, &c->mag, &c->lam, &c->cwork, &c->items})
     release(*b);
   c->rng.free_all();
   delete c;
@@ -452,10 +477,19 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
   if (!C_dev) return fail(PODS_ERR_ARG, "C_dev is null");
   PODS_HIP(hipSetDevice(c->device));
   int64_t ksplit = 0;
-  const int nsplit = pods::syrk_plan(c->p.ns, c->rowlen, &ksplit);
-  if (nsplit > 1) PODS_HIP(ensure(c->cwork, (size_t)nsplit * c->p.ns * c->p.ns * sizeof(double)));
-  PODS_HIP(pods::launch_syrk(c->A.as<double>(), c->rowlen, c->p.ns, c->rowlen, c->mean.as<double>(),
-                             C_dev, c->p.ns, divide, c->cwork.as<double>(), c->stream));
+  const int ns = c->p.ns;
+  const int nsplit = pods::syrk_plan(ns, c->rowlen, &ksplit);
+  if (nsplit > 1) PODS_HIP(ensure(c->cwork, (size_t)nsplit * ns * ns * sizeof(double)));
+  if (c->items_key != ((int64_t)ns << 20 | nsplit)) {
+    std::vector<int> items = syrk_items(ns, nsplit);
+    PODS_HIP(ensure(c->items, items.size() * sizeof(int)));
+    PODS_HIP(hipMemcpy(c->items.p, items.data(), items.size() * sizeof(int), hipMemcpyHostToDevice));
+    c->nitems = (int)items.size() / 4;
+    c->items_key = (int64_t)ns << 20 | nsplit;
+  }
+  PODS_HIP(pods::launch_syrk(c->A.as<double>(), c->rowlen, ns, c->rowlen, c->mean.as<double>(),
+                             c->items.as<int>(), c->nitems, nsplit, ksplit, C_dev, ns, divide,
+                             c->cwork.as<double>(), c->stream));
   return PODS_OK;
   PODS_CATCH
 }

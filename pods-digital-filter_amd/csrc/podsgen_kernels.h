@@ -23,8 +23,11 @@ hipError_t launch_mean(const double* AT, int64_t rowlen, int ns, const int* prog
                        double* mean, hipStream_t st);
 // Split-K plan: returns the number of K splits (work slabs of ns*ns doubles needed when > 1).
 int syrk_plan(int ns, int64_t Kdim, int64_t* ksplit);
+int syrk_tile();
+// items: nitems x int4 {bi, bj, split, 0} in launch order (see podsgen_api.cpp syrk_items)
 hipError_t launch_syrk(const double* AT, int64_t ld, int ns, int64_t Kdim, const double* mean,
-                       double* C, int64_t ldc, int divide, double* work, hipStream_t st);
+                       const int* items, int nitems, int nsplit, int64_t ksplit, double* C,
+                       int64_t ldc, int divide, double* work, hipStream_t st);
 hipError_t launch_divide(double* x, int64_t n, double d, hipStream_t st);
 hipError_t launch_temporal(const double* V, int64_t v_rs, int64_t v_cs, int ns, int ncols,
                            int nvalid, const double* lam, double* mag, double* T, hipStream_t st);

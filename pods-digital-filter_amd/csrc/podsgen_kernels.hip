@@ -476,24 +476,23 @@ __global__ __launch_bounds__(256) void k_syrk(const double* __restrict__ AT, int
 template <int BT, int KT>
 __global__ __launch_bounds__(256, 2) void k_syrk_split(const double* __restrict__ AT, int64_t ld,
                                                        int ns, int64_t Kdim,
-                                                       const double* __restrict__ mean, int ntiles,
-                                                       int nsplit, int64_t ksplit,
-                                                       double* __restrict__ Cout, int64_t ldc,
-                                                       int64_t slab, int final_write, int divide) {
+                                                       const double* __restrict__ mean,
+                                                       const int4* __restrict__ items, int nitems,
+                                                       int64_t ksplit, double* __restrict__ Cout,
+                                                       int64_t ldc, int64_t slab, int final_write,
+                                                       int divide) {
   constexpr int MB = BT / 32;            // 16x16 blocks per wave per dim
   constexpr int PAIRS = BT * KT / 2;     // double2 per operand per K-tile
   constexpr int PPT = PAIRS / 256;       // per thread
   __shared__ __attribute__((aligned(16))) double Xs[BT][KT + 1];
   __shared__ __attribute__((aligned(16))) double Ys[BT][KT + 1];
-  const int nitems = ntiles * nsplit;
+  // items[] is host-ordered (split, super-block, tile); the bijective XCD remap hands each
+  // XCD a contiguous run of it (T1), so co-resident workgroups share panels and K position.
   const int b = blockIdx.x;
   const int xcd = b & 7, qq = nitems >> 3, rr = nitems & 7;
   const int logical = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
-  const int sp = logical / ntiles, t = logical - sp * ntiles;
-  int bi = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
-  while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
-  while (bi * (bi + 1) / 2 > t) --bi;
-  const int bj = t - bi * (bi + 1) / 2;
+  const int4 it = items[logical];
+  const int bi = it.x, bj = it.y, sp = it.z;
   const int64_t kb = (int64_t)sp * ksplit;
   const int64_t ke = min(Kdim, kb + ksplit);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -853,7 +852,9 @@ int syrk_plan(int ns, int64_t Kdim, int64_t* ksplit) {
   const int nb = (ns + BT - 1) / BT;
   const int tiles = nb * (nb + 1) / 2;
   const int slots = 512;  // 256 CUs x 2 workgroups
-  int64_t nsplit = (4LL * slots + tiles - 1) / tiles;
+  // ~8 rounds of work items; one split per XCD when that many fit
+  int64_t nsplit = (8LL * slots + tiles - 1) / tiles;
+  if (nsplit > 8) nsplit = ((nsplit + 7) / 8) * 8;
   const int64_t maxsplit = std::max<int64_t>(1, Kdim / (KT * 64));
   nsplit = std::min(nsplit, maxsplit);
   int64_t ks = (Kdim + nsplit - 1) / nsplit;
@@ -863,18 +864,17 @@ int syrk_plan(int ns, int64_t Kdim, int64_t* ksplit) {
   return (int)std::max<int64_t>(1, nsplit);
 }
 
+int syrk_tile() { return 128; }
+
 hipError_t launch_syrk(const double* AT, int64_t ld, int ns, int64_t Kdim, const double* mean,
-                       double* C, int64_t ldc, int divide, double* work, hipStream_t st) {
+                       const int* items, int nitems, int nsplit, int64_t ksplit, double* C,
+                       int64_t ldc, int divide, double* work, hipStream_t st) {
   constexpr int BT = 128, KT = 16;
-  const int nb = (ns + BT - 1) / BT;
-  const int tiles = nb * (nb + 1) / 2;
-  int64_t ksplit = 0;
-  const int nsplit = syrk_plan(ns, Kdim, &ksplit);
   const int64_t slab = (int64_t)ns * ldc;
   const int final_write = nsplit == 1;
-  hipLaunchKernelGGL((k_syrk_split<BT, KT>), dim3(tiles * nsplit), dim3(256), 0, st, AT, ld, ns, Kdim,
-                     mean, tiles, nsplit, ksplit, final_write ? C : work, ldc, slab, final_write,
-                     divide);
+  hipLaunchKernelGGL((k_syrk_split<BT, KT>), dim3(nitems), dim3(256), 0, st, AT, ld, ns, Kdim, mean,
+                     reinterpret_cast<const int4*>(items), nitems, ksplit, final_write ? C : work, ldc,
+                     slab, final_write, divide);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || final_write) return e;
   hipLaunchKernelGGL(k_syrk_reduce, dim3((ns + 255) / 256, ns), dim3(256), 0, st, work, nsplit, slab,

@@ -1,0 +1,18 @@
+"""Time pods_corr alone at J x K x NS: python tools/syrk_probe.py J K NS reps"""
+import os, sys, time
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "pods-digital-filter_amd"))
+import numpy as np, torch, podsgen
+from podsgen import engine as E
+J, K, NS = (int(a) for a in sys.argv[1:4]); reps = int(sys.argv[4]) if len(sys.argv) > 4 else 5
+s = podsgen.DFSetup(jma=J, kma=K, ns=NS, seed=1)
+gen = E.Generator(s, device=0); snap = gen.generate()
+ctx = gen.ctx
+mean = torch.empty(snap.rowlen, dtype=torch.float64, device="cuda")
+podsgen.check(ctx.lib.pods_mean(ctx.h, E.ptr(mean), 1))
+C = torch.empty((NS, NS), dtype=torch.float64, device="cuda")
+flops = 3 * J * K * NS * (NS + 1)
+for r in range(reps):
+    torch.cuda.synchronize(); t = time.time()
+    podsgen.check(ctx.lib.pods_corr(ctx.h, E.ptr(C), 1))
+    torch.cuda.synchronize(); dt = time.time() - t
+    print("corr %.2f ms  %.1f TFLOP/s (triangle flops)" % (dt * 1e3, flops / dt / 1e12), flush=True)
