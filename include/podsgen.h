@@ -84,11 +84,14 @@ int pods_df_configure(pods_ctx* ctx, const pods_df_params* params, const double*
  * (filter3DSciPy1D :100-140 x3, adapt1d/adapt2prf, rotate_velocity, A[:,i] = ... :1471).
  * The snapshot matrix stays on the device, snapshot-major: A_T[i][c*P_local + p]. */
 int pods_df_generate(pods_ctx* ctx);
-/* Device pointer and row length (= 3*P_local) of the snapshot matrix A_T (ns rows). */
+/* Device pointer and row length (= 3*P_local) of the snapshot matrix.  Device layout is
+ * K-tiled: element (snapshot i, row r of the reference A) is at
+ * a_dev[((r/16)*ns + i)*16 + r%16], rows padded with zeros to a multiple of 16. */
 int pods_df_snapshots(pods_ctx* ctx, double** a_dev, int64_t* row_len);
 
 /* Load an existing snapshot matrix instead of generating one (PODFS.POD called on a
- * user array, PODFS.py:1294).  at_host: snapshot-major ns x row_len (row i = A[:, i]). */
+ * user array, PODFS.py:1294).  at_host: snapshot-major ns x row_len (row i = A[:, i]);
+ * re-laid out into the K-tiled device layout. */
 int pods_set_snapshots(pods_ctx* ctx, const double* at_host, int ns, int64_t row_len);
 
 /* Stream-ordered copy between host/device buffers of this context's device

@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <exception>
@@ -170,24 +171,39 @@ struct RngBuffers {
 // SYRK work items {bi, bj, split, 0}: split-major, then 8x8 super-blocks of 128x128 tiles
 // in the lower triangle, tiles row-major inside a super-block.  Consecutive items go to one
 // XCD, so the 64 workgroups an XCD holds at once cover one super-block: 16 panels, one K range.
-std::vector<int> syrk_items(int ns, int nsplit) {
-  const int T = pods::syrk_tile();
-  const int nb = (ns + T - 1) / T;
-  const int SB = 8;
-  const int nsb = (nb + SB - 1) / SB;
+std::vector<int> syrk_items(int kernel, int ns, int nsplit) {
   std::vector<int> it;
+  auto push = [&](int bi, int bj, int s) {
+    it.push_back(bi);
+    it.push_back(bj);
+    it.push_back(s);
+    it.push_back(0);
+  };
+  if (kernel == 2) {  // 256 x 128 tiles, super-blocks of 4 x 8 tiles (32 = one XCD's CUs)
+    const int nbi = (ns + 255) / 256, nbj = (ns + 127) / 128;
+    for (int s = 0; s < nsplit; ++s)
+      for (int BI = 0; BI < nbi; BI += 4)
+        for (int BJ = 0; BJ < nbj; BJ += 8)
+          for (int bi = BI; bi < std::min(nbi, BI + 4); ++bi)
+            for (int bj = BJ; bj < std::min(nbj, BJ + 8); ++bj)
+              if (bj < 2 * bi + 2) push(bi, bj, s);
+    return it;
+  }
+  const int T = 128, SB = 8;
+  const int nb = (ns + T - 1) / T;
+  const int nsb = (nb + SB - 1) / SB;
   for (int s = 0; s < nsplit; ++s)
     for (int I = 0; I < nsb; ++I)
       for (int Jb = 0; Jb <= I; ++Jb)
         for (int bi = I * SB; bi < std::min(nb, (I + 1) * SB); ++bi)
           for (int bj = Jb * SB; bj < std::min(nb, (Jb + 1) * SB); ++bj)
-            if (bj <= bi) {
-              it.push_back(bi);
-              it.push_back(bj);
-              it.push_back(s);
-              it.push_back(0);
-            }
+            if (bj <= bi) push(bi, bj, s);
   return it;
+}
+
+int syrk_kernel_choice() {
+  const char* e = std::getenv("PODS_SYRK_KERNEL");
+  return (e && e[0] == '1') ? 1 : 2;
 }
 
 }  // namespace
@@ -198,7 +214,7 @@ struct pods_ctx {
   bool configured = false;
   pods_df_params p{};
   int NX = 0, NY = 0, NZ = 0, Kp = 0, jl = 0;
-  int64_t S = 0, Sl = 0, Pl = 0, rowlen = 0;
+  int64_t S = 0, Sl = 0, Pl = 0, rowlen = 0, rowpad = 0;  // rowpad: rowlen rounded up to 16
   RngLayout layout;
   RngBuffers rng;
   DevBuf R, T1, A, mean, lund, taps, rot, prog_mean, prog_dft, tbuf, mag, lam, cwork, items;
@@ -343,6 +359,7 @@ int pods_df_configure(pods_ctx* c, const pods_df_params* prm, const double* bx, 
   c->Sl = (int64_t)(c->jl + 2 * p.nfy) * c->Kp;
   c->Pl = (int64_t)c->jl * p.kma;
   c->rowlen = 3 * c->Pl;
+  c->rowpad = (c->rowlen + 15) / 16 * 16;
   if (p.kma > pods::filter_yz_max_K(c->Kp))
     return fail(PODS_ERR_UNSUPPORTED, "kma too large for the y/z filter kernel");
   const int64_t nplanes = 3 * (int64_t)(c->NX + p.ns - 1);
@@ -350,8 +367,11 @@ int pods_df_configure(pods_ctx* c, const pods_df_params* prm, const double* bx, 
   c->layout = make_layout(ntot);
   PODS_HIP(ensure(c->R, (size_t)nplanes * c->Sl * sizeof(double)));
   PODS_HIP(ensure(c->T1, (size_t)3 * p.ns * c->Sl * sizeof(double)));
-  PODS_HIP(ensure(c->A, (size_t)p.ns * c->rowlen * sizeof(double)));
-  PODS_HIP(ensure(c->mean, (size_t)c->rowlen * sizeof(double)));
+  PODS_HIP(ensure(c->A, (size_t)p.ns * c->rowpad * sizeof(double)));
+  PODS_HIP(ensure(c->mean, (size_t)c->rowpad * sizeof(double)));
+  // padded K columns of the K-tiled snapshot matrix (and of the mean) stay zero
+  PODS_HIP(hipMemset(c->A.p, 0, (size_t)p.ns * c->rowpad * sizeof(double)));
+  PODS_HIP(hipMemset(c->mean.p, 0, (size_t)c->rowpad * sizeof(double)));
   PODS_HIP(ensure(c->lund, (size_t)9 * c->Pl * sizeof(double)));
   PODS_HIP(ensure(c->taps, (size_t)(c->NX + c->NY + c->NZ) * sizeof(double)));
   PODS_HIP(ensure(c->rot, 9 * sizeof(double)));
@@ -419,9 +439,19 @@ int pods_set_snapshots(pods_ctx* c, const double* at, int ns, int64_t rowlen) {
   if (int e = check_ctx(c)) return e;
   if (!at || ns <= 0 || rowlen <= 0) return fail(PODS_ERR_ARG, "bad snapshot matrix");
   PODS_HIP(hipSetDevice(c->device));
-  PODS_HIP(ensure(c->A, (size_t)ns * rowlen * sizeof(double)));
-  PODS_HIP(ensure(c->mean, (size_t)rowlen * sizeof(double)));
-  PODS_HIP(hipMemcpy(c->A.p, at, (size_t)ns * rowlen * sizeof(double), hipMemcpyHostToDevice));
+  const int64_t rowpad = (rowlen + 15) / 16 * 16;
+  // host-side re-layout into the K-tiled device layout (podsgen_kernels.hip at_off)
+  std::vector<double> tiled((size_t)ns * rowpad, 0.0);
+  for (int64_t kb = 0; kb < rowpad / 16; ++kb)
+    for (int64_t i = 0; i < ns; ++i)
+      for (int64_t e = 0; e < 16; ++e) {
+        const int64_t r = kb * 16 + e;
+        if (r < rowlen) tiled[(size_t)((kb * ns + i) * 16 + e)] = at[(size_t)(i * rowlen + r)];
+      }
+  PODS_HIP(ensure(c->A, tiled.size() * sizeof(double)));
+  PODS_HIP(ensure(c->mean, (size_t)rowpad * sizeof(double)));
+  PODS_HIP(hipMemset(c->mean.p, 0, (size_t)rowpad * sizeof(double)));
+  PODS_HIP(hipMemcpy(c->A.p, tiled.data(), tiled.size() * sizeof(double), hipMemcpyHostToDevice));
   std::vector<int> prog = pairwise_program(ns);
   c->nprog_mean = (int)prog.size() / 2;
   PODS_HIP(ensure(c->prog_mean, prog.size() * sizeof(int)));
@@ -429,6 +459,7 @@ int pods_set_snapshots(pods_ctx* c, const double* at, int ns, int64_t rowlen) {
   c->p = pods_df_params{};
   c->p.ns = ns;
   c->rowlen = rowlen;
+  c->rowpad = rowpad;
   c->configured = false;
   c->have_snapshots = true;
   c->mean_valid = false;
@@ -478,16 +509,18 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
   PODS_HIP(hipSetDevice(c->device));
   int64_t ksplit = 0;
   const int ns = c->p.ns;
-  const int nsplit = pods::syrk_plan(ns, c->rowlen, &ksplit);
-  if (nsplit > 1) PODS_HIP(ensure(c->cwork, (size_t)nsplit * ns * ns * sizeof(double)));
-  if (c->items_key != ((int64_t)ns << 20 | nsplit)) {
-    std::vector<int> items = syrk_items(ns, nsplit);
+  const int kern = syrk_kernel_choice();
+  const int nsplit = pods::syrk_plan(kern, ns, c->rowpad, &ksplit);
+  if (nsplit > 1 || kern == 2) PODS_HIP(ensure(c->cwork, (size_t)nsplit * ns * ns * sizeof(double)));
+  const int64_t key = ((int64_t)kern << 40) | ((int64_t)ns << 20) | nsplit;
+  if (c->items_key != key) {
+    std::vector<int> items = syrk_items(kern, ns, nsplit);
     PODS_HIP(ensure(c->items, items.size() * sizeof(int)));
     PODS_HIP(hipMemcpy(c->items.p, items.data(), items.size() * sizeof(int), hipMemcpyHostToDevice));
     c->nitems = (int)items.size() / 4;
-    c->items_key = (int64_t)ns << 20 | nsplit;
+    c->items_key = key;
   }
-  PODS_HIP(pods::launch_syrk(c->A.as<double>(), c->rowlen, ns, c->rowlen, c->mean.as<double>(),
+  PODS_HIP(pods::launch_syrk(kern, c->A.as<double>(), c->rowpad, ns, c->rowpad, c->mean.as<double>(),
                              c->items.as<int>(), c->nitems, nsplit, ksplit, C_dev, ns, divide,
                              c->cwork.as<double>(), c->stream));
   return PODS_OK;

@@ -21,13 +21,13 @@ hipError_t launch_filter_yz(int NY, const double* T1, const double* by, const do
 int filter_yz_max_K(int Kp);
 hipError_t launch_mean(const double* AT, int64_t rowlen, int ns, const int* prog, int nprog,
                        double* mean, hipStream_t st);
+// SYRK kernels: 1 = 128x128 register-staged (k_syrk_split), 2 = 256x128 LDS-DMA (k_syrk_glds).
 // Split-K plan: returns the number of K splits (work slabs of ns*ns doubles needed when > 1).
-int syrk_plan(int ns, int64_t Kdim, int64_t* ksplit);
-int syrk_tile();
+int syrk_plan(int kernel, int ns, int64_t Kdim, int64_t* ksplit);
 // items: nitems x int4 {bi, bj, split, 0} in launch order (see podsgen_api.cpp syrk_items)
-hipError_t launch_syrk(const double* AT, int64_t ld, int ns, int64_t Kdim, const double* mean,
-                       const int* items, int nitems, int nsplit, int64_t ksplit, double* C,
-                       int64_t ldc, int divide, double* work, hipStream_t st);
+hipError_t launch_syrk(int kernel, const double* AT, int64_t ld, int ns, int64_t Kdim,
+                       const double* mean, const int* items, int nitems, int nsplit, int64_t ksplit,
+                       double* C, int64_t ldc, int divide, double* work, hipStream_t st);
 hipError_t launch_divide(double* x, int64_t n, double d, hipStream_t st);
 hipError_t launch_temporal(const double* V, int64_t v_rs, int64_t v_cs, int ns, int ncols,
                            int nvalid, const double* lam, double* mag, double* T, hipStream_t st);

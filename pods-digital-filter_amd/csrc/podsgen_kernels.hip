@@ -16,6 +16,13 @@
 
 namespace pods {
 
+// Snapshot matrix layout ("K-tiled"): element (snapshot i, row r of the reference A) lives at
+// AT[((r / 16) * ns + i) * 16 + r % 16].  A K-tile of 16 rows of A for a panel of snapshots
+// i0..i0+n is then one contiguous block (SYRK operand = one 16 KB chunk per 128 snapshots).
+__device__ __forceinline__ int64_t at_off(int64_t r, int64_t i, int ns) {
+  return (((r >> 4) * ns + i) << 4) + (r & 15);
+}
+
 // -----------------------------------------------------------------------------------------
 // MT19937
 // -----------------------------------------------------------------------------------------
@@ -307,7 +314,7 @@ __global__ __launch_bounds__(512) void k_filter_yz(
 #pragma unroll
     for (int e = 0; e < 9; ++e) R9[e] = rot[e];
   }
-  double* dst = AT + (int64_t)i * rowlen;
+  (void)rowlen;
 #pragma unroll
   for (int m = 0; m < MAXO; ++m) {
     const int o = tid + m * nthr;
@@ -315,7 +322,7 @@ __global__ __launch_bounds__(512) void k_filter_yz(
     if (jj >= rows) continue;
     const int64_t p = (int64_t)(jt + jj) * K + k;
     if (lund_mode < 0) {
-      for (int c = 0; c < ncomp; ++c) dst[c * Pl + p] = res[c][m];
+      for (int c = 0; c < ncomp; ++c) AT[at_off(c * Pl + p, i, ns)] = res[c][m];
       continue;
     }
     const double xu = res[0][m], xv = res[1][m], xw = res[2][m];
@@ -338,9 +345,9 @@ __global__ __launch_bounds__(512) void k_filter_yz(
       v = vr;
       w = wr;
     }
-    dst[p] = u;
-    dst[Pl + p] = v;
-    dst[2 * Pl + p] = w;
+    AT[at_off(p, i, ns)] = u;
+    AT[at_off(Pl + p, i, ns)] = v;
+    AT[at_off(2 * Pl + p, i, ns)] = w;
   }
 }
 
@@ -361,28 +368,28 @@ __global__ __launch_bounds__(256) void k_mean(const double* __restrict__ AT, int
       stk[sp - 1] = stk[sp - 1] + bsum;
       continue;
     }
-    const double* a = AT + (int64_t)s * rowlen + r;
+    const double* a = AT + at_off(r, s, ns);  // consecutive snapshots are 16 doubles apart
     double res;
     if (n < 8) {
       res = 0.0;
-      for (int i = 0; i < n; ++i) res = res + a[(int64_t)i * rowlen];
+      for (int i = 0; i < n; ++i) res = res + a[(int64_t)i * 16];
     } else {
-      double r0 = a[0], r1 = a[rowlen], r2 = a[2 * rowlen], r3 = a[3 * rowlen];
-      double r4 = a[4 * rowlen], r5 = a[5 * rowlen], r6 = a[6 * rowlen], r7 = a[7 * rowlen];
+      double r0 = a[0], r1 = a[16], r2 = a[32], r3 = a[48];
+      double r4 = a[64], r5 = a[80], r6 = a[96], r7 = a[112];
       int i = 8;
       for (; i < n - (n % 8); i += 8) {
-        const double* b = a + (int64_t)i * rowlen;
+        const double* b = a + (int64_t)i * 16;
         r0 = r0 + b[0];
-        r1 = r1 + b[rowlen];
-        r2 = r2 + b[2 * rowlen];
-        r3 = r3 + b[3 * rowlen];
-        r4 = r4 + b[4 * rowlen];
-        r5 = r5 + b[5 * rowlen];
-        r6 = r6 + b[6 * rowlen];
-        r7 = r7 + b[7 * rowlen];
+        r1 = r1 + b[16];
+        r2 = r2 + b[32];
+        r3 = r3 + b[48];
+        r4 = r4 + b[64];
+        r5 = r5 + b[80];
+        r6 = r6 + b[96];
+        r7 = r7 + b[112];
       }
       res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-      for (; i < n; ++i) res = res + a[(int64_t)i * rowlen];
+      for (; i < n; ++i) res = res + a[(int64_t)i * 16];
     }
     stk[sp++] = res;
   }
@@ -394,79 +401,6 @@ __global__ __launch_bounds__(256) void k_mean(const double* __restrict__ AT, int
 // C[i][j] = sum_r (A_T[i][r]-m[r]) (A_T[j][r]-m[r]), lower-triangle tiles, mirrored.
 // -----------------------------------------------------------------------------------------
 typedef double f64x4 __attribute__((ext_vector_type(4)));
-
-template <int BT, int KT>
-__global__ __launch_bounds__(256) void k_syrk(const double* __restrict__ AT, int64_t ld, int ns,
-                                              int64_t Kdim, const double* __restrict__ mean,
-                                              int nb, double* __restrict__ C, int64_t ldc,
-                                              int divide) {
-  // BT x BT output tile; 4 waves as 2x2, each wave (BT/2)x(BT/2) = MB x MB 16x16 blocks
-  constexpr int MB = BT / 32;
-  __shared__ double Xs[BT][KT + 1];
-  __shared__ double Ys[BT][KT + 1];
-  // lower-triangle tile id -> (bi, bj), bi >= bj
-  const int t = blockIdx.x;
-  int bi = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
-  while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
-  while (bi * (bi + 1) / 2 > t) --bi;
-  const int bj = t - bi * (bi + 1) / 2;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int i0 = bi * BT, j0 = bj * BT;
-  f64x4 acc[MB][MB];
-#pragma unroll
-  for (int m = 0; m < MB; ++m)
-#pragma unroll
-    for (int n = 0; n < MB; ++n) acc[m][n] = (f64x4){0.0, 0.0, 0.0, 0.0};
-  constexpr int ELEMS = BT * KT / 256;  // per thread per operand
-  for (int64_t k0 = 0; k0 < Kdim; k0 += KT) {
-#pragma unroll
-    for (int e = 0; e < ELEMS; ++e) {
-      const int idx = tid + e * 256;
-      const int row = idx / KT, kk = idx % KT;
-      const int64_t k = k0 + kk;
-      double xv = 0.0, yv = 0.0;
-      if (k < Kdim) {
-        const double mk = mean[k];
-        if (i0 + row < ns) xv = AT[(int64_t)(i0 + row) * ld + k] - mk;
-        if (j0 + row < ns) yv = AT[(int64_t)(j0 + row) * ld + k] - mk;
-      }
-      Xs[row][kk] = xv;
-      Ys[row][kk] = yv;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < KT; kk += 4) {
-      double a[MB], b[MB];
-#pragma unroll
-      for (int m = 0; m < MB; ++m) a[m] = Xs[wr * (BT / 2) + m * 16 + (lane & 15)][kk + (lane >> 4)];
-#pragma unroll
-      for (int n = 0; n < MB; ++n) b[n] = Ys[wc * (BT / 2) + n * 16 + (lane & 15)][kk + (lane >> 4)];
-#pragma unroll
-      for (int m = 0; m < MB; ++m)
-#pragma unroll
-        for (int n = 0; n < MB; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b[n], acc[m][n], 0, 0, 0);
-    }
-    __syncthreads();
-  }
-  const double dn = (double)ns;
-#pragma unroll
-  for (int m = 0; m < MB; ++m)
-#pragma unroll
-    for (int n = 0; n < MB; ++n)
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int gi = i0 + wr * (BT / 2) + m * 16 + (lane >> 4) + 4 * reg;
-        const int gj = j0 + wc * (BT / 2) + n * 16 + (lane & 15);
-        if (gi < ns && gj < ns) {
-          double v = acc[m][n][reg];
-          if (divide) v = v / dn;
-          C[(int64_t)gi * ldc + gj] = v;
-          if (bi != bj) C[(int64_t)gj * ldc + gi] = v;
-        }
-      }
-}
 
 // Split-K SYRK, 128x128 tiles.  Work item = (lower-triangle tile, K split), dealt so that the
 // items one XCD runs back to back are neighbouring tiles of one split (T1 remap, bijective).
@@ -504,27 +438,24 @@ __global__ __launch_bounds__(256, 2) void k_syrk_split(const double* __restrict_
 #pragma unroll
     for (int n = 0; n < MB; ++n) acc[m][n] = (f64x4){0.0, 0.0, 0.0, 0.0};
   double2 xr[PPT], yr[PPT];
+  // K-tiled layout: the (panel, K-tile) operand is a contiguous BT x KT block; padded K
+  // columns are zero in both A and the mean, so no K guard is needed.
   auto load = [&](int64_t k0) {
+    const double* xb = AT + (((k0 >> 4) * ns + i0) << 4);
+    const double* yb = AT + (((k0 >> 4) * ns + j0) << 4);
 #pragma unroll
     for (int e = 0; e < PPT; ++e) {
       const int pidx = tid + e * 256;
       const int row = pidx / (KT / 2), kk = (pidx % (KT / 2)) * 2;
-      const int64_t k = k0 + kk;
+      const double2 m2 = *reinterpret_cast<const double2*>(mean + k0 + kk);
       double2 xv = make_double2(0.0, 0.0), yv = make_double2(0.0, 0.0);
-      if (k + 1 < ke) {
-        const double2 m2 = *reinterpret_cast<const double2*>(mean + k);
-        if (i0 + row < ns) {
-          const double2 a = *reinterpret_cast<const double2*>(AT + (int64_t)(i0 + row) * ld + k);
-          xv = make_double2(a.x - m2.x, a.y - m2.y);
-        }
-        if (j0 + row < ns) {
-          const double2 a = *reinterpret_cast<const double2*>(AT + (int64_t)(j0 + row) * ld + k);
-          yv = make_double2(a.x - m2.x, a.y - m2.y);
-        }
-      } else if (k < ke) {
-        const double mk = mean[k];
-        if (i0 + row < ns) xv.x = AT[(int64_t)(i0 + row) * ld + k] - mk;
-        if (j0 + row < ns) yv.x = AT[(int64_t)(j0 + row) * ld + k] - mk;
+      if (i0 + row < ns) {
+        const double2 a = *reinterpret_cast<const double2*>(xb + row * KT + kk);
+        xv = make_double2(a.x - m2.x, a.y - m2.y);
+      }
+      if (j0 + row < ns) {
+        const double2 a = *reinterpret_cast<const double2*>(yb + row * KT + kk);
+        yv = make_double2(a.x - m2.x, a.y - m2.y);
       }
       xr[e] = xv;
       yr[e] = yv;
@@ -578,6 +509,126 @@ __global__ __launch_bounds__(256, 2) void k_syrk_split(const double* __restrict_
             dst[(int64_t)gi * ldc + gj] = v;
           }
         }
+      }
+}
+
+// SYRK v2: one 256 x 128 tile per workgroup (one 512-thread workgroup per CU), operands
+// streamed by LDS-DMA (global_load_lds_dwordx4) into a 3-stage ring; counted vmcnt + raw
+// s_barrier keep two K-tiles in flight across barriers.  The K-tiled A makes each (panel,
+// K-tile) operand one contiguous block; rows are XOR-swizzled on the SOURCE address (double2
+// slot j of row R holds logical slot j ^ ((R>>1)&7)) so the MFMA fragment reads are
+// bank-conflict free.  The mean is subtracted while fragments are read (A stays uncentred).
+// 8 waves as 4 x 2, each 64 x 64 = 4 x 4 blocks of v_mfma_f64_16x16x4_f64.  Partial tiles
+// (lower triangle only) go to slab `split`; k_syrk_reduce sums the slabs in split order.
+namespace syrk2 {
+constexpr int BM = 256, BN = 128, KT = 16, NST = 3, NW = 8;
+constexpr int XB = BM * KT * 8;            // 32 KB
+constexpr int YB = BN * KT * 8;            // 16 KB
+constexpr int MBYTES = NW * 128;           // one 16-double mean slot per wave
+constexpr int STAGE = XB + YB + MBYTES;    // 49 KB
+constexpr int XP = XB / 1024 / NW;         // LDS-DMA pieces per wave per stage: 4
+constexpr int YP = YB / 1024 / NW;         //                                    2
+}  // namespace syrk2
+
+__device__ __forceinline__ void glds16(const void* src, uint32_t lds_byte_addr) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(uintptr_t)lds_byte_addr,
+                                   16, 0, 0);
+}
+
+__global__ __launch_bounds__(512, 1) void k_syrk_glds(const double* __restrict__ AT, int ns,
+                                                      int64_t Kdim, const double* __restrict__ mean,
+                                                      const int4* __restrict__ items, int nitems,
+                                                      int64_t ksplit, double* __restrict__ work,
+                                                      int64_t ldc, int64_t slab) {
+  using namespace syrk2;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int b = blockIdx.x;
+  const int xcd = b & 7, qq = nitems >> 3, rr = nitems & 7;
+  const int logical = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
+  const int4 it = items[logical];
+  const int bi = it.x, bj = it.y, sp = it.z;
+  const int i0 = bi * BM, j0 = bj * BN;
+  const int64_t kt0 = (int64_t)sp * (ksplit / KT);
+  const int64_t kt1 = min(Kdim, (int64_t)(sp + 1) * ksplit) / KT;
+  const int nt = (int)(kt1 - kt0);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave >> 1, wc = wave & 1;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+  // LDS-DMA piece q of this wave covers 8 rows of 128 B; lane -> (row R, 16-B slot)
+  const int lrow = lane >> 3, lslot = lane & 7;
+  int64_t xsrc[XP], ysrc[YP];  // per-lane source offsets (doubles) inside one K-tile block
+#pragma unroll
+  for (int q = 0; q < XP; ++q) {
+    const int R = (wave * XP + q) * 8 + lrow;
+    xsrc[q] = ((int64_t)min(i0 + R, ns - 1) << 4) + ((lslot ^ ((R >> 1) & 7)) << 1);
+  }
+#pragma unroll
+  for (int q = 0; q < YP; ++q) {
+    const int R = (wave * YP + q) * 8 + lrow;
+    ysrc[q] = ((int64_t)min(j0 + R, ns - 1) << 4) + ((lslot ^ ((R >> 1) & 7)) << 1);
+  }
+  const int64_t blk = (int64_t)ns << 4;  // doubles per K-tile block
+  auto issue = [&](int t) {
+    const int64_t kt = kt0 + t;
+    const uint32_t base = lds0 + (uint32_t)((t % NST) * STAGE);
+    const double* g = AT + kt * blk;
+#pragma unroll
+    for (int q = 0; q < XP; ++q) glds16(g + xsrc[q], base + (wave * XP + q) * 1024);
+#pragma unroll
+    for (int q = 0; q < YP; ++q) glds16(g + ysrc[q], base + XB + (wave * YP + q) * 1024);
+    // mean K-tile: 16 doubles = lanes 0..7 x 16 B (an LDS-DMA writes base + 16*lane for each
+    // active lane, so the other lanes must be masked off)
+    if (lane < 8) glds16(mean + kt * KT + (lane << 1), base + XB + YB + wave * 128);
+  };
+  f64x4 acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = (f64x4){0.0, 0.0, 0.0, 0.0};
+  if (nt > 0) issue(0);
+  if (nt > 1) issue(1);
+  // fragment offsets: row R = base + 16*m + fr, swizzle (R>>1)&7 = (fr>>1)&7 for every m
+  const int fr = lane & 15, fk = lane >> 4, fs = (fr >> 1) & 7;
+  const int xrow = (wr * 64 + fr) << 4, yrow = (wc * 64 + fr) << 4;
+  for (int t = 0; t < nt; ++t) {
+    if (t + 1 < nt)
+      asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 2 < nt) issue(t + 2);
+    const char* st = smem + (t % NST) * STAGE;
+    const double* Xs = reinterpret_cast<const double*>(st);
+    const double* Ys = reinterpret_cast<const double*>(st + XB);
+    const double* Ms = reinterpret_cast<const double*>(st + XB + YB + wave * 128);
+#pragma unroll
+    for (int kk = 0; kk < KT; kk += 4) {
+      const int k = kk + fk;
+      const int koff = ((((k >> 1) ^ fs)) << 1) + (k & 1);
+      const double mk = Ms[k];
+      double a[4], bv[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) a[m] = Xs[xrow + koff + m * 256] - mk;
+#pragma unroll
+      for (int n = 0; n < 4; ++n) bv[n] = Ys[yrow + koff + n * 256] - mk;
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], bv[n], acc[m][n], 0, 0, 0);
+    }
+  }
+  double* dst = work + (int64_t)sp * slab;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int gi = i0 + wr * 64 + m * 16 + fk + 4 * reg;
+        const int gj = j0 + wc * 64 + n * 16 + fr;
+        if (gi < ns && gj <= gi) dst[(int64_t)gi * ldc + gj] = acc[m][n][reg];
       }
 }
 
@@ -653,7 +704,7 @@ __global__ __launch_bounds__(256) void k_spatial_modes(const double* __restrict_
     if (valid) {
       const int lim = min(CH, ns - i0);
       for (int ii = 0; ii < lim; ++ii) {
-        const double a = AT[(int64_t)(i0 + ii) * rowlen + r] - mr;
+        const double a = AT[at_off(r, i0 + ii, ns)] - mr;
 #pragma unroll
         for (int m = 0; m < NMB; ++m) acc[m] = __builtin_fma(a, Ts[ii][m], acc[m]);
       }
@@ -847,34 +898,69 @@ hipError_t launch_mean(const double* AT, int64_t rowlen, int ns, const int* prog
   return hipGetLastError();
 }
 
-int syrk_plan(int ns, int64_t Kdim, int64_t* ksplit) {
-  constexpr int BT = 128, KT = 16;
-  const int nb = (ns + BT - 1) / BT;
-  const int tiles = nb * (nb + 1) / 2;
-  const int slots = 512;  // 256 CUs x 2 workgroups
-  // ~8 rounds of work items; one split per XCD when that many fit
-  int64_t nsplit = (8LL * slots + tiles - 1) / tiles;
-  if (nsplit > 8) nsplit = ((nsplit + 7) / 8) * 8;
-  const int64_t maxsplit = std::max<int64_t>(1, Kdim / (KT * 64));
-  nsplit = std::min(nsplit, maxsplit);
-  int64_t ks = (Kdim + nsplit - 1) / nsplit;
-  ks = ((ks + KT - 1) / KT) * KT;
-  nsplit = (Kdim + ks - 1) / ks;
+// Number of K splits for `tiles` work tiles on `slots` concurrent workgroups: ~8+ rounds,
+// chosen to minimise the partial last round, >= 64 K-tiles of 16 per item.
+int syrk_plan(int kernel, int ns, int64_t Kdim, int64_t* ksplit) {
+  constexpr int KT = 16;
+  int tiles, slots;
+  if (kernel == 2) {
+    const int nbi = (ns + 255) / 256, nbj = (ns + 127) / 128;
+    tiles = 0;
+    for (int bi = 0; bi < nbi; ++bi) tiles += std::min(2 * bi + 2, nbj);
+    slots = 256;
+  } else {
+    const int nb = (ns + 127) / 128;
+    tiles = nb * (nb + 1) / 2;
+    slots = 512;
+  }
+  const int64_t kts = Kdim / KT;
+  const int64_t maxsplit = std::max<int64_t>(1, kts / 64);
+  int64_t best = 1;
+  double best_cost = 1e300;
+  for (int64_t s = 1; s <= std::min<int64_t>(maxsplit, 32); ++s) {
+    const int64_t items = (int64_t)tiles * s;
+    const double rounds = std::ceil((double)items / slots);
+    // time ~ rounds * (work per item) + small per-split reduce cost
+    const double cost = rounds / (double)s + 0.002 * s;
+    if (cost < best_cost - 1e-12) {
+      best_cost = cost;
+      best = s;
+    }
+  }
+  int64_t ks = (kts + best - 1) / best * KT;
+  const int64_t nsplit = (Kdim + ks - 1) / ks;
   *ksplit = ks;
   return (int)std::max<int64_t>(1, nsplit);
 }
 
-int syrk_tile() { return 128; }
 
-hipError_t launch_syrk(const double* AT, int64_t ld, int ns, int64_t Kdim, const double* mean,
-                       const int* items, int nitems, int nsplit, int64_t ksplit, double* C,
-                       int64_t ldc, int divide, double* work, hipStream_t st) {
-  constexpr int BT = 128, KT = 16;
+hipError_t launch_syrk(int kernel, const double* AT, int64_t ld, int ns, int64_t Kdim,
+                       const double* mean, const int* items, int nitems, int nsplit, int64_t ksplit,
+                       double* C, int64_t ldc, int divide, double* work, hipStream_t st) {
   const int64_t slab = (int64_t)ns * ldc;
   const int final_write = nsplit == 1;
-  hipLaunchKernelGGL((k_syrk_split<BT, KT>), dim3(nitems), dim3(256), 0, st, AT, ld, ns, Kdim, mean,
-                     reinterpret_cast<const int4*>(items), nitems, ksplit, final_write ? C : work, ldc,
-                     slab, final_write, divide);
+  if (kernel == 2) {
+    static bool attr = false;
+    if (!attr) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_syrk_glds),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         syrk2::NST * syrk2::STAGE);
+      if (e != hipSuccess) return e;
+      attr = true;
+    }
+    hipLaunchKernelGGL(k_syrk_glds, dim3(nitems), dim3(512), syrk2::NST * syrk2::STAGE, st, AT, ns, Kdim,
+                       mean, reinterpret_cast<const int4*>(items), nitems, ksplit, work, ldc, slab);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_syrk_reduce, dim3((ns + 255) / 256, ns), dim3(256), 0, st, work, nsplit, slab,
+                       ns, ldc, C, divide);
+    return hipGetLastError();
+  } else {
+    constexpr int BT = 128, KT = 16;
+    hipLaunchKernelGGL((k_syrk_split<BT, KT>), dim3(nitems), dim3(256), 0, st, AT, ld, ns, Kdim, mean,
+                       reinterpret_cast<const int4*>(items), nitems, ksplit, final_write ? C : work, ldc,
+                       slab, final_write, divide);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || final_write) return e;
   hipLaunchKernelGGL(k_syrk_reduce, dim3((ns + 255) / 256, ns), dim3(256), 0, st, work, nsplit, slab,

@@ -80,11 +80,12 @@ class DeviceSnapshots:
         return p.value
 
     def to_host_T(self):
-        """A_T as a host (ns, 3*P_local) array."""
-        out = np.empty((self.ns, self.rowlen), dtype=np.float64)
-        check(self.ctx.lib.pods_copy(self.ctx.h, ptr(out), ctypes.c_void_p(self.data_ptr()),
-                                     out.nbytes, 1), "pods_copy")
-        return out
+        """A_T as a host (ns, 3*P_local) array (device layout is K-tiled, see podsgen.h)."""
+        rowpad = (self.rowlen + 15) // 16 * 16
+        raw = np.empty((rowpad // 16, self.ns, 16), dtype=np.float64)
+        check(self.ctx.lib.pods_copy(self.ctx.h, ptr(raw), ctypes.c_void_p(self.data_ptr()),
+                                     raw.nbytes, 1), "pods_copy")
+        return np.ascontiguousarray(raw.transpose(1, 0, 2).reshape(self.ns, rowpad)[:, :self.rowlen])
 
     def to_host(self):
         """The reference layout A (3*P_local, ns)."""
