@@ -104,6 +104,10 @@ int pods_copy(pods_ctx* ctx, void* dst, const void* src, size_t bytes, int kind)
  * mean_out (3*P_local doubles) may be NULL. */
 int pods_mean(pods_ctx* ctx, double* mean_out, int out_is_device);
 
+/* Set the mean the correlation / spatial-mode kernels subtract (mean_host: row_len doubles,
+ * NULL = zeros, i.e. A is already centred -- PODFS.calculate_correlation_matrix, PODFS.py:1451). */
+int pods_set_mean(pods_ctx* ctx, const double* mean_host);
+
 /* Correlation C = (A-m)^T (A-m) [/ns] (PODFS.py:1451-1455).  C_dev: ns x ns row-major,
  * full symmetric.  divide = 1 divides by ns (single device); multi-device callers pass 0,
  * all-reduce the partials, then call pods_divide_inplace(C, ns*ns, ns). */
@@ -137,6 +141,11 @@ int pods_fourier(pods_ctx* ctx, const double* T_dev, int ldT, int nm, int ns,
 int pods_filter_block(pods_ctx* ctx, const double* x_host, int nfx, int nfy, int nfz, int jma,
                       int kma, const double* bx, const double* by, const double* bz,
                       double* y_host);
+/* adapt1d / adapt2prf (:143-231) and/or rotate_velocity (:1119-1131) on one step's fields
+ * yu, yv, yw (P doubles each, host, updated in place).  lund_host: 9 x P rows as in
+ * pods_df_configure (ignored for PODS_LUND_NONE); rot_host: 3x3 row-major or NULL. */
+int pods_lund_apply(pods_ctx* ctx, double* yu, double* yv, double* yw, int64_t P,
+                    const double* lund_host, int lund_mode, const double* rot_host);
 /* The first n doubles of np.random.RandomState(seed).uniform(low, low+range) computed
  * on the device with jump-ahead substreams; out_dev: n doubles. */
 int pods_rng_uniform(pods_ctx* ctx, uint32_t seed, int64_t n, double low, double range,

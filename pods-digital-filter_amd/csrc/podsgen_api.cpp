@@ -527,6 +527,57 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
   PODS_CATCH
 }
 
+int pods_set_mean(pods_ctx* c, const double* mean_host) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!c->have_snapshots) return fail(PODS_ERR_STATE, "pods_set_mean before snapshots exist");
+  PODS_HIP(hipSetDevice(c->device));
+  PODS_HIP(hipMemsetAsync(c->mean.p, 0, (size_t)c->rowpad * sizeof(double), c->stream));
+  if (mean_host) {
+    PODS_HIP(hipMemcpyAsync(c->mean.p, mean_host, (size_t)c->rowlen * sizeof(double),
+                            hipMemcpyHostToDevice, c->stream));
+    PODS_HIP(hipStreamSynchronize(c->stream));
+  }
+  c->mean_valid = true;
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_lund_apply(pods_ctx* c, double* yu, double* yv, double* yw, int64_t P, const double* lund,
+                    int lund_mode, const double* rot) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!yu || !yv || !yw || P <= 0) return fail(PODS_ERR_ARG, "bad fields");
+  if (lund_mode >= 0 && !lund) return fail(PODS_ERR_ARG, "lund_host is null");
+  PODS_HIP(hipSetDevice(c->device));
+  DevBuf d;
+  const size_t fb = (size_t)P * sizeof(double);
+  hipError_t e = ensure(d, 3 * fb + 9 * fb + 9 * sizeof(double));
+  if (e) return fail(PODS_ERR_NOMEM, "device allocation failed");
+  double* base = d.as<double>();
+  double* du = base;
+  double* dv = base + P;
+  double* dw = base + 2 * P;
+  double* dl = base + 3 * P;
+  double* dr = base + 12 * P;
+  double r9[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+  if (rot) std::memcpy(r9, rot, sizeof(r9));
+  if (!e) e = hipMemcpy(du, yu, fb, hipMemcpyHostToDevice);
+  if (!e) e = hipMemcpy(dv, yv, fb, hipMemcpyHostToDevice);
+  if (!e) e = hipMemcpy(dw, yw, fb, hipMemcpyHostToDevice);
+  if (!e && lund_mode >= 0) e = hipMemcpy(dl, lund, 9 * fb, hipMemcpyHostToDevice);
+  if (!e) e = hipMemcpy(dr, r9, sizeof(r9), hipMemcpyHostToDevice);
+  if (!e) e = pods::launch_lund_apply(du, dv, dw, P, dl, lund_mode, dr, rot ? 1 : 0, c->stream);
+  if (!e) e = hipStreamSynchronize(c->stream);
+  if (!e) e = hipMemcpy(yu, du, fb, hipMemcpyDeviceToHost);
+  if (!e) e = hipMemcpy(yv, dv, fb, hipMemcpyDeviceToHost);
+  if (!e) e = hipMemcpy(yw, dw, fb, hipMemcpyDeviceToHost);
+  release(d);
+  if (e) return fail(PODS_ERR_HIP, std::string("lund_apply: ") + hipGetErrorString(e));
+  return PODS_OK;
+  PODS_CATCH
+}
+
 int pods_divide_inplace(pods_ctx* c, double* x, int64_t n, double d) {
   if (int e = check_ctx(c)) return e;
   PODS_HIP(pods::launch_divide(x, n, d, c->stream));

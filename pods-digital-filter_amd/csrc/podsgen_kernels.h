@@ -19,6 +19,8 @@ hipError_t launch_filter_yz(int NY, const double* T1, const double* by, const do
                             const double* lund, int lund_mode, const double* rot, int rotate,
                             double* AT, int64_t rowlen, hipStream_t st);
 int filter_yz_max_K(int Kp);
+hipError_t launch_lund_apply(double* yu, double* yv, double* yw, int64_t P, const double* lund,
+                             int lund_mode, const double* rot, int rotate, hipStream_t st);
 hipError_t launch_mean(const double* AT, int64_t rowlen, int ns, const int* prog, int nprog,
                        double* mean, hipStream_t st);
 // SYRK kernels: 1 = 128x128 register-staged (k_syrk_split), 2 = 256x128 LDS-DMA (k_syrk_glds).

@@ -351,6 +351,46 @@ __global__ __launch_bounds__(512) void k_filter_yz(
   }
 }
 
+// Stand-alone Lund transform + rotation on one step's (yu, yv, yw) fields (the operator API
+// adapt1d / adapt2prf / rotate_velocity called on their own); same expressions as k_filter_yz.
+__global__ void k_lund_apply(double* __restrict__ yu, double* __restrict__ yv, double* __restrict__ yw,
+                             int64_t P, const double* __restrict__ lund, int lund_mode,
+                             const double* __restrict__ rot, int rotate) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  double u = yu[p], v = yv[p], w = yw[p];
+  if (lund_mode >= 0) {
+    const double xu = u, xv = v, xw = w;
+    const double a00 = lund[0 * P + p], a10 = lund[1 * P + p], a11 = lund[2 * P + p];
+    const double a20 = lund[3 * P + p], a21 = lund[4 * P + p], a22 = lund[5 * P + p];
+    u = ((a00 * xu + 0.0 * xv) + 0.0 * xw) + lund[6 * P + p];
+    v = (a10 * xu + a11 * xv) + 0.0 * xw;
+    w = (a20 * xu + a21 * xv) + a22 * xw;
+    if (lund_mode == 1) {
+      v = v + lund[7 * P + p];
+      w = w + lund[8 * P + p];
+    }
+  }
+  if (rotate) {
+    const double ur = __builtin_fma(rot[2], w, __builtin_fma(rot[0], u, rot[1] * v));
+    const double vr = __builtin_fma(rot[5], w, __builtin_fma(rot[3], u, rot[4] * v));
+    const double wr = __builtin_fma(rot[8], w, __builtin_fma(rot[6], u, rot[7] * v));
+    u = ur;
+    v = vr;
+    w = wr;
+  }
+  yu[p] = u;
+  yv[p] = v;
+  yw[p] = w;
+}
+
+hipError_t launch_lund_apply(double* yu, double* yv, double* yw, int64_t P, const double* lund,
+                             int lund_mode, const double* rot, int rotate, hipStream_t st) {
+  hipLaunchKernelGGL(k_lund_apply, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st, yu, yv, yw, P, lund,
+                     lund_mode, rot, rotate);
+  return hipGetLastError();
+}
+
 // -----------------------------------------------------------------------------------------
 // mean over snapshots: numpy pairwise program (leaf = (start,len), add = (-1, 0))
 // -----------------------------------------------------------------------------------------

@@ -120,6 +120,7 @@ class DFSetup:
     mean_profile: str = "hyperbolic-tangent"
     turb_profile: str = "top-hat"
     prf: Optional[dict] = None          # (jma,kma) arrays U,V,W,uu,vv,ww,uv,uw,vw -> adapt2prf
+    profile1d: Optional[dict] = None    # (kma,) arrays U,uu,vv,ww,uw from read_profile -> adapt1d
     nfx: int = field(default=0, init=False)
     nfy: int = field(default=0, init=False)
     nfz: int = field(default=0, init=False)
@@ -141,7 +142,10 @@ class DFSetup:
         nrm = np.sqrt(n1[0] ** 2 + n1[1] ** 2 + n1[2] ** 2)
         self.n_unit = (n1[0] / nrm, n1[1] / nrm, n1[2] / nrm)
         V = W = 0
-        if self.prf is None:
+        if self.prf is None and self.profile1d is not None:
+            self.profile = {k: np.array(self.profile1d[k], dtype=np.float64) for k in ("U", "uu", "vv", "ww", "uw")}
+            U = self.profile["U"]
+        elif self.prf is None:
             U, uu, vv, ww, uw = build_profile(self.mean_profile, self.turb_profile,
                                               self.bulk_velocity, self.u_dash, self.kma)
             self.profile = dict(U=np.asarray(U, dtype=np.float64), uu=uu, vv=vv, ww=ww, uw=uw)
@@ -170,7 +174,7 @@ class DFSetup:
     @property
     def rotated(self):
         """main() rotates only when the profile was built, not read (:1476)."""
-        return self.prf is None
+        return self.prf is None and self.profile1d is None
 
     def taps(self):
         return (calccoeff(self.nfx, self.lnx), calccoeff(self.nfy, self.lny),
@@ -189,7 +193,8 @@ class DFSetup:
         pr = self.profile
         out = np.zeros((9, J, K))
         if self.prf is None:
-            fac = lund1d_factor(pr["uu"], pr["vv"], pr["ww"], pr["uw"])
+            fac = lund1d_factor(*(np.broadcast_to(np.asarray(pr[k], dtype=np.float64), (K,))
+                                  for k in ("uu", "vv", "ww", "uw")))
             for r, v in enumerate(fac):
                 out[r] = np.broadcast_to(np.asarray(v, dtype=np.float64), (K,))[None, :]
             out[6] = pr["U"][None, :]

@@ -1,0 +1,153 @@
+"""GPU: the reference-facing modules (digitalfilters.py / PODFS.py / HDF5.py) end to end,
+the per-call operator API, and the sharded (multi-rank) pipeline on one device."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+from oracle import pods_oracle as O  # noqa: E402
+
+
+def _parse_podfs_dat(text):
+    lines = text.split("\n")
+    nm = int(lines[0])
+    period = float(lines[1])
+    counts = [int(l.split("\t")[1]) for l in lines[2:2 + nm]]
+    rows = np.array([[float(x) for x in l.split("\t")] for l in lines[2 + nm:]]).reshape(-1, 3)
+    return nm, period, counts, rows
+
+
+def test_main_end_to_end_cli_case(golden_dir, tmp_path, monkeypatch):
+    """python digitalfilters.py -n 5 --seed 7 (the quickstart example) vs the reference run."""
+    import digitalfilters as df
+    g = np.load(os.path.join(golden_dir, "cli_10x11x5.npz"))
+    monkeypatch.chdir(tmp_path)
+    i_d = df.main(["-n", "5", "--seed", "7", "-5"])
+    # PODFS.dat: same counts and ranks; coefficients equal up to the per-mode eigenvector sign
+    nm, period, counts, rows = _parse_podfs_dat(open("PODFS/PODFS.dat").read())
+    nm_g, period_g, counts_g, rows_g = _parse_podfs_dat(str(g["podfs_dat"]))
+    assert (nm, counts) == (nm_g, counts_g) and period == period_g
+    assert np.array_equal(rows[:, 0], rows_g[:, 0])
+    start = 0
+    for c in counts:
+        blk, ref = rows[start:start + c, 1:], rows_g[start:start + c, 1:]
+        s = np.sign(np.sum(blk * ref))
+        assert np.max(np.abs(s * blk - ref)) <= 2e-6 * np.max(np.abs(ref)), start
+        start += c
+    ev = np.loadtxt("PODFS/POD.eigenvalues.dat")
+    ev_g = np.loadtxt(__import__("io").StringIO(str(g["eigenvalues_dat"])))
+    assert ev.shape == ev_g.shape
+    assert np.max(np.abs(ev[:, 1] - ev_g[:, 1])) <= 1e-12 * ev_g[0, 1]
+    # mean field is bit-exact, so PODFS_mean.prf is too
+    import PODFS
+    import nsigproclib as sp
+    pts = PODFS.cell_centres(10, 11, 0.1)
+    u = g["mean_field"].reshape((110, 3), order="F")
+    body = "".join(",".join(sp.str(v) for v in (*pts[j], *u[j])) + "\n" for j in range(110))
+    assert open("PODFS/PODFS_mean.prf").read().endswith(body)
+    assert os.path.exists("PODFS/PODFS_mode_0004.prf") and not os.path.exists("PODFS/PODFS_mode_0005.prf")
+    import HDF5
+    if HDF5._h5py_python() is not None:
+        assert os.path.getsize("PODFS/PODFS.hdf5") > 0
+    assert i_d.nm == 4
+
+
+def test_operator_api_bit_exact(golden_dir):
+    import digitalfilters as df
+    g = np.load(os.path.join(golden_dir, "unit_filter.npz"))
+    y = np.zeros((7, 5))
+    df.filter3DSciPy1D(g["x"], y, None, 7, 5, 4.5, 3.0, 2.0, 9, 6, 4)
+    assert np.array_equal(y, g["y"])
+    rng = np.random.default_rng(5)
+    J, K = 6, 9
+    yu, yv, yw = (rng.standard_normal((J, K)) for _ in range(3))
+    U, uu, vv, ww, uw = O.build_profile("hyperbolic-tangent", "top-hat", 1.0, 0.02, K)
+    uw = 0.3 * np.sqrt(uu * ww)
+    ref = [a.copy() for a in (yu, yv, yw)]
+    O.adapt1d_loops(*ref, U, uu, vv, ww, uw, J, K)
+    got = [a.copy() for a in (yu, yv, yw)]
+    df.adapt1d(*got, U, uu, vv, ww, uw, J, K)
+    assert all(np.array_equal(a, b) for a, b in zip(got, ref))
+    prf = {k: rng.uniform(0.1, 1.0, (J, K)) for k in ("U", "V", "W", "uu", "vv", "ww")}
+    prf.update(uv=0.2 * rng.standard_normal((J, K)), uw=0.1 * rng.standard_normal((J, K)),
+               vw=0.1 * rng.standard_normal((J, K)))
+    co = O.lundprf_coeffs(prf["uu"], prf["vv"], prf["ww"], prf["uv"], prf["uw"], prf["vw"])
+    ref = O.apply_lund(yu, yv, yw, co, prf["U"], prf["V"], prf["W"])
+    got = [a.copy() for a in (yu, yv, yw)]
+    df.adapt2prf(*got, prf["U"], prf["V"], prf["W"], prf["uu"], prf["vv"], prf["ww"], prf["uv"], prf["uw"],
+                 prf["vw"], J, K)
+    assert all(np.array_equal(a, b) for a, b in zip(got, ref))
+    col = rng.standard_normal(3 * J * K)
+    n = np.array([0.3, -0.5, 0.8]) / np.linalg.norm([0.3, -0.5, 0.8])
+    assert np.array_equal(df.rotate_velocity(col, *n), O.rotate_velocity(col, O.rotation_matrix(*n)))
+
+
+def test_pod_on_host_array_matches_reference(golden_dir):
+    """PODFS.POD called like the reference (host A, already mean-subtracted)."""
+    import PODFS
+    g = np.load(os.path.join(golden_dir, "odd_12x9x17_aniso.npz"))
+    Ac = g["A_raw"] - g["mean_field"][:, None]
+
+    class I:
+        verbose = False
+    i_d = I()
+    PODFS.POD(Ac, 17, 108, 3, "false", [], "", "false", 1e-15, 20, 0, "false", "false", None, None,
+              float(g["dt"]), "velocity", 1, 17, 1, 1, i_d)
+    assert i_d.nm == int(g["nm"])
+    lam = g["energy"].real
+    assert np.max(np.abs(i_d.energy - lam)) <= 1e-12 * lam[0]
+    C = np.zeros((17, 17))
+    PODFS.calculate_correlation_matrix(17, 108, 3, "false", [], Ac, C)
+    assert np.max(np.abs(C - g["C"])) <= 1e-12 * np.max(np.abs(g["C"]))
+
+
+def _rank_worker(rank, world, port, out):
+    import torch.distributed as dist
+    import podsgen
+    from podsgen import engine as E
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    s = podsgen.DFSetup(jma=40, kma=24, ns=48, seed=31)
+    gen, pod, fo = E.pipeline(s, device=0, dist=dist)
+    out[rank] = dict(j0=gen.j0, j1=gen.j1, energy=pod.energy, nm=pod.nm, phi=pod.phi.cpu().numpy(),
+                     mean=pod.mean.cpu().numpy(), c=None if fo is None else fo.c)
+    dist.destroy_process_group()
+
+
+def test_sharded_pipeline_two_ranks_one_device():
+    """Row slabs on 2 ranks (gloo transport, one GPU) == the single-rank pipeline."""
+    import multiprocessing as mp
+    import podsgen
+    from podsgen import engine as E
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = 29600 + os.getpid() % 1000
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_rank_worker, args=(r, 2, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+        assert p.exitcode == 0
+    s = podsgen.DFSetup(jma=40, kma=24, ns=48, seed=31)
+    gen, pod, fo = E.pipeline(s, device=0)
+    lam = pod.energy
+    assert np.max(np.abs(out[0]["energy"] - lam)) <= 1e-12 * lam[0]
+    phi = pod.phi.cpu().numpy()
+    mean = pod.mean.cpu().numpy()
+    P, K = s.P, s.kma
+    for r in range(2):
+        d = out[r]
+        pl = (d["j1"] - d["j0"]) * K
+        for comp in range(3):
+            rows = slice(comp * P + d["j0"] * K, comp * P + d["j1"] * K)
+            assert np.array_equal(d["mean"][comp * pl:(comp + 1) * pl], mean[rows])
+            for m in range(pod.nm):
+                a = d["phi"][comp * pl:(comp + 1) * pl, m]
+                b = phi[rows, m]
+                sg = np.sign(np.dot(phi[:, m], phi[:, m]))  # same sign convention on both runs?
+                assert np.max(np.abs(np.abs(a) - np.abs(b))) <= 1e-10 * np.max(np.abs(phi[:, m])) * sg
+    assert np.max(np.abs(np.abs(out[0]["c"]) - np.abs(fo.c))) <= 1e-6 * np.max(np.abs(fo.c))

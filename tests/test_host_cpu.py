@@ -1,0 +1,208 @@
+"""CPU tests: host-side setup vs the oracle, library symbols, MT jump math, formats,
+CLI, HDF5 layout, and the multi-rank decomposition with gloo (world size 2)."""
+import ctypes
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import pods_oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_header_symbol():
+    from podsgen import _lib
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    hdr = open(os.path.join(ROOT, "include", "podsgen.h")).read()
+    names = set(re.findall(r"^\s*(?:int|const char\*)\s+(pods_\w+)\s*\(", hdr, re.M))
+    assert len(names) >= 20
+    for n in sorted(names):
+        assert hasattr(lib, n), n
+        assert n in _lib.SIGNATURES, n
+    assert _lib.load().pods_abi_version() == 1
+
+
+@pytest.mark.parametrize("seed,nblocks", [(0, 2), (12345, 3), (7, 1000), (2 ** 32 - 1, 65537)])
+def test_host_mt_jump_math(seed, nblocks):
+    from podsgen import _lib
+    lib = _lib.load()
+    assert lib.pods_host_mt_charpoly_degree() == 19937
+    assert lib.pods_host_mt_jump_check(seed, nblocks) == 0, lib.pods_last_error()
+
+
+@pytest.mark.parametrize("kw", [dict(jma=12, kma=9, ns=17, seed=3, dt=0.05),
+                                dict(jma=10, kma=11, ns=5, seed=7),
+                                dict(jma=6, kma=7, ns=6, seed=5, normal=(1.0, 1.0, 0.5))])
+def test_setup_matches_oracle(kw):
+    import podsgen
+    s = podsgen.DFSetup(**kw)
+    c = O.DFConfig(**kw)
+    assert (s.nfx, s.nfy, s.nfz) == (c.nfx, c.nfy, c.nfz)
+    assert s.dt_eff == c.dt_eff and s.lnx == c.lnx
+    for a, b in zip(s.taps(), (O.calccoeff(c.nfx, c.lnx), O.calccoeff(c.nfy, c.lny), O.calccoeff(c.nfz, c.lnz))):
+        assert np.array_equal(a, b)
+    assert np.array_equal(s.lund_rows(), O.lund_point_coeffs(c))
+    assert np.array_equal(s.rotation(), O.rotation_matrix(*c.n_unit))
+
+
+def test_lund_rows_slab():
+    import podsgen
+    s = podsgen.DFSetup(jma=9, kma=5, ns=3)
+    full = s.lund_rows()
+    parts = [s.lund_rows(*podsgen.row_slab(9, r, 4)) for r in range(4)]
+    assert np.array_equal(np.concatenate([p.reshape(9, -1, 5) for p in parts], axis=1).reshape(9, -1), full)
+
+
+@pytest.mark.parametrize("J,world", [(256, 1), (256, 8), (10, 3), (7, 7), (512, 8)])
+def test_row_slab_partition(J, world):
+    import podsgen
+    slabs = [podsgen.row_slab(J, r, world) for r in range(world)]
+    assert slabs[0][0] == 0 and slabs[-1][1] == J
+    assert all(a[1] == b[0] for a, b in zip(slabs, slabs[1:]))
+    assert max(b - a for a, b in slabs) - min(b - a for a, b in slabs) <= 1
+
+
+def test_rank_and_count_matches_oracle():
+    import podsgen
+    rng = np.random.default_rng(1)
+    for ns in (5, 64, 257):
+        c = (rng.standard_normal(ns) + 1j * rng.standard_normal(ns)).astype(np.complex64)
+        c[ns // 2 + 1:] = np.conj(c[1:ns - ns // 2][::-1])[:len(c[ns // 2 + 1:])]  # conjugate ties
+        for et in (0.5, 0.9, 0.99):
+            a, n = podsgen.rank_and_count(c, et)
+            b, m = O.rank_and_count(c, et)
+            assert np.array_equal(a, b) and n == m
+
+
+def test_num_valid_modes_closed_form():
+    import podsgen
+    rng = np.random.default_rng(2)
+    for ns in (3, 4, 5, 17, 64):
+        for _ in range(20):
+            lam = np.sort(rng.standard_normal(ns) * 10 ** rng.uniform(-40, 0, ns))[::-1]
+            lam[0] = abs(lam[0]) + 1.0
+            assert podsgen.num_valid_modes(lam, ns) == O.num_valid_modes(lam, ns)
+
+
+def test_text_formats_match_oracle(golden_dir):
+    import PODFS
+    g = np.load(os.path.join(golden_dir, "cli_10x11x5.npz"))
+    # PODFS.dat writer on the golden coefficients reproduces the reference's file
+    Ac = g["A_raw"] - g["mean_field"][:, None]
+    res = O.pod(Ac, 5, 20)
+    fo = O.fourier(res["T"], 5, float(g["dt"]), res["nm"], 0.9)
+    assert PODFS.podfs_dat_text(res["nm"], fo["period"], fo["c"], fo["c_ind"], fo["c_count"], 5) == str(g["podfs_dat"])
+
+
+def test_eigenvalue_file_writer(golden_dir, tmp_path):
+    import PODFS
+    g = np.load(os.path.join(golden_dir, "c1_32x32x64.npz"))
+    fn = str(tmp_path / "POD.eigenvalues.dat")
+    PODFS.write_eigenvalues(int(g["num_valid_modes"]), 64, g["energy"].real, fn)
+    assert open(fn).read() == str(g["eigenvalues_dat"])
+
+
+def test_sort_eigenvalues_semantics():
+    import PODFS
+    energy = np.array([1.0, 3.0, np.nan, 3.0, -2.0])
+    T = np.arange(25, dtype=np.float64).reshape(5, 5)
+    e2, T2 = O.sort_eigen(energy.astype(complex), T.astype(complex))
+    PODFS.sort_eigenvalues(5, energy, T)
+    assert np.array_equal(energy, e2) and np.array_equal(T, T2)
+
+
+def test_prf_geometry_doc_row_and_sizes():
+    import PODFS
+    import nsigproclib as sp
+    pts = PODFS.cell_centres(10, 11, 0.1)
+    assert pts.shape == (110, 3)
+    assert ",".join(sp.str(v) for v in pts[0]) == "0.000000000000,-0.500000000000,0.550000011921"
+    assert np.all(pts[:, 0] == 0.0)
+    assert np.allclose(pts[-1, 1:], [0.5, -0.55], atol=1e-7)
+
+
+def test_cli_options_and_aliases():
+    import digitalfilters as df
+    p = df.make_parser()
+    o, _ = p.parse_args(["-j", "8", "-k", "9", "--num_steps", "7", "--udash", "0.05", "--filter_width", "3",
+                         "--num_modes", "4", "--seed", "11", "-5"])
+    assert (o.jma, o.kma, o.nsteps, o.turbulence_intensity, o.fwidth, o.nm, o.seed, o.hdf5) == \
+        (8, 9, 7, 0.05, 3.0, 4, 11, True)
+    s = df.setup_from_options(o)
+    assert s.nfx == int(np.ceil(3.0 * 3.0)) and s.seed == 11
+
+
+def _h5py_python():
+    import HDF5
+    return HDF5._h5py_python()
+
+
+@pytest.mark.skipif(_h5py_python() is None, reason="no interpreter with h5py")
+def test_hdf5_layout(tmp_path):
+    import HDF5
+
+    class I:
+        pass
+    i_d = I()
+    i_d.nm, i_d.period, i_d.num_points = 2, 0.5, 3
+    i_d.N_FC = np.array([2, 1])
+    i_d.FC = np.arange(9, dtype=np.float64).reshape(3, 3)
+    i_d.mean = np.arange(18, dtype=np.float64).reshape(3, 6)
+    i_d.modes = np.arange(36, dtype=np.float64).reshape(2, 3, 6) * 0.5
+    fn = str(tmp_path / "PODFS.hdf5")
+    HDF5.write_HDF5(i_d, fn)
+    reader = ("import h5py, numpy as np, sys\n"
+              "f = h5py.File(sys.argv[1], 'r'); m = f['main']\n"
+              "print(int(m.attrs['N_POD']), float(m.attrs['period']), list(m['N_FC'][:]), list(m['FC'][:]))\n"
+              "print(list(m['mean'][:]), m['mean'].attrs['Np'], m['mean'].attrs['Nvar'], m['mean'].attrs['Vars'], list(m['mean'].attrs['SF']))\n"
+              "print(sorted(m['modes'].keys()), list(m['modes/mode_0002'][:4]))\n")
+    out = subprocess.run([_h5py_python(), "-c", reader, fn], capture_output=True, text=True).stdout.splitlines()
+    assert out[0] == "2 0.5 [2, 1] %s" % [float(v) for v in i_d.FC.reshape(-1, order="F")]
+    assert out[1].startswith(str([float(v) for v in i_d.mean.reshape(-1, order="F")]))
+    assert "3 6 b'x,y,z,u,v,w,dummy' [1.0, 1.0, 1.0, 1.0, 1.0, 1.0]" in out[1]
+    assert out[2].startswith("['mode_0001', 'mode_0002']")
+
+
+def _gloo_worker(rank, world, port, A, out):
+    import torch
+    import torch.distributed as dist
+    import podsgen
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    J, K, ns = 12, 5, 9
+    j0, j1 = podsgen.row_slab(J, rank, world)
+    P = J * K
+    rows = np.concatenate([np.arange(c * P + j0 * K, c * P + j1 * K) for c in range(3)])
+    Al = A[rows]
+    Ac = Al - np.mean(Al, 1)[:, None]
+    Cp = torch.from_numpy(np.dot(Ac.T, Ac))
+    dist.all_reduce(Cp)
+    out[rank] = (Cp.numpy() / ns).tobytes()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_correlation_decomposition():
+    """The multi-GPU decomposition (row slabs, partial A^T A, one all-reduce sum, divide)
+    reproduces the single-device correlation (oracle arithmetic, gloo transport)."""
+    import multiprocessing as mp
+    rng = np.random.default_rng(0)
+    A = rng.standard_normal((3 * 12 * 5, 9)) + 1.0
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = 29500 + os.getpid() % 1000
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, A, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    Ac = A - np.mean(A, 1)[:, None]
+    ref = np.dot(Ac.T, Ac) / 9
+    for r in range(2):
+        C = np.frombuffer(out[r]).reshape(9, 9)
+        assert np.max(np.abs(C - ref)) <= 1e-13 * np.max(np.abs(ref))
