@@ -124,6 +124,26 @@ int pods_divide_inplace(pods_ctx* ctx, double* x_dev, int64_t n, double divisor)
 int pods_temporal_modes(pods_ctx* ctx, const double* V_dev, int64_t v_rs, int64_t v_cs,
                         const double* lambda_desc_host, int nvalid, int ncols, double* T_dev);
 
+/* Symmetric eigensolve of the POD (replaces `linalg.eig(C)` + `sort_eigenvalues`,
+ * PODFS.py:1309-1310 and :1430-1447): all n eigenvalues in descending order and the unit
+ * eigenvectors of the nvec largest.  C_dev: n x n row-major symmetric (read only).
+ * lambda_desc_dev: n doubles.  vec_dev: n x nvec row-major, column k = eigenvector of
+ * lambda_desc[k] (sign arbitrary, as the reference's dgeev vectors).  1 <= n <= 4096,
+ * 0 <= nvec <= min(n, 64).  Stream-ordered (returns before the result is ready). */
+int pods_syev(pods_ctx* ctx, const double* C_dev, int n, int nvec, double* lambda_desc_dev,
+              double* vec_dev);
+/* The tridiagonalisation step of pods_syev alone (test entry): C = Q T Q^T with
+ * T = tridiag(e, d, e); d_host: n, e_host: n-1 (synchronous). */
+int pods_sytrd(pods_ctx* ctx, const double* C_dev, int n, double* d_host, double* e_host);
+/* Diagnostics: pods_sytrd with 8 s_memrealtime (100 MHz) stamps per column of workgroup
+ * wg written to trace_host (n x 8 int64): column start, inputs arrived, after the dot
+ * reduction, after the norm reduction, update start, update end, after the row-sum
+ * barrier, column end. */
+int pods_sytrd_trace(pods_ctx* ctx, const double* C_dev, int n, int wg, int64_t* trace_host);
+/* 0 if the last pods_syev / pods_sytrd ran to completion, PODS_ERR_INTERNAL if its
+ * cross-workgroup wait timed out (results invalid).  Synchronises the stream. */
+int pods_syev_status(pods_ctx* ctx);
+
 /* Spatial modes Phi = ((A-m) T[:, :nm]) * (1/lambda) / ns (PODFS.py:1330-1333).
  * T_dev: ns x ldT row-major.  phi_dev: 3*P_local x nm row-major (reference layout). */
 int pods_spatial_modes(pods_ctx* ctx, const double* T_dev, int ldT, const double* lambda_host,

@@ -218,6 +218,8 @@ struct pods_ctx {
   RngLayout layout;
   RngBuffers rng;
   DevBuf R, T1, A, mean, lund, taps, rot, prog_mean, prog_dft, tbuf, mag, lam, cwork, items;
+  DevBuf e_wm, e_x, e_flags, e_det, e_v, e_t, e_part, e_w2, e_inv;  // pods_syev workspace
+  int e_G = 0;
   int nitems = 0;
   int64_t items_key = -1;
   int nprog_mean = 0;
@@ -313,7 +315,9 @@ int pods_destroy(pods_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->R, &c->T1, &c->A, &c->mean, &c->lund, &c->taps, &c->rot, &c->prog_mean,
-                    &c->prog_dft, &c->tbuf, &c->mag, &c->lam, &c->cwork, &c->items})
+                    &c->prog_dft, &c->tbuf, &c->mag, &c->lam, &c->cwork, &c->items, &c->e_wm,
+                    &c->e_x, &c->e_flags, &c->e_det, &c->e_v, &c->e_t, &c->e_part, &c->e_w2,
+                    &c->e_inv})
     release(*b);
   c->rng.free_all();
   delete c;
@@ -617,6 +621,132 @@ int pods_spatial_modes(pods_ctx* c, const double* T, int ldT, const double* lam,
   PODS_HIP(pods::launch_spatial(c->A.as<double>(), c->rowlen, c->p.ns, c->mean.as<double>(), T, ldT, nm,
                                 c->lam.as<double>(), phi, c->stream));
   PODS_HIP(hipStreamSynchronize(c->stream));
+  return PODS_OK;
+  PODS_CATCH
+}
+
+namespace {
+
+// Tridiagonalisation into the context workspace: D at e_det, E at +n, tau at +2n.
+int run_sytrd(pods_ctx* c, const double* C, int n, int* R_out, int64_t* trace = nullptr,
+              int trace_wg = 0) {
+  int R = 0, G = 0;
+  int64_t slab = 0;
+  if (pods::trd_plan(n, &R, &G, &slab) != 0)
+    return fail(PODS_ERR_UNSUPPORTED, "pods_syev: n = " + std::to_string(n) + " > 4096");
+  PODS_HIP(ensure(c->e_wm, (size_t)slab * sizeof(double)));
+  PODS_HIP(ensure(c->e_x, (size_t)4 * n * sizeof(double)));  // 2 vectors x 2 parities x n
+  PODS_HIP(ensure(c->e_flags, 64));
+  PODS_HIP(ensure(c->e_det, ((size_t)4 * n + 8) * sizeof(double)));
+  PODS_HIP(ensure(c->e_v, (size_t)std::max(n - 1, 1) * n * sizeof(double)));
+  PODS_HIP(hipMemsetAsync(c->e_flags.p, 0, 64, c->stream));
+  PODS_HIP(hipMemsetAsync(c->e_x.p, 0, (size_t)4 * n * sizeof(double), c->stream));
+  c->e_G = 0;
+  double* det = c->e_det.as<double>();
+  pods::TrdArgs a{};
+  a.C = C;
+  a.ldc = n;
+  a.n = n;
+  a.G = G;
+  a.klast = (n - 1) / 512;
+  a.Wm = c->e_wm.as<double>();
+  a.pbuf = c->e_x.as<double>();
+  a.rbuf = c->e_x.as<double>() + 2 * (int64_t)n;
+  a.flags = c->e_flags.as<uint32_t>();
+  a.D = det;
+  a.E = det + n;
+  a.tau = det + 2 * (int64_t)n;
+  a.V = c->e_v.as<double>();
+  a.ldv = n;
+  a.trace = trace;
+  a.trace_wg = trace_wg;
+  PODS_HIP(pods::launch_trd(a, R, c->stream));
+  *R_out = R;
+  return PODS_OK;
+}
+
+}  // namespace
+
+int pods_syev(pods_ctx* c, const double* C, int n, int nvec, double* lam_desc, double* vec) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!C || !lam_desc || n < 1 || nvec < 0 || nvec > std::min(n, 64) || (nvec > 0 && !vec))
+    return fail(PODS_ERR_ARG, "pods_syev: bad arguments");
+  int R = 0;
+  if (int e = run_sytrd(c, C, n, &R)) return e;
+  double* det = c->e_det.as<double>();
+  double* D = det;
+  double* E = det + n;
+  double* tau = det + 2 * (int64_t)n;
+  double* bounds = det + 3 * (int64_t)n;
+  PODS_HIP(pods::launch_tri_eigvals(D, E, n, bounds, lam_desc, c->stream));
+  if (nvec > 0) {
+    const int nblk = std::max((n - 1 + 63) / 64, 1);
+    const int nchunk = (n + 127) / 128;
+    PODS_HIP(ensure(c->e_inv, (size_t)nvec * n * sizeof(double)));
+    PODS_HIP(ensure(c->e_t, (size_t)nblk * 64 * 64 * sizeof(double)));
+    PODS_HIP(ensure(c->e_part, (size_t)nchunk * 64 * nvec * sizeof(double)));
+    PODS_HIP(ensure(c->e_w2, (size_t)64 * nvec * sizeof(double)));
+    PODS_HIP(pods::launch_tri_eigvecs(D, E, n, lam_desc, bounds, nvec, c->e_inv.as<double>(), vec,
+                                      c->stream));
+    PODS_HIP(pods::launch_back_transform(c->e_v.as<double>(), n, tau, n, nvec, c->e_t.as<double>(),
+                                         c->e_part.as<double>(), c->e_w2.as<double>(), vec,
+                                         c->stream));
+  }
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_sytrd(pods_ctx* c, const double* C, int n, double* d_host, double* e_host) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!C || !d_host || (n > 1 && !e_host) || n < 1) return fail(PODS_ERR_ARG, "pods_sytrd: bad arguments");
+  int R = 0;
+  if (int e = run_sytrd(c, C, n, &R)) return e;
+  const double* det = c->e_det.as<double>();
+  PODS_HIP(hipMemcpyAsync(d_host, det, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  if (n > 1)
+    PODS_HIP(hipMemcpyAsync(e_host, det + n, (size_t)(n - 1) * sizeof(double), hipMemcpyDeviceToHost,
+                            c->stream));
+  uint32_t abort_word = 0;
+  PODS_HIP(hipMemcpyAsync(&abort_word, c->e_flags.as<uint32_t>() + c->e_G, sizeof(uint32_t),
+                          hipMemcpyDeviceToHost, c->stream));
+  PODS_HIP(hipStreamSynchronize(c->stream));
+  if (abort_word) return fail(PODS_ERR_INTERNAL, "pods_sytrd: hand-off wait timed out (aborted)");
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_sytrd_trace(pods_ctx* c, const double* C, int n, int wg, int64_t* trace_host) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!C || !trace_host || n < 2) return fail(PODS_ERR_ARG, "pods_sytrd_trace: bad arguments");
+  DevBuf tb;
+  PODS_HIP(ensure(tb, (size_t)n * 8 * sizeof(int64_t)));
+  PODS_HIP(hipMemsetAsync(tb.p, 0, (size_t)n * 8 * sizeof(int64_t), c->stream));
+  int R = 0;
+  int e = run_sytrd(c, C, n, &R, tb.as<int64_t>(), wg);
+  if (e == PODS_OK) {
+    hipError_t he = hipMemcpyAsync(trace_host, tb.p, (size_t)n * 8 * sizeof(int64_t), hipMemcpyDeviceToHost,
+                                   c->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(c->stream);
+    if (he != hipSuccess) e = fail(PODS_ERR_HIP, std::string("pods_sytrd_trace: ") + hipGetErrorString(he));
+  }
+  (void)hipStreamSynchronize(c->stream);
+  release(tb);
+  return e;
+  PODS_CATCH
+}
+
+int pods_syev_status(pods_ctx* c) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!c->e_flags.p) return PODS_OK;
+  uint32_t abort_word = 0;
+  PODS_HIP(hipMemcpyAsync(&abort_word, c->e_flags.as<uint32_t>() + c->e_G, sizeof(uint32_t),
+                          hipMemcpyDeviceToHost, c->stream));
+  PODS_HIP(hipStreamSynchronize(c->stream));
+  if (abort_word) return fail(PODS_ERR_INTERNAL, "pods_syev: hand-off wait timed out (aborted)");
   return PODS_OK;
   PODS_CATCH
 }

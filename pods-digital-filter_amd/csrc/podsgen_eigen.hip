@@ -1,0 +1,987 @@
+// gfx950 symmetric eigensolver for the POD correlation matrix (PODFS.py:1309-1310:
+// `linalg.eig(C)` + `sort_eigenvalues`): all n eigenvalues and the eigenvectors of the
+// nvec largest.
+//
+//   k_trd      Householder tridiagonalisation (LAPACK dsytd2 'L' arithmetic) as a few
+//              persistent launches (one per 512-column range).  The live matrix stays on
+//              chip: workgroup g (one per CU) owns rows g, g+G, ... ; lane t of its 512
+//              threads owns columns t, t+512, ... of those rows, held in VGPRs and LDS (plus,
+//              for the first range at n > 2048, an L2-resident slab).  Per column j there is ONE cross-CU
+//              hand-off: every workgroup publishes p = A v for its rows plus (owner only) the
+//              updated row j+1, and every workgroup then recomputes the rank-2 update vector w,
+//              the next column and its Householder vector redundantly from those two vectors,
+//              so no second exchange (norm, dot) is needed.
+//   k_bisect   all eigenvalues of T by Sturm-count multisection (16 lanes per eigenvalue).
+//   k_invit    inverse iteration on T for the wanted eigenvalues (dgttrf-style LU in LDS).
+//   k_orth     modified Gram-Schmidt inside eigenvalue clusters (dstein's ORTOL rule).
+//   k_larft / k_bt_*  back-transformation Y = Q Z with compact-WY blocks of 64 reflectors.
+//
+// FMA is requested explicitly (the file is built with -ffp-contract=off like the others).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cstdint>
+
+#include "podsgen_kernels.h"
+
+namespace pods {
+namespace eig {
+
+constexpr int TT = 512;  // k_trd workgroup: 8 waves
+
+// ---- cross-CU hand-off primitives (MI355X_MICROARCH.md "Valid forms": sc1 payload stores,
+// ---- drained, one sc1 flag per workgroup; sc1 poll; sc1 payload loads) ------------------
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  const unsigned long long u = __hip_atomic_load(
+      const_cast<unsigned long long*>(reinterpret_cast<const unsigned long long*>(p)),
+      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __longlong_as_double((long long)u);
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
+                     (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_flag(const uint32_t* p) {
+  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_flag(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// DPP row reduction: afterwards every lane of each 16-lane row holds the row sum (the same
+// bits in all 16 lanes: each step adds a pair in both orders, a+b == b+a).
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double row16_sum(double x) {
+  x += dpp_mov<0xB1>(x);   // quad_perm [1,0,3,2]
+  x += dpp_mov<0x4E>(x);   // quad_perm [2,3,0,1]
+  x += dpp_mov<0x141>(x);  // row_half_mirror
+  x += dpp_mov<0x140>(x);  // row_mirror
+  return x;
+}
+// gfx950 cross-row swaps: permlane32_swap(a, b) -> a = {a.lo32, b.lo32}, b = {a.hi32, b.hi32};
+// permlane16_swap(a, b) -> a = {a.r0, b.r0, a.r2, b.r2}, b = {a.r1, b.r1, a.r3, b.r3}.
+__device__ __forceinline__ void pl32_swap(double& a, double& b) {
+  const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(a), __double2loint(b), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(a), __double2hiint(b), false, false);
+  a = __hiloint2double((int)hi[0], (int)lo[0]);
+  b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+__device__ __forceinline__ void pl16_swap(double& a, double& b) {
+  const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(a), __double2loint(b), false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(a), __double2hiint(b), false, false);
+  a = __hiloint2double((int)hi[0], (int)lo[0]);
+  b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+// Wave sum, the same bits in every lane (exec must be full).
+__device__ __forceinline__ double wave_sum(double x) {
+  double y = x;
+  pl32_swap(x, y);
+  x = x + y;
+  y = x;
+  pl16_swap(x, y);
+  x = x + y;
+  return row16_sum(x);
+}
+
+// Workgroup sum in a fixed order; `red` alternates between two 8-double slots per call so
+// no trailing barrier is needed.
+template <int NW>
+__device__ __forceinline__ double block_sum(double x, double* red) {
+  x = wave_sum(x);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+  __syncthreads();
+  double s = red[0];
+#pragma unroll
+  for (int k = 1; k < NW; ++k) s += red[k];
+  return s;
+}
+
+// A wave-uniform double (moved to SGPRs by readfirstlane).
+__device__ __forceinline__ double uniform(double x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffll));
+  const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Reduce-scatter of RH (1, 2 or 4) per-lane values over the wave: afterwards lane row q
+// (lanes 16q..16q+15) holds the wave sum of value q*RH/4 (RH = 4: value q; RH = 2: value q/2).
+template <int RH>
+__device__ __forceinline__ double rows_wave_sum(double (&a)[RH]) {
+  double s;
+  if constexpr (RH == 4) {
+    double a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
+    pl32_swap(a0, a2);
+    pl32_swap(a1, a3);
+    double s0 = a0 + a2, s1 = a1 + a3;
+    pl16_swap(s0, s1);
+    s = s0 + s1;
+  } else if constexpr (RH == 2) {
+    double a0 = a[0], a1 = a[1];
+    pl32_swap(a0, a1);
+    double s0 = a0 + a1, s1 = s0;
+    pl16_swap(s0, s1);
+    s = s0 + s1;
+  } else {
+    s = a[0];
+    double y = s;
+    pl32_swap(s, y);
+    s = s + y;
+    y = s;
+    pl16_swap(s, y);
+    s = s + y;
+  }
+  return row16_sum(s);
+}
+
+template <int S>
+__device__ __forceinline__ double pick(const double (&v)[S], int m) {
+  double r = 0.0;
+#pragma unroll
+  for (int k = 0; k < S; ++k)
+    if (k == m) r = v[k];
+  return r;
+}
+
+// ---- tagged 8-byte hand-off values: the two lowest mantissa bits carry the column parity
+// ---- tag (j mod 4).  One 8-B sc1 store publishes value and tag together; the consumer
+// ---- spins on its own loads until the tag matches -- no flag, no producer drain, one hop.
+// ---- A stale entry of the same (parity) buffer is always two columns old, so two bits
+// ---- suffice; the value perturbation is <= 3 ulp, below dsytd2's own rounding per step.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc8(const double* base, int n) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), 0, n * 8, 0x00020000);
+}
+__device__ __forceinline__ double gld(__amdgpu_buffer_rsrc_t r, int idx) {
+  // volatile (bit 31) + sc1 (bit 4): re-read every spin, served by L2 but never by L1
+  const auto q = __builtin_amdgcn_raw_buffer_load_b64(r, idx * 8, 0, (1u << 31) | 16u);
+  return __builtin_bit_cast(double, q);
+}
+__device__ __forceinline__ double tagged(double v, uint32_t tag) {
+  const long long b = (__double_as_longlong(v) & ~3ll) | (long long)(tag & 3u);
+  return __longlong_as_double(b);
+}
+__device__ __forceinline__ bool tag_ok(double v, uint32_t tag) {
+  return ((uint32_t)__double2loint(v) & 3u) == (tag & 3u);
+}
+__device__ __forceinline__ void gst(__amdgpu_buffer_rsrc_t r, int idx, double v, uint32_t tag) {
+  const double t = tagged(v, tag);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0)), t),
+                                        r, idx * 8, 0, 16u);
+}
+
+constexpr int SPIN_LIMIT = 1 << 20;  // ~1 s of polling before a workgroup raises the abort word
+
+// -----------------------------------------------------------------------------------------
+// k_trd<R, S, K, SG, SL>: one column range of the tridiagonalisation.
+//
+// Workgroup g (of G <= 256) owns rows r = g + G*i (i < R); lane t owns columns c = t + 512*m
+// (m < S).  The column loop is cut into S ranges: range K runs columns j in
+// [512K-1, 512(K+1)-1) (K = 0 starts at 0).  Throughout range K the slots m < K and the rows
+// i < 2K hold nothing live (every such row/column index is <= j), so each range is its own
+// launch that keeps only rows [2K, R) x slots [K, S) on chip -- the storage shrinks as the
+// matrix does, and each launch is a single-exit loop with compile-time slot/row bounds.
+// Between launches the live block is parked in the per-workgroup slab Wm[g][m][i][t]; the
+// pending reflector v_{j-1} is re-read from V and tau from the tau array.
+// Storage inside a launch: slots [K, K+SG) stay in Wm (L2-resident), the next SL slots in
+// LDS, the rest in VGPRs.
+//
+// Column j (dsytd2 'L'): every workgroup reads p_{j-1} = A^{(j-1)} v_{j-1} and column j of
+// A^{(j-1)} (both published in column j-1 as tagged granules by the owners of the rows),
+// recomputes w_{j-1}, column j of A^{(j)} and the reflector v_j redundantly (two workgroup
+// reductions), applies the pending rank-2 update to its rows fused with p_j = A^{(j)} v_j,
+// and publishes p_j and column j+1 of its rows.  Three workgroup barriers, one cross-CU hop.
+// -----------------------------------------------------------------------------------------
+template <int R, int S, int K, int SG, int SL>
+__global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
+  constexpr int I0 = (2 * K < R) ? 2 * K : R;  // first live row slot
+  constexpr int RL = R - I0;                    // live rows
+  constexpr int SR = S - K - SG - SL;           // register slots
+  static_assert(SR >= 0 && RL > 0, "bad trd range configuration");
+  extern __shared__ double lds[];
+  double* Al = lds;                  // [SL][RL][TT]
+  double* red = lds + SL * RL * TT;  // 2 x 8 reduction slots
+  double* bc = red + 16;             // 4: alpha0 (double-buffered by column parity)
+  double* rsv = bc + 4;              // R: v_{j-1}[r_i]
+  double* rsw = rsv + R;             // R: w_{j-1}[r_i]
+  double* rr = rsw + R;              // R x 8 wave partials
+  const int t0 = threadIdx.x, wv = t0 >> 6;
+  const int g0 = blockIdx.x, G = a.G, n = a.n;
+  if (g0 >= n) return;
+  const int lastrow = g0 + G * ((n - 1 - g0) / G);
+  double* Wg = a.Wm + (int64_t)g0 * S * R * TT;  // this workgroup's slab
+  auto wm = [&](int m, int i, int t) -> double& { return Wg[((int64_t)m * R + i) * TT + t]; };
+  double Ar[RL][SR > 0 ? SR : 1];
+  uint32_t* abortw = a.flags;
+
+  // Ranges K > klast = (n-1)/512 hold no column and are not launched; klast runs the tail.
+  const bool last = K == a.klast;
+  const int jend = min(lastrow + 1, n - 1);
+  const int jb = K == 0 ? 0 : TT * K - 1;
+  const int je = last ? jend : min(jend, TT * (K + 1) - 1);
+
+  // ---- load the live block -----------------------------------------------------------------
+#pragma unroll
+  for (int ii = 0; ii < RL; ++ii) {
+    const int i = I0 + ii;
+    const int r = g0 + G * i;
+#pragma unroll
+    for (int m = K; m < S; ++m) {
+      const int c = t0 + TT * m;
+      double v;
+      if (K == 0)
+        v = (r < n && c < n) ? a.C[(int64_t)r * a.ldc + c] : 0.0;
+      else
+        v = wm(m, i, t0);
+      if (m < K + SG) {
+        if (K == 0) wm(m, i, t0) = v;
+      } else if (m < K + SG + SL) {
+        Al[((m - K - SG) * RL + ii) * TT + t0] = v;
+      } else {
+        Ar[ii][m - K - SG - SL] = v;
+      }
+    }
+  }
+  double vp[S];
+  double tau_p = 0.0;
+#pragma unroll
+  for (int m = 0; m < S; ++m) {
+    const int c = t0 + TT * m;
+    vp[m] = (jb > 0 && c < n) ? a.V[(int64_t)(jb - 1) * a.ldv + c] : 0.0;
+  }
+  if (jb > 0) tau_p = a.tau[jb - 1];
+  int rk = 0;
+
+  int64_t* trace = (a.trace && g0 == a.trace_wg && t0 == 0) ? a.trace : nullptr;
+  for (int j = jb; j < je; ++j) {
+    if (trace) trace[j * 8 + 0] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    // Re-materialise the lane/workgroup indices every column: without this the compiler
+    // hoists ~100 loop-invariant addresses and masks out of the column loop and spills.
+    int t = t0, g = g0;
+    asm volatile("" : "+v"(t));
+    asm volatile("" : "+s"(g));
+    const int lane = t & 63;
+    // ---- inputs: p_{j-1} (p), column j of A^{(j-1)} (x), p_{j-1}[j] -----------------------
+    double p[S], x[S], pj = 0.0;
+    if (j == 0) {
+#pragma unroll
+      for (int m = 0; m < S; ++m) {
+        const int c = t + TT * m;
+        p[m] = 0.0;
+        x[m] = c < n ? a.C[c] : 0.0;
+      }
+    } else {
+      const __amdgpu_buffer_rsrc_t rp = rsrc8(a.pbuf + (int64_t)((j - 1) & 1) * n, n);
+      const __amdgpu_buffer_rsrc_t rc = rsrc8(a.rbuf + (int64_t)((j - 1) & 1) * n, n);
+      const uint32_t want = (uint32_t)j;
+      // Every spin re-reads all of this lane's granules (simple straight-line code keeps the
+      // register allocation flat); the wave leaves when all its lanes saw the tag.
+      for (int spin = 0;; ++spin) {
+        bool ok = true;
+#pragma unroll
+        for (int m = 0; m < S; ++m) {
+          const int c = t + TT * m;
+          const bool in = c >= j && c < n;
+          const double q1 = gld(rp, in ? c : j);
+          const double q2 = gld(rc, in ? c : j);
+          ok = ok && tag_ok(q1, want) && tag_ok(q2, want);
+          p[m] = in ? q1 : 0.0;
+          x[m] = in ? q2 : 0.0;
+        }
+        const double qj = gld(rp, j);
+        ok = ok && tag_ok(qj, want);
+        pj = qj;
+        if (__all(ok)) break;
+        if ((spin & 1023) == 1023) {
+          if (ld_flag(abortw) != 0) break;
+          if (spin > SPIN_LIMIT) {
+            st_flag(abortw, 1u);
+            break;
+          }
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    if (trace) trace[j * 8 + 1] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    // ---- w = tau p ; alpha = -tau/2 (w . v) ; w += alpha v  (dsytd2) -------------------
+    double dot = 0.0;
+#pragma unroll
+    for (int m = 0; m < S; ++m) {
+      p[m] = tau_p * p[m];
+      dot = __builtin_fma(p[m], vp[m], dot);
+    }
+#pragma unroll
+    for (int i = I0; i < R; ++i) {
+      const int r = g + G * i;
+      if (r < n && (r & (TT - 1)) == t) rsv[i] = pick(vp, r / TT);
+    }
+    dot = block_sum<TT / 64>(dot, red + 8 * (rk++ & 1));                       // B1
+    if (trace) trace[j * 8 + 2] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    const double alpha = -0.5 * tau_p * dot;
+    // p now holds w_{j-1} (in place)
+#pragma unroll
+    for (int m = 0; m < S; ++m) p[m] = __builtin_fma(alpha, vp[m], p[m]);
+    const double vj = j >= 1 ? 1.0 : 0.0;  // v_{j-1}[j] (the reflector's unit entry)
+    const double wj = __builtin_fma(alpha, vj, tau_p * pj);
+    // ---- column j of A^{(j)} -------------------------------------------------------------
+#pragma unroll
+    for (int m = 0; m < S; ++m) {
+      const int c = t + TT * m;
+      x[m] = (c >= j && c < n) ? __builtin_fma(-p[m], vj, __builtin_fma(-vp[m], wj, x[m])) : 0.0;
+    }
+    if (t == ((j + 1) & (TT - 1))) bc[(j & 1) * 2] = pick(x, (j + 1) / TT);
+#pragma unroll
+    for (int i = I0; i < R; ++i) {
+      const int r = g + G * i;
+      if (r < n && (r & (TT - 1)) == t) rsw[i] = pick(p, r / TT);
+    }
+    double ss = 0.0;
+#pragma unroll
+    for (int m = 0; m < S; ++m) {
+      const int c = t + TT * m;
+      if (c >= j + 2 && c < n) ss = __builtin_fma(x[m], x[m], ss);
+    }
+    ss = block_sum<TT / 64>(ss, red + 8 * (rk++ & 1));                          // B2
+    if (trace) trace[j * 8 + 3] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    // ---- Householder reflector of x = A^{(j)}[j+1:, j] (dlarfg) --------------------------
+    const double alpha0 = bc[(j & 1) * 2];
+    double tau_j = 0.0, beta = alpha0, scal = 0.0;
+    if (ss != 0.0) {
+      beta = -copysign(sqrt(__builtin_fma(alpha0, alpha0, ss)), alpha0);
+      tau_j = (beta - alpha0) / beta;
+      scal = 1.0 / (alpha0 - beta);
+    }
+    const bool writer = g == j % G;
+    if (writer && t == (j & (TT - 1))) a.D[j] = pick(x, j / TT);
+#pragma unroll
+    for (int m = 0; m < S; ++m) {
+      const int c = t + TT * m;
+      x[m] = (c == j + 1) ? 1.0 : ((c >= j + 2 && c < n) ? x[m] * scal : 0.0);
+    }
+    // ---- rank-2 update of step j-1 fused with p_j = A^{(j)} v_j on rows >= j+1 -------------
+    // Slot-outer, row-inner; RH rows per pass bound the live accumulators; dead rows get zero
+    // multipliers (exact no-op update, sums never published) so no branch touches the
+    // matrix registers.  The lane holding column j+1 publishes that column of its rows.
+    if (trace) trace[j * 8 + 4] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    const __amdgpu_buffer_rsrc_t pw = rsrc8(a.pbuf + (int64_t)(j & 1) * n, n);
+    const __amdgpu_buffer_rsrc_t cw = rsrc8(a.rbuf + (int64_t)(j & 1) * n, n);
+    const uint32_t tag = (uint32_t)(j + 1);
+    const int mj1 = (j + 1) / TT;
+    const bool pubcol = t == ((j + 1) & (TT - 1));
+    constexpr int RH = (SG > 0) ? 2 : ((RL % 4 == 0) ? 4 : ((RL % 2 == 0) ? 2 : 1));
+#pragma unroll
+    for (int h = 0; h < RL / RH; ++h) {
+      double vr[RH], wr[RH], acc[RH];
+      bool live[RH];
+#pragma unroll
+      for (int q = 0; q < RH; ++q) {
+        const int i = I0 + h * RH + q;
+        const int r = g + G * i;
+        live[q] = r >= j + 1 && r < n;
+        vr[q] = live[q] ? uniform(rsv[i]) : 0.0;
+        wr[q] = live[q] ? uniform(rsw[i]) : 0.0;
+        acc[q] = 0.0;
+      }
+#pragma unroll
+      for (int m = K; m < S; ++m) {
+        const int c = t + TT * m;
+#pragma unroll
+        for (int q = 0; q < RH; ++q) {
+          const int ii = h * RH + q;
+          double val;
+          if (m < K + SG) {
+            val = 0.0;
+            if (live[q] && c >= j + 1) val = wm(m, I0 + ii, t);
+          } else if (m < K + SG + SL) {
+            val = Al[((m - K - SG) * RL + ii) * TT + t];
+          } else {
+            val = Ar[ii][m - K - SG - SL];
+          }
+          val = __builtin_fma(-vr[q], p[m], __builtin_fma(-wr[q], vp[m], val));
+          if (m < K + SG) {
+            if (live[q] && c >= j + 1) wm(m, I0 + ii, t) = val;
+          } else if (m < K + SG + SL) {
+            Al[((m - K - SG) * RL + ii) * TT + t] = val;
+          } else {
+            Ar[ii][m - K - SG - SL] = val;
+          }
+          acc[q] = __builtin_fma(val, x[m], acc[q]);
+          if (pubcol && m == mj1 && live[q]) gst(cw, g + G * (I0 + ii), val, tag);
+        }
+      }
+      const double sum = rows_wave_sum(acc);
+      if ((lane & (64 / RH - 1)) == 0) rr[(I0 + h * RH + lane / (64 / RH)) * 8 + wv] = sum;
+    }
+    if (trace) trace[j * 8 + 5] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    __syncthreads();                                                               // B3
+    if (trace) trace[j * 8 + 6] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    if (t >= I0 && t < R) {
+      const int r = g + G * t;
+      if (r >= j + 1 && r < n) {
+        double sum = rr[t * 8];
+#pragma unroll
+        for (int q = 1; q < 8; ++q) sum += rr[t * 8 + q];
+        gst(pw, r, sum, tag);
+      }
+    }
+    // the writer's outputs leave after the hand-off so they never delay it
+    if (writer) {
+      if (t == 0) {
+        a.E[j] = beta;
+        a.tau[j] = tau_j;
+      }
+#pragma unroll
+      for (int m = 0; m < S; ++m) {
+        const int c = t + TT * m;
+        if (c < n) st_sc1(a.V + (int64_t)j * a.ldv + c, x[m]);  // sc1: keep V out of L2
+      }
+    }
+    if (trace) trace[j * 8 + 7] = (int64_t)__builtin_amdgcn_s_memrealtime();
+#pragma unroll
+    for (int m = 0; m < S; ++m) vp[m] = x[m];
+    tau_p = tau_j;
+  }
+
+  if (!last) {
+    // ---- park the live block for the next range ---------------------------------------------
+#pragma unroll
+    for (int ii = 0; ii < RL; ++ii) {
+#pragma unroll
+      for (int m = K + SG; m < S; ++m) {
+        if (m < K + SG + SL)
+          wm(m, I0 + ii, t0) = Al[((m - K - SG) * RL + ii) * TT + t0];
+        else
+          wm(m, I0 + ii, t0) = Ar[ii][m - K - SG - SL];
+      }
+    }
+  } else if (lastrow == n - 1 && n > 1) {
+    // ---- D[n-1] = A^{(n-1)}[n-1, n-1] (owner of row n-1) ----------------------------------
+    // tau_{n-2} = 0 (nothing below row n-1), v_{n-2} = e_{n-1}: d = a - 2 w[n-1]
+    const int j = n - 1;
+    if (t0 == (j & (TT - 1))) {
+      const __amdgpu_buffer_rsrc_t rp = rsrc8(a.pbuf + (int64_t)((j - 1) & 1) * n, n);
+      const __amdgpu_buffer_rsrc_t rc = rsrc8(a.rbuf + (int64_t)((j - 1) & 1) * n, n);
+      double pv = 0.0, cv = 0.0;
+      bool np = true, nc = true;
+      for (int spin = 0; (np || nc) && spin <= SPIN_LIMIT; ++spin) {
+        if (np) {
+          const double q = gld(rp, j);
+          if (tag_ok(q, (uint32_t)j)) { pv = q; np = false; }
+        }
+        if (nc) {
+          const double q = gld(rc, j);
+          if (tag_ok(q, (uint32_t)j)) { cv = q; nc = false; }
+        }
+      }
+      if (np || nc) st_flag(abortw, 1u);
+      const double wv_ = tau_p * pv;
+      const double al = -0.5 * tau_p * wv_;
+      const double wj = __builtin_fma(al, 1.0, wv_);
+      a.D[j] = __builtin_fma(-wj, 1.0, __builtin_fma(-1.0, wj, cv));
+    }
+  } else if (n == 1 && g0 == 0 && t0 == 0) {
+    a.D[0] = a.C[0];
+  }
+}
+
+// -----------------------------------------------------------------------------------------
+// Gershgorin bounds, pivmin and the bisection tolerance of T (one 256-thread workgroup).
+// out: {gl, gu, pivmin, atol}
+// -----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_tri_bounds(const double* __restrict__ D,
+                                                    const double* __restrict__ E, int n,
+                                                    double* __restrict__ out) {
+  __shared__ double s_lo[256], s_hi[256], s_e2[256];
+  const int t = threadIdx.x;
+  double lo = DBL_MAX, hi = -DBL_MAX, e2m = 0.0;
+  for (int i = t; i < n; i += 256) {
+    const double el = i > 0 ? fabs(E[i - 1]) : 0.0;
+    const double er = i < n - 1 ? fabs(E[i]) : 0.0;
+    lo = fmin(lo, D[i] - (el + er));
+    hi = fmax(hi, D[i] + (el + er));
+    e2m = fmax(e2m, er * er);
+  }
+  s_lo[t] = lo;
+  s_hi[t] = hi;
+  s_e2[t] = e2m;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) {
+      s_lo[t] = fmin(s_lo[t], s_lo[t + o]);
+      s_hi[t] = fmax(s_hi[t], s_hi[t + o]);
+      s_e2[t] = fmax(s_e2[t], s_e2[t + o]);
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    const double ulp = DBL_EPSILON;
+    const double pivmin = DBL_MIN * fmax(1.0, s_e2[0]);
+    const double tnorm = fmax(fabs(s_lo[0]), fabs(s_hi[0]));
+    // dstebz: widen by FUDGE*TNORM*ULP*N + FUDGE*2*PIVMIN, FUDGE = 2.1
+    const double wid = 2.1 * tnorm * ulp * n + 2.1 * 2.0 * pivmin;
+    out[0] = s_lo[0] - wid;
+    out[1] = s_hi[0] + wid;
+    out[2] = pivmin;
+    out[3] = 2.0 * ulp * tnorm;
+  }
+}
+
+// Number of eigenvalues of T below sig (dlaebz's Sturm count, pivmin-guarded).
+__device__ __forceinline__ int sturm_count(const double2* __restrict__ de, int n, double sig,
+                                           double pivmin) {
+  int cnt = 0;
+  double q = 1.0;
+  for (int i = 0; i < n; ++i) {
+    const double2 v = de[i];
+    q = (v.x - sig) - v.y / q;
+    if (fabs(q) < pivmin) q = -pivmin;
+    cnt += q < 0.0 ? 1 : 0;
+  }
+  return cnt;
+}
+
+constexpr int BL = 16;  // lanes (shifts) per eigenvalue
+
+// Eigenvalue k (ascending) of T by multisection: 16 shifts per step split the bracket into 17.
+// Output lam_desc[n-1-k].  LDS: n x {d_i, e_{i-1}^2}.
+__global__ __launch_bounds__(256) void k_bisect(const double* __restrict__ D,
+                                                const double* __restrict__ E, int n,
+                                                const double* __restrict__ bounds,
+                                                double* __restrict__ lam_desc) {
+  extern __shared__ double2 de[];
+  const int t = threadIdx.x, lane = t & 63;
+  for (int i = t; i < n; i += 256) {
+    const double e = i > 0 ? E[i - 1] : 0.0;
+    de[i] = make_double2(D[i], e * e);
+  }
+  __syncthreads();
+  const double gl = bounds[0], gu = bounds[1], pivmin = bounds[2], atol = bounds[3];
+  const int l = t % BL;
+  const int k = blockIdx.x * (256 / BL) + t / BL;
+  const bool active = k < n;
+  double lo = gl, hi = gu;
+  for (int it = 0; it < 128; ++it) {
+    const bool conv = !active || (hi - lo) <= fmax(atol, 2.0 * DBL_EPSILON * fmax(fabs(lo), fabs(hi)));
+    if (__all(conv)) break;
+    const double step = (hi - lo) * (1.0 / (BL + 1));
+    const double sig = lo + step * (double)(l + 1);
+    const int cnt = sturm_count(de, n, sig, pivmin);
+    const unsigned long long m = __ballot(cnt >= k + 1);
+    const uint32_t gm = (uint32_t)((m >> (lane & ~(BL - 1))) & ((1u << BL) - 1));
+    if (!conv) {
+      const int f = gm ? __ffs(gm) - 1 : BL;  // first shift with count >= k+1
+      const double nhi = f < BL ? lo + step * (double)(f + 1) : hi;
+      const double nlo = f > 0 ? lo + step * (double)f : lo;
+      lo = nlo;
+      hi = nhi;
+    }
+  }
+  if (active && l == 0) lam_desc[n - 1 - k] = 0.5 * (lo + hi);
+}
+
+// -----------------------------------------------------------------------------------------
+// Inverse iteration for eigenvalue lam_desc[k] of T (dstein's role): LU with partial pivoting
+// of T - lam I (dgttrf) in LDS, three solves from a fixed pseudo-random start, unit 2-norm.
+// One workgroup per vector; thread 0 runs the recurrences, the others stage data.
+// Z: n x ldz row-major, column k.
+// -----------------------------------------------------------------------------------------
+__device__ __forceinline__ double start_value(int i, int k) {
+  uint32_t h = (uint32_t)i * 0x9E3779B1u ^ ((uint32_t)k + 1u) * 0x85EBCA77u;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  h *= 0x297A2D39u;
+  h ^= h >> 15;
+  return (double)(h >> 8) * (2.0 / 16777216.0) - 1.0;
+}
+
+__global__ __launch_bounds__(256) void k_invit(const double* __restrict__ D,
+                                               const double* __restrict__ E, int n,
+                                               const double* __restrict__ lam_desc,
+                                               const double* __restrict__ bounds, double* __restrict__ X,
+                                               double* __restrict__ Z, int ldz) {
+  extern __shared__ double sh[];
+  double* ua = sh;          // U diagonal
+  double* ub = sh + n;      // U first superdiagonal
+  double* uc = sh + 2 * n;  // U second superdiagonal (pivoting fill-in)
+  double* lm = sh + 3 * n;  // multipliers; sign bit of the stored value unused
+  unsigned char* pv = reinterpret_cast<unsigned char*>(sh + 4 * n);
+  const int k = blockIdx.x, t = threadIdx.x;
+  const double lam = lam_desc[k];
+  const double tnorm = fmax(fabs(bounds[0]), fabs(bounds[1]));
+  const double tiny = fmax(DBL_EPSILON * tnorm, DBL_MIN);
+  double* x = X + (int64_t)k * n;
+  for (int i = t; i < n; i += 256) {
+    ua[i] = D[i] - lam;
+    ub[i] = i < n - 1 ? E[i] : 0.0;
+    lm[i] = i < n - 1 ? E[i] : 0.0;  // subdiagonal, overwritten by the multiplier
+    uc[i] = 0.0;
+    x[i] = start_value(i, k);
+  }
+  __syncthreads();
+  if (t == 0) {
+    // dgttrf on (lm = sub, ua = diag, ub = super), fill-in in uc
+    for (int i = 0; i < n - 1; ++i) {
+      const double ai = ua[i], ci = lm[i];
+      if (fabs(ai) >= fabs(ci)) {
+        const double a0 = ai != 0.0 ? ai : tiny;
+        ua[i] = a0;
+        const double f = ci / a0;
+        lm[i] = f;
+        ua[i + 1] = ua[i + 1] - f * ub[i];
+        pv[i] = 0;
+      } else {
+        const double f = ai / ci;
+        ua[i] = ci;
+        lm[i] = f;
+        const double tmp = ub[i];
+        ub[i] = ua[i + 1];
+        ua[i + 1] = tmp - f * ua[i + 1];
+        if (i < n - 2) {
+          uc[i] = ub[i + 1];
+          ub[i + 1] = -f * ub[i + 1];
+        }
+        pv[i] = 1;
+      }
+    }
+    for (int i = 0; i < n; ++i)
+      if (fabs(ua[i]) < tiny) ua[i] = ua[i] < 0.0 ? -tiny : tiny;
+    for (int it = 0; it < 3; ++it) {
+      // forward: apply P and L^{-1}
+      for (int i = 0; i < n - 1; ++i) {
+        if (pv[i]) {
+          const double xi = x[i], xn = x[i + 1];
+          x[i] = xn;
+          x[i + 1] = xi - lm[i] * xn;
+        } else {
+          x[i + 1] = x[i + 1] - lm[i] * x[i];
+        }
+      }
+      // back substitution with U (3 diagonals)
+      double x2 = 0.0, x1 = 0.0, amax = 0.0;
+      for (int i = n - 1; i >= 0; --i) {
+        const double v = (x[i] - ub[i] * x1 - uc[i] * x2) / ua[i];
+        x[i] = v;
+        x2 = x1;
+        x1 = v;
+        amax = fmax(amax, fabs(v));
+      }
+      const double s = amax > 0.0 ? 1.0 / amax : 1.0;
+      for (int i = 0; i < n; ++i) x[i] = x[i] * s;
+    }
+  }
+  __syncthreads();
+  // unit 2-norm
+  __shared__ double red[4];
+  double ss = 0.0;
+  for (int i = t; i < n; i += 256) ss = __builtin_fma(x[i], x[i], ss);
+  ss = wave_sum(ss);
+  if ((t & 63) == 0) red[t >> 6] = ss;
+  __syncthreads();
+  const double inv = 1.0 / sqrt(red[0] + red[1] + red[2] + red[3]);
+  for (int i = t; i < n; i += 256) Z[(int64_t)i * ldz + k] = x[i] * inv;
+}
+
+// Modified Gram-Schmidt of the nvec vectors inside clusters |lam_i - lam_k| <= 1e-3 ||T||
+// (dstein ORTOL), in descending order, then re-normalise.  One workgroup.
+__global__ __launch_bounds__(256) void k_orth(const double* __restrict__ lam_desc,
+                                              const double* __restrict__ bounds, int n, int nvec,
+                                              double* __restrict__ Z, int ldz) {
+  __shared__ double red[2][4];
+  const int t = threadIdx.x;
+  const double tnorm = fmax(fabs(bounds[0]), fabs(bounds[1]));
+  int rk = 0;
+  for (int k = 1; k < nvec; ++k) {
+    bool touched = false;
+    for (int jj = 0; jj < k; ++jj) {
+      if (fabs(lam_desc[jj] - lam_desc[k]) > 1e-3 * tnorm) continue;
+      double d = 0.0;
+      for (int i = t; i < n; i += 256) d = __builtin_fma(Z[(int64_t)i * ldz + jj], Z[(int64_t)i * ldz + k], d);
+      d = wave_sum(d);
+      double* rb = red[rk++ & 1];
+      if ((t & 63) == 0) rb[t >> 6] = d;
+      __syncthreads();
+      d = rb[0] + rb[1] + rb[2] + rb[3];
+      for (int i = t; i < n; i += 256)
+        Z[(int64_t)i * ldz + k] = __builtin_fma(-d, Z[(int64_t)i * ldz + jj], Z[(int64_t)i * ldz + k]);
+      __syncthreads();
+      touched = true;
+    }
+    if (touched) {
+      double s = 0.0;
+      for (int i = t; i < n; i += 256) s = __builtin_fma(Z[(int64_t)i * ldz + k], Z[(int64_t)i * ldz + k], s);
+      s = wave_sum(s);
+      double* rb = red[rk++ & 1];
+      if ((t & 63) == 0) rb[t >> 6] = s;
+      __syncthreads();
+      const double inv = 1.0 / sqrt(rb[0] + rb[1] + rb[2] + rb[3]);
+      for (int i = t; i < n; i += 256) Z[(int64_t)i * ldz + k] = Z[(int64_t)i * ldz + k] * inv;
+      __syncthreads();
+    }
+  }
+}
+
+// -----------------------------------------------------------------------------------------
+// Back-transformation.  Reflector j (0..n-2): H_j = I - tau_j v_j v_j^T, v_j = row j of V
+// (zeros at c <= j, 1 at c = j+1).  Block b holds reflectors [64b, 64b+nb); its compact-WY
+// factor T_b (dlarft 'F','C') makes H_{64b} ... H_{64b+nb-1} = I - V_b T_b V_b^T.
+// -----------------------------------------------------------------------------------------
+constexpr int WB = 64;
+
+__global__ __launch_bounds__(256) void k_larft(const double* __restrict__ V, int64_t ldv,
+                                               const double* __restrict__ tau, int n,
+                                               double* __restrict__ Tg) {
+  __shared__ double vt[WB][WB + 1];
+  __shared__ double gm[WB][WB + 1];
+  __shared__ double tm[WB][WB + 1];
+  __shared__ double tmp[WB];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int j0 = b * WB;
+  const int nb = min(WB, n - 1 - j0);
+  // Gram matrix of the block's vectors (upper triangle incl. diagonal): 2080 pairs
+  double acc[9];
+  int pp[9], qq[9];
+#pragma unroll
+  for (int s = 0; s < 9; ++s) {
+    acc[s] = 0.0;
+    int id = t + 256 * s, p = 0;
+    // pair id -> (p, q), q >= p, row-major over the upper triangle of a 64 x 64
+    while (id >= WB - p) {
+      id -= WB - p;
+      ++p;
+      if (p >= WB) break;
+    }
+    pp[s] = p;
+    qq[s] = p + id;
+  }
+  for (int c0 = j0 + 1; c0 < n; c0 += WB) {
+    for (int e = t; e < WB * WB; e += 256) {
+      const int p = e / WB, cc = e % WB;
+      vt[p][cc] = (p < nb && c0 + cc < n) ? V[(int64_t)(j0 + p) * ldv + c0 + cc] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      if (pp[s] < WB) {
+        double a = acc[s];
+        for (int cc = 0; cc < WB; ++cc) a = __builtin_fma(vt[pp[s]][cc], vt[qq[s]][cc], a);
+        acc[s] = a;
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int s = 0; s < 9; ++s)
+    if (pp[s] < WB) {
+      gm[pp[s]][qq[s]] = acc[s];
+      gm[qq[s]][pp[s]] = acc[s];
+    }
+  for (int e = t; e < WB * WB; e += 256) tm[e / WB][e % WB] = 0.0;
+  __syncthreads();
+  for (int i = 0; i < nb; ++i) {
+    const double ti = tau[j0 + i];
+    if (t == 0) tm[i][i] = ti;
+    if (t < i) tmp[t] = -ti * gm[t][i];
+    __syncthreads();
+    if (t < i) {
+      double s = 0.0;
+      for (int q = t; q < i; ++q) s = __builtin_fma(tm[t][q], tmp[q], s);
+      tm[t][i] = s;
+    }
+    __syncthreads();
+  }
+  for (int e = t; e < WB * WB; e += 256) Tg[(int64_t)b * WB * WB + e] = tm[e / WB][e % WB];
+}
+
+constexpr int BT_ROWS = 128;  // rows of Z per workgroup in the back-transformation
+
+// W_part[chunk][p][k] = sum_{c in chunk} V[j0+p][c] Z[c][k]
+__global__ __launch_bounds__(256) void k_bt_w(const double* __restrict__ V, int64_t ldv, int n,
+                                              int j0, int nb, int ch0, const double* __restrict__ Z,
+                                              int ldz, int nvec, double* __restrict__ part) {
+  __shared__ double vs[WB][BT_ROWS + 1];
+  __shared__ double zs[BT_ROWS][65];
+  const int t = threadIdx.x;
+  const int ch = ch0 + blockIdx.x;
+  const int c0 = ch * BT_ROWS;
+  for (int e = t; e < WB * BT_ROWS; e += 256) {
+    const int p = e / BT_ROWS, cc = e % BT_ROWS, c = c0 + cc;
+    vs[p][cc] = (p < nb && c < n) ? V[(int64_t)(j0 + p) * ldv + c] : 0.0;
+  }
+  for (int e = t; e < BT_ROWS * nvec; e += 256) {
+    const int cc = e / nvec, k = e % nvec, c = c0 + cc;
+    zs[cc][k] = c < n ? Z[(int64_t)c * ldz + k] : 0.0;
+  }
+  __syncthreads();
+  for (int o = t; o < WB * nvec; o += 256) {
+    const int p = o / nvec, k = o % nvec;
+    double s = 0.0;
+    for (int cc = 0; cc < BT_ROWS; ++cc) s = __builtin_fma(vs[p][cc], zs[cc][k], s);
+    part[((int64_t)ch * WB + p) * nvec + k] = s;
+  }
+}
+
+// W = sum_chunks part (fixed order); W2 = T_b W
+__global__ __launch_bounds__(256) void k_bt_reduce(const double* __restrict__ part, int nchunk,
+                                                   int chunk0, const double* __restrict__ Tb, int nvec,
+                                                   double* __restrict__ W2) {
+  __shared__ double ws[WB][65];
+  const int t = threadIdx.x;
+  for (int o = t; o < WB * nvec; o += 256) {
+    double s = 0.0;
+    for (int ch = chunk0; ch < nchunk; ++ch) s += part[(int64_t)ch * WB * nvec + o];
+    ws[o / nvec][o % nvec] = s;
+  }
+  __syncthreads();
+  for (int o = t; o < WB * nvec; o += 256) {
+    const int p = o / nvec, k = o % nvec;
+    double s = 0.0;
+    for (int q = p; q < WB; ++q) s = __builtin_fma(Tb[p * WB + q], ws[q][k], s);
+    W2[o] = s;
+  }
+}
+
+// Z[c][k] -= sum_p V[j0+p][c] W2[p][k]
+__global__ __launch_bounds__(256) void k_bt_apply(const double* __restrict__ V, int64_t ldv, int n,
+                                                  int j0, int nb, int ch0, const double* __restrict__ W2,
+                                                  int nvec, double* __restrict__ Z, int ldz) {
+  __shared__ double vs[WB][BT_ROWS + 1];
+  __shared__ double w2[WB][65];
+  const int t = threadIdx.x;
+  const int c0 = (ch0 + blockIdx.x) * BT_ROWS;
+  for (int e = t; e < WB * BT_ROWS; e += 256) {
+    const int p = e / BT_ROWS, cc = e % BT_ROWS, c = c0 + cc;
+    vs[p][cc] = (p < nb && c < n) ? V[(int64_t)(j0 + p) * ldv + c] : 0.0;
+  }
+  for (int o = t; o < WB * nvec; o += 256) w2[o / nvec][o % nvec] = W2[o];
+  __syncthreads();
+  for (int o = t; o < BT_ROWS * nvec; o += 256) {
+    const int cc = o / nvec, k = o % nvec, c = c0 + cc;
+    if (c >= n) continue;
+    double s = 0.0;
+    for (int p = 0; p < WB; ++p) s = __builtin_fma(vs[p][cc], w2[p][k], s);
+    Z[(int64_t)c * ldz + k] -= s;
+  }
+}
+
+template <int R, int S, int K, int SG, int SL>
+static hipError_t launch_trd_t(const TrdArgs& a, hipStream_t st) {
+  constexpr int I0 = (2 * K < R) ? 2 * K : R;
+  const size_t lds = ((size_t)SL * (R - I0) * TT + 16 + 4 + 2 * R + 8 * R) * sizeof(double);
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_trd<R, S, K, SG, SL>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_trd<R, S, K, SG, SL>), dim3(a.G), dim3(TT), lds, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace eig
+
+// Tridiagonalisation plan: rows per workgroup R (G = ceil(n/R) <= 256 workgroups),
+// S = ceil(n/512) column slots per lane.
+int trd_plan(int n, int* R, int* G, int64_t* slab_doubles) {
+  int r = 0;
+  if (n <= 256) r = 1;
+  else if (n <= 512) r = 2;
+  else if (n <= 1024) r = 4;
+  else if (n <= 2048) r = 8;
+  else if (n <= 4096) r = 16;
+  else return -1;
+  const int s = r == 16 ? 8 : (r == 8 ? 4 : (r == 4 ? 2 : 1));
+  *R = r;
+  *G = (n + r - 1) / r;
+  *slab_doubles = (int64_t)(*G) * s * r * eig::TT;
+  return 0;
+}
+
+// One launch per column range (k_trd header).  Storage split per range {SG, SL}: 16 rows
+// x 8 slots = 128 doubles/lane at range 0 do not fit VGPRs + LDS next to the vectors, so
+// two slots stay in the (L2-resident) slab there; later ranges hold everything on chip.
+hipError_t launch_trd(const TrdArgs& a, int R, hipStream_t st) {
+  using namespace eig;
+  hipError_t e = hipSuccess;
+  if (a.klast != (a.n - 1) / TT) return hipErrorInvalidValue;
+#define PODS_TRD(RR, SS, KK, SGG, SLL) \
+  if (e == hipSuccess && KK <= a.klast) e = launch_trd_t<RR, SS, KK, SGG, SLL>(a, st)
+  switch (R) {
+    case 1: PODS_TRD(1, 1, 0, 0, 0); break;
+    case 2: PODS_TRD(2, 1, 0, 0, 0); break;
+    case 4:
+      PODS_TRD(4, 2, 0, 0, 0);
+      PODS_TRD(4, 2, 1, 0, 0);
+      break;
+    case 8:
+      PODS_TRD(8, 4, 0, 0, 0);
+      PODS_TRD(8, 4, 1, 0, 0);
+      PODS_TRD(8, 4, 2, 0, 0);
+      PODS_TRD(8, 4, 3, 0, 0);
+      break;
+    case 16:
+      PODS_TRD(16, 8, 0, 2, 2);
+      PODS_TRD(16, 8, 1, 2, 2);
+      PODS_TRD(16, 8, 2, 0, 2);
+      PODS_TRD(16, 8, 3, 0, 1);
+      PODS_TRD(16, 8, 4, 0, 0);
+      PODS_TRD(16, 8, 5, 0, 0);
+      PODS_TRD(16, 8, 6, 0, 0);
+      PODS_TRD(16, 8, 7, 0, 0);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+#undef PODS_TRD
+  return e;
+}
+
+hipError_t launch_tri_eigvals(const double* D, const double* E, int n, double* bounds,
+                              double* lam_desc, hipStream_t st) {
+  hipLaunchKernelGGL(eig::k_tri_bounds, dim3(1), dim3(256), 0, st, D, E, n, bounds);
+  const size_t lds = (size_t)n * sizeof(double2);
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&eig::k_bisect),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  const int per = 256 / eig::BL;
+  hipLaunchKernelGGL(eig::k_bisect, dim3((n + per - 1) / per), dim3(256), lds, st, D, E, n,
+                     (const double*)bounds, lam_desc);
+  return hipGetLastError();
+}
+
+hipError_t launch_tri_eigvecs(const double* D, const double* E, int n, const double* lam_desc,
+                              const double* bounds, int nvec, double* X, double* Z, hipStream_t st) {
+  const size_t lds = (size_t)n * 4 * sizeof(double) + (size_t)n;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&eig::k_invit),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(eig::k_invit, dim3(nvec), dim3(256), lds, st, D, E, n, lam_desc, bounds, X, Z,
+                     nvec);
+  hipLaunchKernelGGL(eig::k_orth, dim3(1), dim3(256), 0, st, lam_desc, bounds, n, nvec, Z, nvec);
+  return hipGetLastError();
+}
+
+hipError_t launch_back_transform(const double* V, int64_t ldv, const double* tau, int n, int nvec,
+                                 double* Tg, double* part, double* W2, double* Z, hipStream_t st) {
+  const int nref = n - 1;
+  if (nref <= 0) return hipSuccess;
+  const int nblk = (nref + eig::WB - 1) / eig::WB;
+  hipLaunchKernelGGL(eig::k_larft, dim3(nblk), dim3(256), 0, st, V, ldv, tau, n, Tg);
+  const int nchunk = (n + eig::BT_ROWS - 1) / eig::BT_ROWS;
+  for (int b = nblk - 1; b >= 0; --b) {
+    const int j0 = b * eig::WB;
+    const int nb = std::min(eig::WB, nref - j0);
+    const int ch0 = (j0 + 1) / eig::BT_ROWS;  // rows below j0+1 are zero in V_b
+    hipLaunchKernelGGL(eig::k_bt_w, dim3(nchunk - ch0), dim3(256), 0, st, V, ldv, n, j0, nb, ch0,
+                       (const double*)Z, nvec, nvec, part);
+    hipLaunchKernelGGL(eig::k_bt_reduce, dim3(1), dim3(256), 0, st, (const double*)part, nchunk, ch0,
+                       (const double*)Tg + (int64_t)b * eig::WB * eig::WB, nvec, W2);
+    hipLaunchKernelGGL(eig::k_bt_apply, dim3(nchunk - ch0), dim3(256), 0, st, V, ldv, n, j0, nb, ch0,
+                       (const double*)W2, nvec, Z, nvec);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace pods

@@ -39,4 +39,36 @@ hipError_t launch_spatial(const double* AT, int64_t rowlen, int ns, const double
 hipError_t launch_dft(const double* T, int ldT, int nm, int ns, const double* t, double inv_period,
                       double inv_n, const int* prog, int nprog, float2* c, hipStream_t st);
 
+// ---- symmetric eigensolver (podsgen_eigen.hip) ----------------------------------------
+struct TrdArgs {
+  const double* C;   // n x n row-major symmetric input (read only)
+  int64_t ldc;
+  int n;
+  int G;             // workgroups (= ceil(n / R)), all co-resident
+  int klast;         // last column range: (n - 1) / 512
+  double* Wm;        // per-workgroup slabs G x S x R x 512 (trd_plan's slab_doubles)
+  double* pbuf;      // 2 x n tagged values: p = A v (double-buffered by column parity)
+  double* rbuf;      // 2 x n tagged values: next column of A (zeroed before the launches)
+  uint32_t* flags;   // [0]: abort word (set if a hand-off wait timed out), zeroed
+  double* D;         // n   diagonal of T
+  double* E;         // n-1 off-diagonal of T
+  double* tau;       // n-1 reflector scalars
+  double* V;         // (n-1) x ldv reflector vectors, row j = v_j
+  int64_t ldv;
+  int64_t* trace;    // diagnostics: n x 8 s_memrealtime stamps of workgroup trace_wg, or null
+  int trace_wg;
+};
+int trd_plan(int n, int* R, int* G, int64_t* slab_doubles);
+hipError_t launch_trd(const TrdArgs& a, int R, hipStream_t st);
+// bounds: 4 doubles {gl, gu, pivmin, atol}; lam_desc: n eigenvalues of T, descending
+hipError_t launch_tri_eigvals(const double* D, const double* E, int n, double* bounds,
+                              double* lam_desc, hipStream_t st);
+// Z: n x nvec row-major eigenvectors of T for lam_desc[0..nvec); X: nvec x n scratch
+hipError_t launch_tri_eigvecs(const double* D, const double* E, int n, const double* lam_desc,
+                              const double* bounds, int nvec, double* X, double* Z, hipStream_t st);
+// Z <- Q Z with Q = H_0 ... H_{n-2}; Tg: ceil((n-1)/64) x 64 x 64, part: ceil(n/128) x 64 x nvec,
+// W2: 64 x nvec
+hipError_t launch_back_transform(const double* V, int64_t ldv, const double* tau, int n, int nvec,
+                                 double* Tg, double* part, double* W2, double* Z, hipStream_t st);
+
 }  // namespace pods

@@ -51,6 +51,10 @@ SIGNATURES = {
     "pods_corr": (c_int, [c_void_p, c_void_p, c_int]),
     "pods_divide_inplace": (c_int, [c_void_p, c_void_p, c_i64, c_dbl]),
     "pods_temporal_modes": (c_int, [c_void_p, c_void_p, c_i64, c_i64, c_void_p, c_int, c_int, c_void_p]),
+    "pods_syev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "pods_sytrd": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "pods_syev_status": (c_int, [c_void_p]),
+    "pods_sytrd_trace": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "pods_spatial_modes": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "pods_fourier": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_dbl, c_void_p]),
     "pods_filter_block": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
