@@ -15,13 +15,14 @@ Same entry points and i_d contract as the reference's PODFS.py (Python 3):
   make_inflow_plane(i_d)                                          PODFS.py:1243-1290
 
 The arithmetic runs on the MI355X through libpodsgen (podsgen/): the correlation matrix
-on fp64 MFMA, the eigensolve with torch.linalg.eigh on the GPU, the spatial modes and the
-shifted DFT in HIP kernels.  `A` may be the reference's host array (3P, ns) or the
+on fp64 MFMA, the eigensolve with pods_syev (all eigenvalues + the nm leading vectors;
+torch.linalg.eigh when the full temporal-mode matrix is requested), the spatial modes and
+the shifted DFT in HIP kernels.  `A` may be the reference's host array (3P, ns) or the
 device-resident snapshots handed over by digitalfilters.main() (podsgen.DeviceSnapshots).
 There is no CPU fallback: without the GPU library these functions raise.
 
 Differences from the reference, by design:
-  * the symmetric eigensolver (eigh) replaces dgeev: eigenvalues agree to ~1e-12 of
+  * a symmetric eigensolver replaces dgeev: eigenvalues agree to ~1e-12 of
     lambda_0, eigenvectors up to a per-mode sign (the PODFS reconstruction is invariant);
   * VTK is not used: the inlet geometry is computed analytically with VTK's float32
     rounding chain (make_inflow_plane / cell_centres), and the VTK visualisation writers
@@ -224,7 +225,9 @@ def POD(A, num_snapshots, num_points, num_components, correct_for_cell_volumes, 
                                   "(the only value digitalfilters.main passes); use "
                                   "calculate_correlation_matrix for the weighted form")
     snap = _ctx_for(A, i_d)
-    full = getattr(i_d, "full_temporal_modes", True)
+    # The full (ns x ns) temporal-mode matrix is only consumed by the verbose outputs
+    # (write_temporal_modes, PSD plots); the compressed PODFS output needs T[:, :nm].
+    full = getattr(i_d, "full_temporal_modes", bool(getattr(i_d, "verbose", False)))
     if isinstance(A, _E.DeviceSnapshots):
         res = _E.run_pod(snap, num_modes_trunc, tol_CN=tol_CN, dist=dist, full_temporal=full)
     else:
@@ -256,14 +259,8 @@ def _run_pod_centred(snap, nm, tol_CN, full):
     ns = snap.ns
     C = torch.empty((ns, ns), dtype=torch.float64, device="cuda")
     podsgen.check(ctx.lib.pods_corr(ctx.h, _E.ptr(C), 1), "pods_corr")
-    lam, V = torch.linalg.eigh(C)
-    lam_desc = torch.flip(lam, dims=(0,)).cpu().numpy()
-    nvalid = _num_valid_modes(lam_desc, ns, tol_CN)
-    nmt = nm if (0 <= nm <= nvalid) else nvalid
-    ncols = ns if full else max(nmt, 1)
-    T = torch.empty((ns, ncols), dtype=torch.float64, device="cuda")
-    podsgen.check(ctx.lib.pods_temporal_modes(ctx.h, _E.ptr(V), V.stride(0), V.stride(1), _E.ptr(lam_desc),
-                                              nvalid, ncols, _E.ptr(T)), "pods_temporal_modes")
+    lam_desc, nvalid, nmt, T = _E.eigen_modes(ctx, C, ns, nm, tol_CN, full)
+    ncols = T.shape[1]
     phi = torch.empty((snap.rowlen, max(nmt, 1)), dtype=torch.float64, device="cuda")
     if nmt > 0:
         podsgen.check(ctx.lib.pods_spatial_modes(ctx.h, _E.ptr(T), ncols,

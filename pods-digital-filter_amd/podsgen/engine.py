@@ -10,10 +10,17 @@ Multi-GPU: one process per GPU.  Each rank owns a contiguous slab of inlet rows
 all_reduce (RCCL over xGMI with the "nccl" backend).  Rank 0 solves the eigenproblem
 and broadcasts lambda and T[:, :nm]; every rank then forms its slab of the spatial modes.
 
-PyTorch is used for device memory, the stream, torch.distributed and
-torch.linalg.eigh (the POD eigensolve) -- nothing else.
+Eigensolve: pods_syev (register-resident tridiagonalisation + bisection + inverse
+iteration, all eigenvalues and the nm leading vectors) whenever only the truncated temporal
+modes are needed (ns <= 4096, 0 <= nm <= 64); torch.linalg.eigh (rocSOLVER dsyevd) when the
+full temporal-mode matrix is requested (verbose output), for ns > 4096, or with
+PODS_EIGEN=torch.
+
+PyTorch is used for device memory, the stream, torch.distributed and that fallback
+eigensolve -- nothing else.
 """
 import ctypes
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Optional
@@ -150,7 +157,58 @@ def _dist_info(dist):
     return dist, dist.get_rank(), dist.get_world_size()
 
 
-def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=True,
+SYEV_MAX_N = 4096   # pods_syev's on-chip limit (trd_plan)
+SYEV_MAX_VEC = 64
+
+
+def eigen_modes(ctx: Context, C, ns, nm, tol_CN, full_temporal, tm=None):
+    """Eigensolve + sort + valid-mode count + temporal scaling (PODFS.py:1309-1325).
+
+    Returns (lambda descending (numpy), num_valid, nm_trunc, T (ns x ncols device tensor,
+    ncols = ns if full_temporal else max(nm_trunc, 1)))."""
+    tm = tm or (lambda name: _NullCtx())
+    lib, dev = ctx.lib, C.device
+    method = os.environ.get("PODS_EIGEN", "auto")
+    if method not in ("auto", "pods", "torch"):
+        raise ValueError("PODS_EIGEN must be auto, pods or torch")
+    nvec = max(min(nm, ns), 1) if nm >= 0 else ns
+    use_pods = (method != "torch" and not full_temporal and ns <= SYEV_MAX_N
+                and nvec <= SYEV_MAX_VEC)
+    if method == "pods" and not use_pods:
+        raise ValueError("PODS_EIGEN=pods needs ns <= %d, nm <= %d and truncated temporal modes"
+                         % (SYEV_MAX_N, SYEV_MAX_VEC))
+    if use_pods:
+        lam_t = torch.empty(ns, dtype=torch.float64, device=dev)
+        Y = torch.empty((ns, nvec), dtype=torch.float64, device=dev)
+        with tm("eigh"):
+            check(lib.pods_syev(ctx.h, ptr(C), ns, nvec, ptr(lam_t), ptr(Y)), "pods_syev")
+            check(lib.pods_syev_status(ctx.h), "pods_syev")
+            lam_desc = lam_t.cpu().numpy()
+        nvalid = num_valid_modes(lam_desc, ns, tol_CN)
+        nmt = nm if (0 <= nm <= nvalid) else nvalid
+        ncols = max(min(nmt, nvec), 1)
+        T = torch.empty((ns, ncols), dtype=torch.float64, device=dev)
+        # pods_temporal_modes reads eigh's ascending columns: column ns-1-j of a view with
+        # column stride -1 starting at Y[:, ns-1] is Y[:, j]
+        v0 = ctypes.c_void_p(Y.data_ptr() + (ns - 1) * 8)
+        with tm("temporal"):
+            check(lib.pods_temporal_modes(ctx.h, v0, nvec, -1, ptr(lam_desc), min(nvalid, ncols), ncols,
+                                          ptr(T)), "pods_temporal_modes")
+        return lam_desc, nvalid, nmt, T
+    with tm("eigh"):
+        lam, V = torch.linalg.eigh(C)
+        lam_desc = torch.flip(lam, dims=(0,)).cpu().numpy()
+    nvalid = num_valid_modes(lam_desc, ns, tol_CN)
+    nmt = nm if (0 <= nm <= nvalid) else nvalid
+    ncols = ns if full_temporal else max(nmt, 1)
+    T = torch.empty((ns, ncols), dtype=torch.float64, device=dev)
+    with tm("temporal"):
+        check(lib.pods_temporal_modes(ctx.h, ptr(V), V.stride(0), V.stride(1), ptr(lam_desc),
+                                      min(nvalid, ncols), ncols, ptr(T)), "pods_temporal_modes")
+    return lam_desc, nvalid, nmt, T
+
+
+def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=False,
             keep_C=False, timer=None):
     """PODFS.POD (PODFS.py:1294-1393) with correct_for_cell_volumes='false'."""
     ctx, lib = snap.ctx, snap.ctx.lib
@@ -172,18 +230,8 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
     lam_desc_t = torch.empty(ns, dtype=torch.float64, device=dev)
     T = None
     if rank == 0:
-        with tm("eigh"):
-            lam, V = torch.linalg.eigh(C)
-            lam_desc_t.copy_(torch.flip(lam, dims=(0,)))
-            lam_desc = lam_desc_t.cpu().numpy()
-        nvalid = num_valid_modes(lam_desc, ns, tol_CN)
-        nmt = nm if (0 <= nm <= nvalid) else nvalid
-        ncols = ns if full_temporal else max(nmt, 1)
-        T = torch.empty((ns, ncols), dtype=torch.float64, device=dev)
-        with tm("temporal"):
-            check(lib.pods_temporal_modes(ctx.h, ptr(V), V.stride(0), V.stride(1), ptr(lam_desc),
-                                          nvalid, ncols, ptr(T)), "pods_temporal_modes")
-        del V
+        lam_desc, nvalid, nmt, T = eigen_modes(ctx, C, ns, nm, tol_CN, full_temporal, tm)
+        lam_desc_t.copy_(torch.from_numpy(lam_desc).to(dev))
         meta[0], meta[1] = nvalid, nmt
     if world > 1:
         dist.broadcast(meta, 0)
@@ -296,7 +344,7 @@ class StageTimer:
         return out
 
 
-def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=True, timer=None, gen=None):
+def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=None, gen=None):
     """The whole hot path; returns (Generator, PODResult, FourierResult | None)."""
     dist_, rank, world = _dist_info(dist)
     tm = timer or (lambda name: _NullCtx())

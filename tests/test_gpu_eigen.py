@@ -1,0 +1,138 @@
+"""GPU checks of pods_syev (the POD eigensolve, PODFS.py:1309-1310 + sort_eigenvalues) against
+torch.linalg.eigh (rocSOLVER dsyevd) on the same device matrix.
+
+Tolerances (DESIGN.md 'Parity'):
+  eigenvalues          |dlambda| <= 1e-12 * |lambda_0|            (all n, descending)
+  eigenvectors         ||C y - lambda y|| <= 1e-12 * |lambda_0|, |Y^T Y - I| <= 1e-12,
+                       sign-aligned difference <= 1e-10 for modes with relative gap > 1e-6
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+import podsgen  # noqa: E402
+from podsgen import engine as E  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return E.Context(0)
+
+
+def pod_like(n, seed=0):
+    """C = B^T B / m with temporally smoothed columns: a decaying POD-like spectrum."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    m = max(n + n // 2, 8)
+    B = torch.randn(m, n, generator=g, dtype=torch.float64)
+    k = torch.exp(-0.5 * (torch.arange(-12, 13, dtype=torch.float64) / 4.0) ** 2)
+    Bs = torch.nn.functional.conv1d(B.unsqueeze(1), k.view(1, 1, -1), padding=12).squeeze(1) + 0.05 * B
+    Bd = Bs.cuda()
+    C = Bd.T @ Bd / m
+    return (0.5 * (C + C.T)).contiguous()
+
+
+def solve(ctx, C, nvec):
+    n = C.shape[0]
+    lam = torch.empty(n, dtype=torch.float64, device="cuda")
+    Y = torch.empty((n, max(nvec, 1)), dtype=torch.float64, device="cuda")
+    podsgen.check(ctx.lib.pods_syev(ctx.h, E.ptr(C), n, nvec, E.ptr(lam), E.ptr(Y)), "pods_syev")
+    podsgen.check(ctx.lib.pods_syev_status(ctx.h), "pods_syev_status")
+    return lam.cpu().numpy(), Y.cpu().numpy()[:, :nvec]
+
+
+def check_against_eigh(C, lam, Y):
+    n = C.shape[0]
+    lr, Vr = torch.linalg.eigh(C)
+    lr = torch.flip(lr, (0,)).cpu().numpy()
+    Vr = torch.flip(Vr, (1,)).cpu().numpy()
+    scale = max(abs(lr[0]), abs(lr[-1]), 1e-300)
+    assert np.all(np.diff(lam) <= 0), "not descending"
+    assert np.max(np.abs(lam - lr)) <= 1e-12 * scale
+    nv = Y.shape[1]
+    if nv == 0:
+        return
+    Ch = C.cpu().numpy()
+    res = np.linalg.norm(Ch @ Y - Y * lam[:nv], axis=0)
+    assert np.max(res) <= 1e-12 * scale
+    assert np.max(np.abs(Y.T @ Y - np.eye(nv))) <= 1e-12
+    gl = np.abs(np.diff(lr)) / scale
+    gap = np.minimum(np.r_[gl, np.inf][:nv], np.r_[np.inf, gl][:nv])
+    for k in np.nonzero(gap > 1e-6)[0]:
+        s = np.sign(np.dot(Y[:, k], Vr[:, k]))
+        assert np.max(np.abs(s * Y[:, k] - Vr[:, k])) <= 1e-10, (n, k)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 17, 64, 255, 256, 257, 511, 512, 513, 1000, 1024, 1025,
+                               2048, 2049, 3000, 4095, 4096])
+def test_syev_pod_like(ctx, n):
+    C = pod_like(n, seed=n)
+    nvec = min(n, 20)
+    lam, Y = solve(ctx, C, nvec)
+    check_against_eigh(C, lam, Y)
+
+
+def test_syev_values_only_and_64_vectors(ctx):
+    C = pod_like(700, seed=3)
+    lam0, _ = solve(ctx, C, 0)
+    lam1, Y = solve(ctx, C, 64)
+    assert np.array_equal(lam0, lam1)
+    check_against_eigh(C, lam1, Y)
+
+
+def test_syev_special_matrices(ctx):
+    # diagonal (already tridiagonal: every reflector is the identity)
+    d = torch.linspace(3.0, -1.0, 300, dtype=torch.float64, device="cuda")
+    lam, Y = solve(ctx, torch.diag(d).contiguous(), 5)
+    assert np.allclose(lam, np.sort(d.cpu().numpy())[::-1], rtol=0, atol=1e-14)
+    # zero matrix
+    lam, Y = solve(ctx, torch.zeros((100, 100), dtype=torch.float64, device="cuda"), 3)
+    assert np.all(np.abs(lam) <= 1e-290)
+    assert np.allclose(np.abs(Y.T @ Y), np.eye(3), atol=1e-12)
+    # exactly repeated eigenvalues: I + u u^T (eigenvalue 1 with multiplicity n-1)
+    n = 400
+    u = torch.randn(n, dtype=torch.float64, device="cuda")
+    C = (torch.eye(n, dtype=torch.float64, device="cuda") + torch.outer(u, u)).contiguous()
+    lam, Y = solve(ctx, C, 6)
+    check_against_eigh(C, lam, Y)   # the degenerate modes are skipped by the gap rule
+    # orthonormal basis of the degenerate subspace anyway
+    assert np.max(np.abs(Y.T @ Y - np.eye(6))) <= 1e-12
+
+
+def test_syev_deterministic(ctx):
+    C = pod_like(1500, seed=9)
+    a = solve(ctx, C, 20)
+    b = solve(ctx, C, 20)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_sytrd_similarity(ctx):
+    """T from pods_sytrd has C's spectrum (eigvalsh_tridiagonal on the host)."""
+    from scipy.linalg import eigvalsh_tridiagonal
+    n = 2600
+    C = pod_like(n, seed=1)
+    d = np.zeros(n)
+    e = np.zeros(n - 1)
+    podsgen.check(ctx.lib.pods_sytrd(ctx.h, E.ptr(C), n, E.ptr(d), E.ptr(e)), "pods_sytrd")
+    lt = np.sort(eigvalsh_tridiagonal(d, e))[::-1]
+    lr = torch.flip(torch.linalg.eigvalsh(C), (0,)).cpu().numpy()
+    assert np.max(np.abs(lt - lr)) <= 1e-12 * lr[0]
+
+
+def test_eigen_modes_paths_agree(ctx, monkeypatch):
+    """eigen_modes via pods_syev (truncated T) == via torch eigh (full T), first nm columns."""
+    n, nm = 900, 20
+    C = pod_like(n, seed=4)
+    E.load_snapshots(np.random.default_rng(0).standard_normal((48, n)), ctx=ctx)  # sets ns
+    monkeypatch.setenv("PODS_EIGEN", "pods")
+    la, nva, nma, Ta = E.eigen_modes(ctx, C, n, nm, 1e-15, False)
+    monkeypatch.setenv("PODS_EIGEN", "torch")
+    lb, nvb, nmb, Tb = E.eigen_modes(ctx, C, n, nm, 1e-15, True)
+    assert (nva, nma) == (nvb, nmb) and Ta.shape == (n, nm) and Tb.shape == (n, n)
+    assert np.max(np.abs(la - lb)) <= 1e-12 * lb[0]
+    Ta, Tb = Ta.cpu().numpy(), Tb.cpu().numpy()[:, :nm]
+    for k in range(nm):
+        s = np.sign(np.dot(Ta[:, k], Tb[:, k]))
+        assert np.max(np.abs(s * Ta[:, k] - Tb[:, k])) <= 1e-9 * np.max(np.abs(Tb[:, k])), k
