@@ -12,7 +12,7 @@
 //              the next column and its Householder vector redundantly from those two vectors,
 //              so no second exchange (norm, dot) is needed.
 //   k_bisect   all eigenvalues of T by Sturm-count multisection (16 lanes per eigenvalue).
-//   k_invit    inverse iteration on T for the wanted eigenvalues (dgttrf-style LU in LDS).
+//   k_twisted  eigenvectors of T for the wanted eigenvalues by twisted factorisation (dlar1v).
 //   k_orth     modified Gram-Schmidt inside eigenvalue clusters (dstein's ORTOL rule).
 //   k_larft / k_bt_*  back-transformation Y = Q Z with compact-WY blocks of 64 reflectors.
 //
@@ -208,9 +208,9 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
   double* Al = lds;                  // [SL][RL][TT]
   double* red = lds + SL * RL * TT;  // 2 x 8 reduction slots
   double* bc = red + 16;             // 4: alpha0 (double-buffered by column parity)
-  double* rsv = bc + 4;              // R: v_{j-1}[r_i]
-  double* rsw = rsv + R;             // R: w_{j-1}[r_i]
-  double* rr = rsw + R;              // R x 8 wave partials
+  double* rsv0 = bc + 4;             // 2 x R: v_{j-1}[r_i]   (double-buffered by column parity:
+  double* rsw0 = rsv0 + 2 * R;       // 2 x R: w_{j-1}[r_i]    the update reads them after B3)
+  double* rr = rsw0 + 2 * R;         // (R + 2) x 8 wave partials (rows, then the two dots)
   const int t0 = threadIdx.x, wv = t0 >> 6;
   const int g0 = blockIdx.x, G = a.G, n = a.n;
   if (g0 >= n) return;
@@ -267,6 +267,8 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
     asm volatile("" : "+v"(t));
     asm volatile("" : "+s"(g));
     const int lane = t & 63;
+    double* rsv = rsv0 + (j & 1) * R;
+    double* rsw = rsw0 + (j & 1) * R;
     // ---- inputs: p_{j-1} (p), column j of A^{(j-1)} (x), p_{j-1}[j] -----------------------
     double p[S], x[S], pj = 0.0;
     if (j == 0) {
@@ -364,28 +366,39 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
       const int c = t + TT * m;
       x[m] = (c == j + 1) ? 1.0 : ((c >= j + 2 && c < n) ? x[m] * scal : 0.0);
     }
-    // ---- rank-2 update of step j-1 fused with p_j = A^{(j)} v_j on rows >= j+1 -------------
-    // Slot-outer, row-inner; RH rows per pass bound the live accumulators; dead rows get zero
-    // multipliers (exact no-op update, sums never published) so no branch touches the
-    // matrix registers.  The lane holding column j+1 publishes that column of its rows.
+    // ---- p_j = A^{(j)} v_j from the stored A^{(j-1)} (dlatrd's correction):
+    // ----   p_j = A^{(j-1)} v_j - v_{j-1} (w_{j-1} . v_j) - w_{j-1} (v_{j-1} . v_j)
+    // ---- so the hand-off needs only a read of the stored rows; the rank-2 update of step
+    // ---- j-1 is applied after the publish, overlapping the next column's hop.
     if (trace) trace[j * 8 + 4] = (int64_t)__builtin_amdgcn_s_memrealtime();
     const __amdgpu_buffer_rsrc_t pw = rsrc8(a.pbuf + (int64_t)(j & 1) * n, n);
     const __amdgpu_buffer_rsrc_t cw = rsrc8(a.rbuf + (int64_t)(j & 1) * n, n);
     const uint32_t tag = (uint32_t)(j + 1);
-    const int mj1 = (j + 1) / TT;
     const bool pubcol = t == ((j + 1) & (TT - 1));
     constexpr int RH = (SG > 0) ? 2 : ((RL % 4 == 0) ? 4 : ((RL % 2 == 0) ? 2 : 1));
+    {
+      double dd[2] = {0.0, 0.0};
+#pragma unroll
+      for (int m = 0; m < S; ++m) {
+        dd[0] = __builtin_fma(p[m], x[m], dd[0]);   // w_{j-1} . v_j
+        dd[1] = __builtin_fma(vp[m], x[m], dd[1]);  // v_{j-1} . v_j
+      }
+      const double sd = rows_wave_sum(dd);          // rows 0,1: dd[0]; rows 2,3: dd[1]
+      if (lane == 0) rr[R * 8 + wv] = sd;
+      if (lane == 32) rr[(R + 1) * 8 + wv] = sd;
+    }
+    // The lane holding column j+1 also publishes column j+1 of A^{(j)} (stored value minus
+    // the pending rank-2 update) for its rows, from the values the symv loop just read.
+    // (j+1 always lies in slot K during range K.)
 #pragma unroll
     for (int h = 0; h < RL / RH; ++h) {
-      double vr[RH], wr[RH], acc[RH];
+      double acc[RH], colv[RH];
       bool live[RH];
 #pragma unroll
       for (int q = 0; q < RH; ++q) {
         const int i = I0 + h * RH + q;
         const int r = g + G * i;
         live[q] = r >= j + 1 && r < n;
-        vr[q] = live[q] ? uniform(rsv[i]) : 0.0;
-        wr[q] = live[q] ? uniform(rsw[i]) : 0.0;
         acc[q] = 0.0;
       }
 #pragma unroll
@@ -403,16 +416,16 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
           } else {
             val = Ar[ii][m - K - SG - SL];
           }
-          val = __builtin_fma(-vr[q], p[m], __builtin_fma(-wr[q], vp[m], val));
-          if (m < K + SG) {
-            if (live[q] && c >= j + 1) wm(m, I0 + ii, t) = val;
-          } else if (m < K + SG + SL) {
-            Al[((m - K - SG) * RL + ii) * TT + t] = val;
-          } else {
-            Ar[ii][m - K - SG - SL] = val;
-          }
           acc[q] = __builtin_fma(val, x[m], acc[q]);
-          if (pubcol && m == mj1 && live[q]) gst(cw, g + G * (I0 + ii), val, tag);
+          if (m == K) colv[q] = val;
+        }
+      }
+      if (pubcol) {
+#pragma unroll
+        for (int q = 0; q < RH; ++q) {
+          const int i = I0 + h * RH + q;
+          if (live[q])
+            gst(cw, g + G * i, __builtin_fma(-rsv[i], p[K], __builtin_fma(-rsw[i], vp[K], colv[q])), tag);
         }
       }
       const double sum = rows_wave_sum(acc);
@@ -424,10 +437,14 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
     if (t >= I0 && t < R) {
       const int r = g + G * t;
       if (r >= j + 1 && r < n) {
-        double sum = rr[t * 8];
+        double sum = rr[t * 8], d1 = rr[R * 8], d2 = rr[(R + 1) * 8];
 #pragma unroll
-        for (int q = 1; q < 8; ++q) sum += rr[t * 8 + q];
-        gst(pw, r, sum, tag);
+        for (int q = 1; q < 8; ++q) {
+          sum += rr[t * 8 + q];
+          d1 += rr[R * 8 + q];
+          d2 += rr[(R + 1) * 8 + q];
+        }
+        gst(pw, r, __builtin_fma(-rsw[t], d2, __builtin_fma(-rsv[t], d1, sum)), tag);
       }
     }
     // the writer's outputs leave after the hand-off so they never delay it
@@ -440,6 +457,41 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
       for (int m = 0; m < S; ++m) {
         const int c = t + TT * m;
         if (c < n) st_sc1(a.V + (int64_t)j * a.ldv + c, x[m]);  // sc1: keep V out of L2
+      }
+    }
+    // ---- rank-2 update of step j-1 on rows >= j+1 (dead rows: zero multipliers, exact
+    // ---- no-op arithmetic, so no branch touches the matrix registers) --------------------
+#pragma unroll
+    for (int h = 0; h < RL / RH; ++h) {
+      double vr[RH], wr[RH];
+      bool live[RH];
+#pragma unroll
+      for (int q = 0; q < RH; ++q) {
+        const int i = I0 + h * RH + q;
+        const int r = g + G * i;
+        live[q] = r >= j + 1 && r < n;
+        vr[q] = live[q] ? uniform(rsv[i]) : 0.0;
+        wr[q] = live[q] ? uniform(rsw[i]) : 0.0;
+      }
+#pragma unroll
+      for (int m = K; m < S; ++m) {
+        const int c = t + TT * m;
+#pragma unroll
+        for (int q = 0; q < RH; ++q) {
+          const int ii = h * RH + q;
+          if (m < K + SG) {
+            if (live[q] && c >= j + 1) {
+              double& ref = wm(m, I0 + ii, t);
+              ref = __builtin_fma(-vr[q], p[m], __builtin_fma(-wr[q], vp[m], ref));
+            }
+          } else if (m < K + SG + SL) {
+            double& ref = Al[((m - K - SG) * RL + ii) * TT + t];
+            ref = __builtin_fma(-vr[q], p[m], __builtin_fma(-wr[q], vp[m], ref));
+          } else {
+            double& ref = Ar[ii][m - K - SG - SL];
+            ref = __builtin_fma(-vr[q], p[m], __builtin_fma(-wr[q], vp[m], ref));
+          }
+        }
       }
     }
     if (trace) trace[j * 8 + 7] = (int64_t)__builtin_amdgcn_s_memrealtime();
@@ -586,106 +638,137 @@ __global__ __launch_bounds__(256) void k_bisect(const double* __restrict__ D,
 }
 
 // -----------------------------------------------------------------------------------------
-// Inverse iteration for eigenvalue lam_desc[k] of T (dstein's role): LU with partial pivoting
-// of T - lam I (dgttrf) in LDS, three solves from a fixed pseudo-random start, unit 2-norm.
-// One workgroup per vector; thread 0 runs the recurrences, the others stage data.
-// Z: n x ldz row-major, column k.
+// Eigenvector of T for lam_desc[k] by a twisted factorisation (LAPACK dlar1v's recurrences):
+// T - lam I = L+ D+ L+^T (top down) = U- D- U-^T (bottom up); the twist index r minimises
+// |gamma_r| = |D+_r + D-_r - (d_r - lam)|, then z_r = 1, z_i = -L+_i z_{i+1} (i < r),
+// z_{i+1} = -U-_i z_i (i >= r), normalised.  One workgroup per vector; thread 0 runs the
+// recurrences out of LDS (d - lam, e, D+ / z, L+, U-: 5n doubles = 160 KB at n = 4096).
 // -----------------------------------------------------------------------------------------
-__device__ __forceinline__ double start_value(int i, int k) {
-  uint32_t h = (uint32_t)i * 0x9E3779B1u ^ ((uint32_t)k + 1u) * 0x85EBCA77u;
-  h ^= h >> 15;
-  h *= 0x2C1B3C6Du;
-  h ^= h >> 12;
-  h *= 0x297A2D39u;
-  h ^= h >> 15;
-  return (double)(h >> 8) * (2.0 / 16777216.0) - 1.0;
-}
-
-__global__ __launch_bounds__(256) void k_invit(const double* __restrict__ D,
-                                               const double* __restrict__ E, int n,
-                                               const double* __restrict__ lam_desc,
-                                               const double* __restrict__ bounds, double* __restrict__ X,
-                                               double* __restrict__ Z, int ldz) {
+__global__ __launch_bounds__(256) void k_twisted(const double* __restrict__ D,
+                                                 const double* __restrict__ E, int n,
+                                                 const double* __restrict__ lam_desc,
+                                                 const double* __restrict__ bounds,
+                                                 double* __restrict__ G, double* __restrict__ Z,
+                                                 int ldz) {
   extern __shared__ double sh[];
-  double* ua = sh;          // U diagonal
-  double* ub = sh + n;      // U first superdiagonal
-  double* uc = sh + 2 * n;  // U second superdiagonal (pivoting fill-in)
-  double* lm = sh + 3 * n;  // multipliers; sign bit of the stored value unused
-  unsigned char* pv = reinterpret_cast<unsigned char*>(sh + 4 * n);
+  double* sa = sh;          // d - lam
+  double* se = sh + n;      // e
+  double* dp = sh + 2 * n;  // D+, then z
+  double* sl = sh + 3 * n;  // L+
+  double* su = sh + 4 * n;  // U-
+  // after the two passes sa (d - lam) is dead: sa[0..3] / sa[4..7] hold the argmin
+  // reduction, sa[8] the twist index (the whole 160 KB of LDS is the five arrays)
+  double* scr = n >= 16 ? sa : sh + 5 * n;  // tiny n: 16 extra doubles are allocated
+  double* rv = scr;
+  double* ri = scr + 4;
   const int k = blockIdx.x, t = threadIdx.x;
   const double lam = lam_desc[k];
-  const double tnorm = fmax(fabs(bounds[0]), fabs(bounds[1]));
-  const double tiny = fmax(DBL_EPSILON * tnorm, DBL_MIN);
-  double* x = X + (int64_t)k * n;
+  const double pivmin = bounds[2], atol = bounds[3];
+  double* g = G + (int64_t)k * n;  // |gamma_i|
   for (int i = t; i < n; i += 256) {
-    ua[i] = D[i] - lam;
-    ub[i] = i < n - 1 ? E[i] : 0.0;
-    lm[i] = i < n - 1 ? E[i] : 0.0;  // subdiagonal, overwritten by the multiplier
-    uc[i] = 0.0;
-    x[i] = start_value(i, k);
+    sa[i] = D[i] - lam;
+    se[i] = i < n - 1 ? E[i] : 0.0;
   }
   __syncthreads();
   if (t == 0) {
-    // dgttrf on (lm = sub, ua = diag, ub = super), fill-in in uc
+    double dpi = sa[0];
     for (int i = 0; i < n - 1; ++i) {
-      const double ai = ua[i], ci = lm[i];
-      if (fabs(ai) >= fabs(ci)) {
-        const double a0 = ai != 0.0 ? ai : tiny;
-        ua[i] = a0;
-        const double f = ci / a0;
-        lm[i] = f;
-        ua[i + 1] = ua[i + 1] - f * ub[i];
-        pv[i] = 0;
-      } else {
-        const double f = ai / ci;
-        ua[i] = ci;
-        lm[i] = f;
-        const double tmp = ub[i];
-        ub[i] = ua[i + 1];
-        ua[i + 1] = tmp - f * ua[i + 1];
-        if (i < n - 2) {
-          uc[i] = ub[i + 1];
-          ub[i + 1] = -f * ub[i + 1];
-        }
-        pv[i] = 1;
+      if (fabs(dpi) < pivmin) dpi = -pivmin;
+      dp[i] = dpi;
+      const double li = se[i] / dpi;
+      sl[i] = li;
+      dpi = sa[i + 1] - li * se[i];
+    }
+    if (fabs(dpi) < pivmin) dpi = -pivmin;
+    dp[n - 1] = dpi;
+    double dmi = sa[n - 1];
+    if (fabs(dmi) < pivmin) dmi = -pivmin;
+    int r = n - 1;
+    double gbest = fabs(dp[n - 1] + dmi - sa[n - 1]);
+    g[n - 1] = gbest;
+    for (int i = n - 2; i >= 0; --i) {
+      const double ui = se[i] / dmi;
+      su[i] = ui;
+      dmi = sa[i] - ui * se[i];
+      if (fabs(dmi) < pivmin) dmi = -pivmin;
+      const double gi = fabs(dp[i] + dmi - sa[i]);
+      g[i] = gi;
+      if (gi < gbest) {
+        gbest = gi;
+        r = i;
       }
     }
-    for (int i = 0; i < n; ++i)
-      if (fabs(ua[i]) < tiny) ua[i] = ua[i] < 0.0 ? -tiny : tiny;
-    for (int it = 0; it < 3; ++it) {
-      // forward: apply P and L^{-1}
-      for (int i = 0; i < n - 1; ++i) {
-        if (pv[i]) {
-          const double xi = x[i], xn = x[i + 1];
-          x[i] = xn;
-          x[i + 1] = xi - lm[i] * xn;
-        } else {
-          x[i + 1] = x[i + 1] - lm[i] * x[i];
+    scr[8] = (double)r;
+  }
+  // A numerically repeated eigenvalue (T split into blocks, e.g. zero or diagonal blocks):
+  // the q-th member of such a cluster twists at the index with the (q+1)-th smallest
+  // |gamma|, which lands each member in a different block.
+  int q = 0;
+  for (int jj = 0; jj < k; ++jj)
+    if (fabs(lam_desc[jj] - lam) <= 4.0 * atol) ++q;
+  if (q > 0) {
+    __syncthreads();
+    for (int round = 0; round <= q; ++round) {
+      double bv = DBL_MAX;
+      int bi = n;
+      for (int i = t; i < n; i += 256) {
+        const double v = g[i];
+        if (v < bv || (v == bv && i < bi)) {
+          bv = v;
+          bi = i;
         }
       }
-      // back substitution with U (3 diagonals)
-      double x2 = 0.0, x1 = 0.0, amax = 0.0;
-      for (int i = n - 1; i >= 0; --i) {
-        const double v = (x[i] - ub[i] * x1 - uc[i] * x2) / ua[i];
-        x[i] = v;
-        x2 = x1;
-        x1 = v;
-        amax = fmax(amax, fabs(v));
+      for (int o = 32; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ov < bv || (ov == bv && oi < bi)) {
+          bv = ov;
+          bi = oi;
+        }
       }
-      const double s = amax > 0.0 ? 1.0 / amax : 1.0;
-      for (int i = 0; i < n; ++i) x[i] = x[i] * s;
+      if ((t & 63) == 0) {
+        rv[t >> 6] = bv;
+        ri[t >> 6] = (double)bi;
+      }
+      __syncthreads();
+      if (t == 0) {
+        int best = 0;
+        for (int w = 1; w < 4; ++w)
+          if (rv[w] < rv[best] || (rv[w] == rv[best] && ri[w] < ri[best])) best = w;
+        scr[8] = ri[best];
+        g[(int)ri[best]] = DBL_MAX;  // excluded from later rounds
+      }
+      __syncthreads();
     }
   }
   __syncthreads();
-  // unit 2-norm
-  __shared__ double red[4];
-  double ss = 0.0;
-  for (int i = t; i < n; i += 256) ss = __builtin_fma(x[i], x[i], ss);
-  ss = wave_sum(ss);
-  if ((t & 63) == 0) red[t >> 6] = ss;
+  if (t == 0) {
+    const int r = (int)scr[8];
+    double* z = dp;
+    z[r] = 1.0;
+    for (int i = r - 1; i >= 0; --i) {
+      double zi = -sl[i] * z[i + 1];
+      // a zero component: use row i+1 of (T - lam I) z = 0 instead (dlar1v)
+      if (z[i + 1] == 0.0 && se[i] != 0.0 && i + 2 < n) zi = -(se[i + 1] / se[i]) * z[i + 2];
+      z[i] = zi;
+    }
+    for (int i = r; i < n - 1; ++i) {
+      double zn = -su[i] * z[i];
+      if (z[i] == 0.0 && se[i] != 0.0 && i >= 1) zn = -(se[i - 1] / se[i]) * z[i - 1];
+      z[i + 1] = zn;
+    }
+  }
   __syncthreads();
-  const double inv = 1.0 / sqrt(red[0] + red[1] + red[2] + red[3]);
-  for (int i = t; i < n; i += 256) Z[(int64_t)i * ldz + k] = x[i] * inv;
+  // unit 2-norm (sa reused as reduction scratch)
+  const double* z = dp;
+  double ss = 0.0;
+  for (int i = t; i < n; i += 256) ss = __builtin_fma(z[i], z[i], ss);
+  ss = wave_sum(ss);
+  __syncthreads();
+  if ((t & 63) == 0) scr[t >> 6] = ss;
+  __syncthreads();
+  const double inv = 1.0 / sqrt((scr[0] + scr[1]) + (scr[2] + scr[3]));
+  for (int i = t; i < n; i += 256) Z[(int64_t)i * ldz + k] = z[i] * inv;
 }
 
 // Modified Gram-Schmidt of the nvec vectors inside clusters |lam_i - lam_k| <= 1e-3 ||T||
@@ -827,24 +910,20 @@ __global__ __launch_bounds__(256) void k_bt_w(const double* __restrict__ V, int6
   }
 }
 
-// W = sum_chunks part (fixed order); W2 = T_b W
-__global__ __launch_bounds__(256) void k_bt_reduce(const double* __restrict__ part, int nchunk,
-                                                   int chunk0, const double* __restrict__ Tb, int nvec,
-                                                   double* __restrict__ W2) {
-  __shared__ double ws[WB][65];
-  const int t = threadIdx.x;
-  for (int o = t; o < WB * nvec; o += 256) {
-    double s = 0.0;
-    for (int ch = chunk0; ch < nchunk; ++ch) s += part[(int64_t)ch * WB * nvec + o];
-    ws[o / nvec][o % nvec] = s;
-  }
+// W = sum_chunks part (fixed order); W2 = T_b W.  One 64-thread workgroup per vector k.
+__global__ __launch_bounds__(64) void k_bt_reduce(const double* __restrict__ part, int nchunk,
+                                                  int chunk0, const double* __restrict__ Tb, int nvec,
+                                                  double* __restrict__ W2) {
+  __shared__ double ws[WB];
+  const int p = threadIdx.x, k = blockIdx.x;
+  double s = 0.0;
+#pragma unroll 8
+  for (int ch = chunk0; ch < nchunk; ++ch) s += part[((int64_t)ch * WB + p) * nvec + k];
+  ws[p] = s;
   __syncthreads();
-  for (int o = t; o < WB * nvec; o += 256) {
-    const int p = o / nvec, k = o % nvec;
-    double s = 0.0;
-    for (int q = p; q < WB; ++q) s = __builtin_fma(Tb[p * WB + q], ws[q][k], s);
-    W2[o] = s;
-  }
+  double w = 0.0;
+  for (int q = p; q < WB; ++q) w = __builtin_fma(Tb[p * WB + q], ws[q], w);
+  W2[p * nvec + k] = w;
 }
 
 // Z[c][k] -= sum_p V[j0+p][c] W2[p][k]
@@ -873,7 +952,7 @@ __global__ __launch_bounds__(256) void k_bt_apply(const double* __restrict__ V, 
 template <int R, int S, int K, int SG, int SL>
 static hipError_t launch_trd_t(const TrdArgs& a, hipStream_t st) {
   constexpr int I0 = (2 * K < R) ? 2 * K : R;
-  const size_t lds = ((size_t)SL * (R - I0) * TT + 16 + 4 + 2 * R + 8 * R) * sizeof(double);
+  const size_t lds = ((size_t)SL * (R - I0) * TT + 16 + 4 + 4 * R + 8 * (R + 2)) * sizeof(double);
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_trd<R, S, K, SG, SL>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
@@ -923,8 +1002,8 @@ hipError_t launch_trd(const TrdArgs& a, int R, hipStream_t st) {
       PODS_TRD(8, 4, 3, 0, 0);
       break;
     case 16:
-      PODS_TRD(16, 8, 0, 2, 2);
-      PODS_TRD(16, 8, 1, 2, 2);
+      PODS_TRD(16, 8, 0, 1, 2);
+      PODS_TRD(16, 8, 1, 1, 2);
       PODS_TRD(16, 8, 2, 0, 2);
       PODS_TRD(16, 8, 3, 0, 1);
       PODS_TRD(16, 8, 4, 0, 0);
@@ -953,11 +1032,11 @@ hipError_t launch_tri_eigvals(const double* D, const double* E, int n, double* b
 
 hipError_t launch_tri_eigvecs(const double* D, const double* E, int n, const double* lam_desc,
                               const double* bounds, int nvec, double* X, double* Z, hipStream_t st) {
-  const size_t lds = (size_t)n * 4 * sizeof(double) + (size_t)n;
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&eig::k_invit),
+  const size_t lds = ((size_t)n * 5 + (n < 16 ? 16 : 0)) * sizeof(double);
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&eig::k_twisted),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(eig::k_invit, dim3(nvec), dim3(256), lds, st, D, E, n, lam_desc, bounds, X, Z,
+  hipLaunchKernelGGL(eig::k_twisted, dim3(nvec), dim3(256), lds, st, D, E, n, lam_desc, bounds, X, Z,
                      nvec);
   hipLaunchKernelGGL(eig::k_orth, dim3(1), dim3(256), 0, st, lam_desc, bounds, n, nvec, Z, nvec);
   return hipGetLastError();
@@ -976,7 +1055,7 @@ hipError_t launch_back_transform(const double* V, int64_t ldv, const double* tau
     const int ch0 = (j0 + 1) / eig::BT_ROWS;  // rows below j0+1 are zero in V_b
     hipLaunchKernelGGL(eig::k_bt_w, dim3(nchunk - ch0), dim3(256), 0, st, V, ldv, n, j0, nb, ch0,
                        (const double*)Z, nvec, nvec, part);
-    hipLaunchKernelGGL(eig::k_bt_reduce, dim3(1), dim3(256), 0, st, (const double*)part, nchunk, ch0,
+    hipLaunchKernelGGL(eig::k_bt_reduce, dim3(nvec), dim3(64), 0, st, (const double*)part, nchunk, ch0,
                        (const double*)Tg + (int64_t)b * eig::WB * eig::WB, nvec, W2);
     hipLaunchKernelGGL(eig::k_bt_apply, dim3(nchunk - ch0), dim3(256), 0, st, V, ldv, n, j0, nb, ch0,
                        (const double*)W2, nvec, Z, nvec);

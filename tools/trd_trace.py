@@ -17,7 +17,7 @@ from podsgen._lib import check, ptr  # noqa: E402
 from podsgen.engine import Context  # noqa: E402
 from eig_probe import corr_like  # noqa: E402
 
-STAGES = ["wait", "dot+B1", "col+B2", "hh", "update", "B3", "publish"]
+STAGES = ["wait", "dot+B1", "col+B2", "hh", "symv", "B3", "pub+upd"]
 
 
 def main():
