@@ -222,6 +222,7 @@ struct pods_ctx {
   int e_G = 0;
   int nitems = 0;
   int64_t items_key = -1;
+  int64_t lund_sj = 0;  // j-stride of the Lund table (0: constant along j)
   int nprog_mean = 0;
   bool mean_valid = false;
   bool have_snapshots = false;  // A holds ns x rowlen snapshots (generated or loaded)
@@ -384,8 +385,18 @@ int pods_df_configure(pods_ctx* c, const pods_df_params* prm, const double* bx, 
   std::copy(by, by + c->NY, taps.begin() + c->NX);
   std::copy(bz, bz + c->NZ, taps.begin() + c->NX + c->NY);
   PODS_HIP(hipMemcpy(c->taps.p, taps.data(), taps.size() * sizeof(double), hipMemcpyHostToDevice));
-  if (lund_host)
+  c->lund_sj = p.kma;
+  if (lund_host) {
     PODS_HIP(hipMemcpy(c->lund.p, lund_host, (size_t)9 * c->Pl * sizeof(double), hipMemcpyHostToDevice));
+    // a profile that does not vary along j (adapt1d's 1-D profiles) is read with j-stride 0
+    bool same = true;
+    for (int e = 0; e < 9 && same; ++e) {
+      const double* row0 = lund_host + (int64_t)e * c->Pl;
+      for (int jj = 1; jj < c->jl && same; ++jj)
+        same = std::memcmp(row0, row0 + (int64_t)jj * p.kma, (size_t)p.kma * sizeof(double)) == 0;
+    }
+    if (same) c->lund_sj = 0;
+  }
   double r9[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
   if (p.rotate) std::memcpy(r9, rot_host, sizeof(r9));
   PODS_HIP(hipMemcpy(c->rot.p, r9, sizeof(r9), hipMemcpyHostToDevice));
@@ -422,8 +433,8 @@ int pods_df_generate(pods_ctx* c) {
                                  c->T1.as<double>(), c->stream));
   PODS_HIP(pods::launch_filter_yz(c->NY, c->T1.as<double>(), taps + c->NX, taps + c->NX + c->NY,
                                   c->NZ, p.ns, c->jl, p.kma, c->Kp, c->Sl, 3, c->lund.as<double>(),
-                                  p.lund_mode, c->rot.as<double>(), p.rotate, c->A.as<double>(),
-                                  c->rowlen, c->stream));
+                                  c->lund_sj, p.lund_mode, c->rot.as<double>(), p.rotate,
+                                  c->A.as<double>(), c->stream));
   c->have_snapshots = true;
   c->mean_valid = false;
   return PODS_OK;
@@ -801,8 +812,7 @@ int pods_filter_block(pods_ctx* c, const double* x, int nfx, int nfy, int nfz, i
   if (!e) e = pods::launch_filter_x(NX, dx.as<double>(), tp, 1, S, 1, 1, dt1.as<double>(), c->stream);
   if (!e)
     e = pods::launch_filter_yz(NY, dt1.as<double>(), tp + NX, tp + NX + NY, NZ, 1, jma, kma, Kp, S, 1,
-                               nullptr, PODS_LUND_NONE, nullptr, 0, dy.as<double>(), (int64_t)jma * kma,
-                               c->stream);
+                               nullptr, 0, PODS_LUND_NONE, nullptr, 0, dy.as<double>(), c->stream);
   if (!e) e = hipMemcpyAsync(y, dy.p, (size_t)jma * kma * 8, hipMemcpyDeviceToHost, c->stream);
   if (!e) e = hipStreamSynchronize(c->stream);
   cleanup();

@@ -179,14 +179,18 @@ __global__ __launch_bounds__(256) void k_mt_generate(const uint32_t* __restrict_
   for (int i = lane; i < MTN; i += 64) mt[i] = src[i];
   wave_sync();
   const int64_t D0 = (int64_t)g * Bs * 312;
-  // per-lane position of double D0 + lane within (plane, offset)
+  // per-lane position of double D0 + lane: plane q, padded row, column -- advanced
+  // incrementally (one 64-bit division per substream instead of one per double)
+  const int rows_pp = (int)(S / Kp);
   int64_t q = (D0 + lane) / S;
-  int64_t o = (D0 + lane) - q * S;
+  int o = (int)((D0 + lane) - q * S);
+  int row = o / Kp, col = o - (o / Kp) * Kp;
   for (int64_t b = 0; b < Bs; ++b) {
     const int64_t Db = D0 + b * 312;
     if (Db >= ntot) break;
     twist_wave(mt, lane);
-    int64_t qq = q, oo = o;
+    int64_t qq = q;
+    int rr = row, cc = col;
 #pragma unroll
     for (int r = 0; r < 5; ++r) {
       const int d = lane + 64 * r;
@@ -195,23 +199,25 @@ __global__ __launch_bounds__(256) void k_mt_generate(const uint32_t* __restrict_
         const uint32_t a = mt_temper(w.x) >> 5, bb = mt_temper(w.y) >> 6;
         const double u = ((double)a * 67108864.0 + (double)bb) / 9007199254740992.0;
         const double val = low + range * u;
-        const int row = (int)(oo / Kp);
-        if (row >= rlo && row < rhi) {
-          const int col = (int)(oo - (int64_t)row * Kp);
-          out[qq * Sl + (int64_t)(row - rlo) * Kp + col] = val;
-        }
+        if (rr >= rlo && rr < rhi) out[qq * Sl + (int64_t)(rr - rlo) * Kp + cc] = val;
       }
-      oo += 64;
-      while (oo >= S) {
-        oo -= S;
-        ++qq;
+      cc += 64;
+      while (cc >= Kp) {
+        cc -= Kp;
+        if (++rr == rows_pp) {
+          rr = 0;
+          ++qq;
+        }
       }
     }
     wave_sync();
-    o += 312;
-    while (o >= S) {
-      o -= S;
-      ++q;
+    col += 312;
+    while (col >= Kp) {
+      col -= Kp;
+      if (++row == rows_pp) {
+        row = 0;
+        ++q;
+      }
     }
   }
 }
@@ -254,100 +260,200 @@ __global__ __launch_bounds__(256) void k_filter_x(const double* __restrict__ R,
 }
 
 // y + z passes, Lund transform, rotation, snapshot store.
-// Block = (row tile of TJ output rows, step i).  y pass streams the TJ+NY-1 padded rows of
-// one column through registers (t2 order b ascending), z pass reads t2 from LDS.
-template <int TJ, int NY>
+// Block = (tile of TJ output rows, step i), 512 threads.  Per component: the y pass streams
+// YR-row groups of one padded column through registers (b ascending, the scipy order) into
+// LDS t2; the z pass gives each thread 16 consecutive outputs of one row from a register
+// window of 16+NZ-1 t2 values (cc ascending).  t2 rows are padded by one double per 16 so the
+// window reads are LDS-bank-conflict-free.  The three components' results stay in registers
+// for the Lund transform (digitalfilters.py:174-176 / :227-229) and the rotation, and each
+// thread stores its 16 consecutive snapshot rows as one 128-B line (K-tiled layout).
+// lund_sj: j-stride of the Lund table (0 when the profile does not vary with j, e.g. the
+// 1-D profiles of adapt1d: the table then stays in L1).
+__device__ __forceinline__ int kpad(int k) { return k + (k >> 4); }
+
+// NZC: compile-time z width (0: runtime NZ <= 25, the generic instance)
+template <int TJ, int NY, int NZC>
 __global__ __launch_bounds__(512) void k_filter_yz(
     const double* __restrict__ T1, const double* __restrict__ by, const double* __restrict__ bz,
-    int NZ, int ns, int jl, int K, int Kp, int64_t Sl, int ncomp,
-    const double* __restrict__ lund, int lund_mode, const double* __restrict__ rot, int rotate,
-    double* __restrict__ AT, int64_t rowlen) {
-  extern __shared__ __attribute__((aligned(16))) double t2[];  // TJ x Kp
-  constexpr int MAXO = 8;
+    int NZr, int ns, int jl, int K, int Kp, int64_t Sl, int ncomp,
+    const double* __restrict__ lund, int64_t lund_sj, int lund_mode, const double* __restrict__ rot,
+    int rotate, double* __restrict__ AT, int nsb) {
+  extern __shared__ __attribute__((aligned(16))) double t2[];  // TJ x ldt
+  constexpr int YR = TJ < 16 ? TJ : 16;  // rows per y-pass item
+  constexpr int NZMAX = NZC > 0 ? NZC : 25;
+  const int NZ = NZC > 0 ? NZC : NZr;
+  constexpr int WIN = 16 + NZMAX - 1;
+  const int ldt = kpad(Kp + 16) + 1;
   const int jt = blockIdx.x * TJ;
-  const int i = blockIdx.y;
-  const int nthr = blockDim.x;
-  const int tid = threadIdx.x;
+  const int tid0 = threadIdx.x;
   const int rows = min(TJ, jl - jt);
   const int64_t Pl = (int64_t)jl * K;
+  const int kch = (K + 15) >> 4;       // 16-wide output chunks per row
+  const int zitems = TJ * kch;         // <= 512 (host guarantees)
   double byr[NY];
 #pragma unroll
   for (int b = 0; b < NY; ++b) byr[b] = by[NY - 1 - b];
-  double res[3][MAXO];
-  for (int c = 0; c < ncomp; ++c) {
-    const double* src = T1 + ((int64_t)c * ns + i) * Sl + (int64_t)jt * Kp;
-    for (int col = tid; col < Kp; col += nthr) {
-      double acc[TJ];
+  double bzr[NZMAX];
 #pragma unroll
-      for (int jj = 0; jj < TJ; ++jj) acc[jj] = 0.0;
+  for (int cc = 0; cc < NZMAX; ++cc) bzr[cc] = cc < NZ ? bz[NZ - 1 - cc] : 0.0;
+  // A Lund table that does not vary along j (lund_sj == 0) is staged once per block in LDS
+  // (9 rows of K, padded like t2) and read conflict-free by the 16-wide output chunks.
+  const bool lsh = lund_sj == 0 && lund_mode >= 0;
+  const int ldl = kpad(K) + 1;
+  double* lt = t2 + (size_t)TJ * ldt;
+  if (lsh) {
+    const int ne = lund_mode == 1 ? 9 : 7;
+    for (int e = 0; e < ne; ++e)
+      for (int k = tid0; k < K; k += 512) lt[e * ldl + kpad(k)] = lund[(int64_t)e * Pl + k];
+  }
+  // NSB consecutive steps per block: each thread's stores for one snapshot-row group then
+  // land on consecutive 128-B lines of the K-tiled layout (steps are contiguous there)
+  const int ib = blockIdx.y * nsb;
+  const int ie = min(ns, ib + nsb);
+#pragma clang loop unroll(disable)
+  for (int i = ib; i < ie; ++i) {
+    // the Lund table pointer is re-materialised per step: otherwise the (step-invariant)
+    // parameter loads are hoisted out of the loop and spill
+    int zero = 0;
+    asm volatile("" : "+s"(zero));
+    const double* lund_i = lund + zero;
+    const double* T1i = T1 + zero;
+    const double* roti = rot + zero;
+    int tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const int zr = tid / kch, zk0 = (tid - (tid / kch) * kch) * 16;
+    const bool zact = tid < zitems && zr < rows;
+    double res[3][16];
 #pragma unroll
-      for (int r = 0; r < TJ + NY - 1; ++r) {
-        if (r < rows + NY - 1) {
-          const double v = src[(int64_t)r * Kp + col];
+    for (int c = 0; c < 3; ++c) {
+      // ncomp is 3 (generator) or 1 (pods_filter_block): the unrolled body is guarded
+      if (c < ncomp) {
+      const double* src = T1i + ((int64_t)c * ns + i) * Sl + (int64_t)jt * Kp;
+      // main items: (column, YR-row group) for the first cmain columns, one per thread;
+      // the remaining halo columns as single-output mini items spread over all threads
+      // (2*Kp items on 512 threads would leave a few threads a second full item)
+      constexpr int GRP = TJ / YR;
+      const int cmain = min(Kp, 512 / GRP);
+      for (int it = tid; it < GRP * cmain; it += 512) {
+        const int grp = it / cmain, col = it - grp * cmain;
+        const int r0 = grp * YR;
+        if (r0 >= rows) continue;
+        // all rows of the column first (clamped to the tile, so every load is in bounds and
+        // they issue back to back), then the taps
+        double v[YR + NY - 1];
+        const int rmax = rows + NY - 2 - r0;
 #pragma unroll
-          for (int jj = 0; jj < TJ; ++jj) {
+        for (int r = 0; r < YR + NY - 1; ++r)
+          v[r] = src[(int64_t)(r0 + min(r, rmax)) * Kp + col];
+        double acc[YR];
+#pragma unroll
+        for (int jj = 0; jj < YR; ++jj) acc[jj] = 0.0;
+#pragma unroll
+        for (int r = 0; r < YR + NY - 1; ++r) {
+#pragma unroll
+          for (int jj = 0; jj < YR; ++jj) {
             const int b = r - jj;
-            if (b >= 0 && b < NY) acc[jj] = acc[jj] + v * byr[b];
+            if (b >= 0 && b < NY) acc[jj] = acc[jj] + v[r] * byr[b];
           }
         }
+#pragma unroll
+        for (int jj = 0; jj < YR; ++jj)
+          if (r0 + jj < rows) t2[(r0 + jj) * ldt + kpad(col)] = acc[jj];
       }
+      for (int it = tid; it < (Kp - cmain) * TJ; it += 512) {
+        const int col = cmain + it / TJ, jj = it - (it / TJ) * TJ;
+        if (jj >= rows) continue;
+        double v[NY];
 #pragma unroll
-      for (int jj = 0; jj < TJ; ++jj)
-        if (jj < rows) t2[jj * Kp + col] = acc[jj];
-    }
-    __syncthreads();
+        for (int b = 0; b < NY; ++b) v[b] = src[(int64_t)(jj + b) * Kp + col];
+        double acc = 0.0;
 #pragma unroll
-    for (int m = 0; m < MAXO; ++m) {
-      const int o = tid + m * nthr;
-      const int jj = o / K, k = o - jj * K;
-      double acc = 0.0;
-      if (jj < rows) {
-        const double* rowp = t2 + jj * Kp + k;
-        for (int cc = 0; cc < NZ; ++cc) acc = acc + rowp[cc] * bz[NZ - 1 - cc];
+        for (int b = 0; b < NY; ++b) acc = acc + v[b] * byr[b];
+        t2[jj * ldt + kpad(col)] = acc;
       }
-      res[c][m] = acc;
-    }
-    __syncthreads();
-  }
-  double R9[9];
-  if (rotate) {
+      __syncthreads();
+      if (zact) {
+        const double* rowp = t2 + zr * ldt;
+        double w[WIN];
 #pragma unroll
-    for (int e = 0; e < 9; ++e) R9[e] = rot[e];
-  }
-  (void)rowlen;
+        for (int e = 0; e < WIN; ++e) w[e] = (e < 16 + NZ - 1) ? rowp[kpad(zk0 + e)] : 0.0;
 #pragma unroll
-  for (int m = 0; m < MAXO; ++m) {
-    const int o = tid + m * nthr;
-    const int jj = o / K, k = o - jj * K;
-    if (jj >= rows) continue;
-    const int64_t p = (int64_t)(jt + jj) * K + k;
-    if (lund_mode < 0) {
-      for (int c = 0; c < ncomp; ++c) AT[at_off(c * Pl + p, i, ns)] = res[c][m];
-      continue;
+        for (int kk = 0; kk < 16; ++kk) {
+          double acc = 0.0;
+#pragma unroll
+          for (int cc = 0; cc < NZMAX; ++cc)
+            if (cc < NZ) acc = acc + w[kk + cc] * bzr[cc];
+          res[c][kk] = acc;
+        }
+      }
+      __syncthreads();
+      }
     }
-    const double xu = res[0][m], xv = res[1][m], xw = res[2][m];
-    const double a00 = lund[0 * Pl + p], a10 = lund[1 * Pl + p], a11 = lund[2 * Pl + p];
-    const double a20 = lund[3 * Pl + p], a21 = lund[4 * Pl + p], a22 = lund[5 * Pl + p];
-    // digitalfilters.py:174-176 (adapt1d) / :227-229 (adapt2prf), left to right, zero terms kept
-    double u = ((a00 * xu + 0.0 * xv) + 0.0 * xw) + lund[6 * Pl + p];
-    double v = (a10 * xu + a11 * xv) + 0.0 * xw;
-    double w = (a20 * xu + a21 * xv) + a22 * xw;
-    if (lund_mode == 1) {
-      v = v + lund[7 * Pl + p];
-      w = w + lund[8 * Pl + p];
+    if (zact) {
+    double R9[9];
+    if (rotate) {
+#pragma unroll
+      for (int e = 0; e < 9; ++e) R9[e] = roti[e];
     }
-    if (rotate) {  // rotate_velocity :1119-1131: numpy R.dot(V) -> OpenBLAS dgemv, whose
-                   // 3-term row dot is fma(R2, w, fma(R0, u, R1*v)) (pinned by golden rot case)
-      const double ur = __builtin_fma(R9[2], w, __builtin_fma(R9[0], u, R9[1] * v));
-      const double vr = __builtin_fma(R9[5], w, __builtin_fma(R9[3], u, R9[4] * v));
-      const double wr = __builtin_fma(R9[8], w, __builtin_fma(R9[6], u, R9[7] * v));
-      u = ur;
-      v = vr;
-      w = wr;
+    const int j = jt + zr;
+    const int64_t p0 = (int64_t)j * K + zk0;
+    const int64_t lbase = (int64_t)j * lund_sj + zk0;
+    // the Lund transform / rotation overwrite res in place
+    double (&out)[3][16] = res;
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      if (lund_mode < 0) continue;
+      double prm[9];
+      if (lsh) {
+        const double* L = lt + kpad(zk0 + kk);
+#pragma unroll
+        for (int e = 0; e < 9; ++e) prm[e] = (e < 7 || lund_mode == 1) ? L[e * ldl] : 0.0;
+      } else {
+        const double* L = lund_i + lbase + kk;
+#pragma unroll
+        for (int e = 0; e < 9; ++e) prm[e] = (e < 7 || lund_mode == 1) ? L[e * Pl] : 0.0;
+      }
+      const double xu = res[0][kk], xv = res[1][kk], xw = res[2][kk];
+      const double a00 = prm[0], a10 = prm[1], a11 = prm[2];
+      const double a20 = prm[3], a21 = prm[4], a22 = prm[5];
+      // digitalfilters.py:174-176 (adapt1d) / :227-229 (adapt2prf), left to right, zero terms kept
+      double u = ((a00 * xu + 0.0 * xv) + 0.0 * xw) + prm[6];
+      double v = (a10 * xu + a11 * xv) + 0.0 * xw;
+      double ww = (a20 * xu + a21 * xv) + a22 * xw;
+      if (lund_mode == 1) {
+        v = v + prm[7];
+        ww = ww + prm[8];
+      }
+      if (rotate) {  // rotate_velocity :1119-1131: numpy R.dot(V) -> OpenBLAS dgemv, whose
+                     // 3-term row dot is fma(R2, w, fma(R0, u, R1*v)) (pinned by golden rot case)
+        const double ur = __builtin_fma(R9[2], ww, __builtin_fma(R9[0], u, R9[1] * v));
+        const double vr = __builtin_fma(R9[5], ww, __builtin_fma(R9[3], u, R9[4] * v));
+        const double wr = __builtin_fma(R9[8], ww, __builtin_fma(R9[6], u, R9[7] * v));
+        u = ur;
+        v = vr;
+        ww = wr;
+      }
+      out[0][kk] = u;
+      out[1][kk] = v;
+      out[2][kk] = ww;
     }
-    AT[at_off(p, i, ns)] = u;
-    AT[at_off(Pl + p, i, ns)] = v;
-    AT[at_off(2 * Pl + p, i, ns)] = w;
+    const int nk = min(16, K - zk0);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      if (c >= ncomp) break;
+      const int64_t r0 = c * Pl + p0;
+      if (nk == 16 && (r0 & 15) == 0) {
+        // one full 128-B line of the K-tiled layout
+        double2* dst = reinterpret_cast<double2*>(AT + at_off(r0, i, ns));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dst[e] = make_double2(out[c][2 * e], out[c][2 * e + 1]);
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk)
+          if (kk < nk) AT[at_off(r0 + kk, i, ns)] = out[c][kk];
+      }
+    }
+    }
   }
 }
 
@@ -891,32 +997,72 @@ hipError_t launch_filter_x(int NX, const double* R, const double* bx, int ns, in
   }
 }
 
-static constexpr int YZ_TJ = 8;
+// Row-tile height for the y/z kernel: 32 rows when 32 x ceil(K/16) z items fit 512 threads.
+static int yz_tj(int K) {
+  const int kch = (K + 15) / 16;
+  if (32 * kch <= 512) return 32;
+  if (16 * kch <= 512) return 16;
+  if (8 * kch <= 512) return 8;
+  return 0;
+}
+
+template <int TJ, int NY, int NZC>
+static hipError_t launch_fyz_t(const double* T1, const double* by, const double* bz, int NZ, int ns,
+                               int jl, int K, int Kp, int64_t Sl, int ncomp, const double* lund,
+                               int64_t lund_sj, int lund_mode, const double* rot, int rotate,
+                               double* AT, hipStream_t st) {
+  const int ldt = (Kp + 16) + ((Kp + 16) >> 4) + 1;
+  const int ldl = K + (K >> 4) + 1;
+  const size_t lds = ((size_t)TJ * ldt + (lund_sj == 0 ? 9 * (size_t)ldl : 0)) * sizeof(double);
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_filter_yz<TJ, NY, NZC>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  // enough blocks to fill the chip twice over, at most 16 steps each
+  const int tiles = (jl + TJ - 1) / TJ;
+  const int nsb = (int)std::max<int64_t>(1, std::min<int64_t>(16, (int64_t)tiles * ns / 512));
+  const dim3 grid((unsigned)tiles, (unsigned)((ns + nsb - 1) / nsb));
+  hipLaunchKernelGGL((k_filter_yz<TJ, NY, NZC>), grid, dim3(512), lds, st, T1, by, bz, NZ, ns, jl, K,
+                     Kp, Sl, ncomp, lund, lund_sj, lund_mode, rot, rotate, AT, nsb);
+  return hipGetLastError();
+}
+
+template <int TJ, int NY>
+static hipError_t launch_fyz_tj(const double* T1, const double* by, const double* bz, int NZ, int ns,
+                                int jl, int K, int Kp, int64_t Sl, int ncomp, const double* lund,
+                                int64_t lund_sj, int lund_mode, const double* rot, int rotate,
+                                double* AT, hipStream_t st) {
+  if (NZ == NY)  // isotropic y/z widths: the z taps are compile-time too
+    return launch_fyz_t<TJ, NY, NY>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj, lund_mode,
+                                    rot, rotate, AT, st);
+  return launch_fyz_t<TJ, NY, 0>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj, lund_mode,
+                                 rot, rotate, AT, st);
+}
 
 template <int NY>
 static hipError_t launch_fyz(const double* T1, const double* by, const double* bz, int NZ, int ns,
                              int jl, int K, int Kp, int64_t Sl, int ncomp, const double* lund,
-                             int lund_mode, const double* rot, int rotate, double* AT,
-                             int64_t rowlen, hipStream_t st) {
-  int nthr = ((Kp + 63) / 64) * 64;
-  if (nthr > 512) nthr = 512;
-  // MAXO = 8 outputs per thread per component
-  if ((int64_t)YZ_TJ * K > (int64_t)8 * nthr) return hipErrorInvalidConfiguration;
-  dim3 grid((unsigned)((jl + YZ_TJ - 1) / YZ_TJ), (unsigned)ns);
-  const size_t lds = (size_t)YZ_TJ * Kp * sizeof(double);
-  hipLaunchKernelGGL((k_filter_yz<YZ_TJ, NY>), grid, dim3(nthr), lds, st, T1, by, bz, NZ, ns, jl, K,
-                     Kp, Sl, ncomp, lund, lund_mode, rot, rotate, AT, rowlen);
-  return hipGetLastError();
+                             int64_t lund_sj, int lund_mode, const double* rot, int rotate,
+                             double* AT, hipStream_t st) {
+  if (NZ > 25) return hipErrorInvalidValue;
+  switch (yz_tj(K)) {
+    case 32: return launch_fyz_tj<32, NY>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj,
+                                          lund_mode, rot, rotate, AT, st);
+    case 16: return launch_fyz_tj<16, NY>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj,
+                                          lund_mode, rot, rotate, AT, st);
+    case 8: return launch_fyz_tj<8, NY>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj,
+                                        lund_mode, rot, rotate, AT, st);
+    default: return hipErrorInvalidConfiguration;
+  }
 }
 
 hipError_t launch_filter_yz(int NY, const double* T1, const double* by, const double* bz, int NZ,
                             int ns, int jl, int K, int Kp, int64_t Sl, int ncomp,
-                            const double* lund, int lund_mode, const double* rot, int rotate,
-                            double* AT, int64_t rowlen, hipStream_t st) {
+                            const double* lund, int64_t lund_sj, int lund_mode, const double* rot,
+                            int rotate, double* AT, hipStream_t st) {
   switch (NY) {
 #define PODS_FYZ(n) \
   case n:           \
-    return launch_fyz<n>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_mode, rot, rotate, AT, rowlen, st);
+    return launch_fyz<n>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj, lund_mode, rot, rotate, AT, st);
     PODS_FYZ(1) PODS_FYZ(3) PODS_FYZ(5) PODS_FYZ(7) PODS_FYZ(9) PODS_FYZ(11) PODS_FYZ(13)
     PODS_FYZ(15) PODS_FYZ(17) PODS_FYZ(19) PODS_FYZ(21) PODS_FYZ(23) PODS_FYZ(25)
 #undef PODS_FYZ
@@ -926,9 +1072,8 @@ hipError_t launch_filter_yz(int NY, const double* T1, const double* by, const do
 }
 
 int filter_yz_max_K(int Kp) {
-  int nthr = ((Kp + 63) / 64) * 64;
-  if (nthr > 512) nthr = 512;
-  return 8 * nthr / YZ_TJ;
+  (void)Kp;
+  return 512;  // 8-row tiles x 32 chunks of 16 outputs
 }
 
 hipError_t launch_mean(const double* AT, int64_t rowlen, int ns, const int* prog, int nprog,
