@@ -380,6 +380,7 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
       double dd[2] = {0.0, 0.0};
 #pragma unroll
       for (int m = 0; m < S; ++m) {
+        if (m >= K && m < K + SG) continue;         // slab columns are updated in the symv
         dd[0] = __builtin_fma(p[m], x[m], dd[0]);   // w_{j-1} . v_j
         dd[1] = __builtin_fma(vp[m], x[m], dd[1]);  // v_{j-1} . v_j
       }
@@ -390,9 +391,26 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
     // The lane holding column j+1 also publishes column j+1 of A^{(j)} (stored value minus
     // the pending rank-2 update) for its rows, from the values the symv loop just read.
     // (j+1 always lies in slot K during range K.)
+    // Slab slots (L2-resident, SG > 0) get the rank-2 update of step j-1 here, in the same
+    // pass that reads them (one read + one write per column, straight-line code so all the
+    // loads issue up front), and enter the row sums as A^{(j)}; the dlatrd corrections
+    // above cover the other columns only.
+    // slab loads run SPF row groups ahead (the publish stores in between would otherwise pin
+    // each load behind the previous group's stores and serialise the L2 round trips)
+    constexpr int SPF = K == 0 ? 0 : 3;  // range 0 has no registers to spare
+    double slab[SG > 0 ? RL : 1][SG > 0 ? SG : 1];
+#pragma unroll
+    for (int ii = 0; ii < (SG > 0 ? SPF * RH : 0); ++ii)
+#pragma unroll
+      for (int m = K; m < K + SG; ++m) slab[ii][m - K] = wm(m, I0 + ii, t);
 #pragma unroll
     for (int h = 0; h < RL / RH; ++h) {
-      double acc[RH], colv[RH];
+#pragma unroll
+      for (int ii = (h + SPF) * RH; ii < (SG > 0 ? (h + SPF + 1) * RH : 0); ++ii)
+        if (ii < RL)
+#pragma unroll
+          for (int m = K; m < K + SG; ++m) slab[ii][m - K] = wm(m, I0 + ii, t);
+      double acc[RH], colv[RH], vr[RH], wr[RH];
       bool live[RH];
 #pragma unroll
       for (int q = 0; q < RH; ++q) {
@@ -400,6 +418,10 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
         const int r = g + G * i;
         live[q] = r >= j + 1 && r < n;
         acc[q] = 0.0;
+        if (SG > 0) {
+          vr[q] = live[q] ? uniform(rsv[i]) : 0.0;
+          wr[q] = live[q] ? uniform(rsw[i]) : 0.0;
+        }
       }
 #pragma unroll
       for (int m = K; m < S; ++m) {
@@ -409,8 +431,11 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
           const int ii = h * RH + q;
           double val;
           if (m < K + SG) {
-            val = 0.0;
-            if (live[q] && c >= j + 1) val = wm(m, I0 + ii, t);
+            const double old = slab[ii][m - K];
+            const bool upd = live[q] && c >= j + 1;
+            const double nv = __builtin_fma(-vr[q], p[m], __builtin_fma(-wr[q], vp[m], old));
+            if (upd) wm(m, I0 + ii, t) = nv;
+            val = upd ? nv : 0.0;
           } else if (m < K + SG + SL) {
             val = Al[((m - K - SG) * RL + ii) * TT + t];
           } else {
@@ -425,7 +450,10 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
         for (int q = 0; q < RH; ++q) {
           const int i = I0 + h * RH + q;
           if (live[q])
-            gst(cw, g + G * i, __builtin_fma(-rsv[i], p[K], __builtin_fma(-rsw[i], vp[K], colv[q])), tag);
+            gst(cw, g + G * i,
+                SG > 0 ? colv[q]
+                       : __builtin_fma(-rsv[i], p[K], __builtin_fma(-rsw[i], vp[K], colv[q])),
+                tag);
         }
       }
       const double sum = rows_wave_sum(acc);
@@ -474,16 +502,11 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
         wr[q] = live[q] ? uniform(rsw[i]) : 0.0;
       }
 #pragma unroll
-      for (int m = K; m < S; ++m) {
-        const int c = t + TT * m;
+      for (int m = K + SG; m < S; ++m) {  // slab slots were updated in the symv pass
 #pragma unroll
         for (int q = 0; q < RH; ++q) {
           const int ii = h * RH + q;
           if (m < K + SG) {
-            if (live[q] && c >= j + 1) {
-              double& ref = wm(m, I0 + ii, t);
-              ref = __builtin_fma(-vr[q], p[m], __builtin_fma(-wr[q], vp[m], ref));
-            }
           } else if (m < K + SG + SL) {
             double& ref = Al[((m - K - SG) * RL + ii) * TT + t];
             ref = __builtin_fma(-vr[q], p[m], __builtin_fma(-wr[q], vp[m], ref));
