@@ -138,7 +138,7 @@ int pods_sytrd(pods_ctx* ctx, const double* C_dev, int n, double* d_host, double
 /* Diagnostics: pods_sytrd with 8 s_memrealtime (100 MHz) stamps per column of workgroup
  * wg written to trace_host (n x 8 int64): column start, inputs arrived, after the dot
  * reduction, after the norm reduction, update start, update end, after the row-sum
- * barrier, column end. */
+ * barrier, column end.  wg < 0 traces every workgroup: trace_host holds 256 x n x 8. */
 int pods_sytrd_trace(pods_ctx* ctx, const double* C_dev, int n, int wg, int64_t* trace_host);
 /* 0 if the last pods_syev / pods_sytrd ran to completion, PODS_ERR_INTERNAL if its
  * cross-workgroup wait timed out (results invalid).  Synchronises the stream. */

@@ -177,6 +177,18 @@ __device__ __forceinline__ void gst(__amdgpu_buffer_rsrc_t r, int idx, double v,
 }
 
 constexpr int SPIN_LIMIT = 1 << 20;  // ~1 s of polling before a workgroup raises the abort word
+// The hand-off vectors are published in NREP copies, one per XCD: every consumer polls the copy
+// of its own XCD, so no line is requested by more than the 32 workgroups of one XCD.
+constexpr int NREP = 8;
+__device__ __forceinline__ int xcc_id() {
+  int x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & 15;
+}
+// buffer (p or column) for replica r, column parity q
+__device__ __forceinline__ double* hbuf(double* base, int r, int q, int n) {
+  return base + ((int64_t)r * 2 + q) * n;
+}
 
 // -----------------------------------------------------------------------------------------
 // k_trd<R, S, K, SG, SL>: one column range of the tridiagonalisation.
@@ -211,6 +223,7 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
   double* rsv0 = bc + 4;             // 2 x R: v_{j-1}[r_i]   (double-buffered by column parity:
   double* rsw0 = rsv0 + 2 * R;       // 2 x R: w_{j-1}[r_i]    the update reads them after B3)
   double* rr = rsw0 + 2 * R;         // (R + 2) x 8 wave partials (rows, then the two dots)
+  double* rcol = rr + 8 * (R + 2);   // R: column j+1 of A^{(j)} at this workgroup's rows
   const int t0 = threadIdx.x, wv = t0 >> 6;
   const int g0 = blockIdx.x, G = a.G, n = a.n;
   if (g0 >= n) return;
@@ -258,7 +271,10 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
   if (jb > 0) tau_p = a.tau[jb - 1];
   int rk = 0;
 
-  int64_t* trace = (a.trace && g0 == a.trace_wg && t0 == 0) ? a.trace : nullptr;
+  const int xrep = xcc_id() % a.nrep;
+  int64_t* trace = (a.trace && (g0 == a.trace_wg || a.trace_wg < 0) && t0 == 0)
+                       ? a.trace + (a.trace_wg < 0 ? (int64_t)g0 * n * 8 : 0)
+                       : nullptr;
   for (int j = jb; j < je; ++j) {
     if (trace) trace[j * 8 + 0] = (int64_t)__builtin_amdgcn_s_memrealtime();
     // Re-materialise the lane/workgroup indices every column: without this the compiler
@@ -271,6 +287,7 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
     double* rsw = rsw0 + (j & 1) * R;
     // ---- inputs: p_{j-1} (p), column j of A^{(j-1)} (x), p_{j-1}[j] -----------------------
     double p[S], x[S], pj = 0.0;
+    int nspin = 0;
     if (j == 0) {
 #pragma unroll
       for (int m = 0; m < S; ++m) {
@@ -279,8 +296,8 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
         x[m] = c < n ? a.C[c] : 0.0;
       }
     } else {
-      const __amdgpu_buffer_rsrc_t rp = rsrc8(a.pbuf + (int64_t)((j - 1) & 1) * n, n);
-      const __amdgpu_buffer_rsrc_t rc = rsrc8(a.rbuf + (int64_t)((j - 1) & 1) * n, n);
+      const __amdgpu_buffer_rsrc_t rp = rsrc8(hbuf(a.pbuf, xrep, (j - 1) & 1, n), n);
+      const __amdgpu_buffer_rsrc_t rc = rsrc8(hbuf(a.rbuf, xrep, (j - 1) & 1, n), n);
       const uint32_t want = (uint32_t)j;
       // Every spin re-reads all of this lane's granules (simple straight-line code keeps the
       // register allocation flat); the wave leaves when all its lanes saw the tag.
@@ -288,6 +305,13 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
         bool ok = true;
 #pragma unroll
         for (int m = 0; m < S; ++m) {
+          // slots below K hold only columns < j (slot K-1 reaches j = 512K-1 only in the
+          // range's first column): no loads for them
+          if (m < K && (m < K - 1 || j != jb)) {
+            p[m] = 0.0;
+            x[m] = 0.0;
+            continue;
+          }
           const int c = t + TT * m;
           const bool in = c >= j && c < n;
           const double q1 = gld(rp, in ? c : j);
@@ -299,6 +323,7 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
         const double qj = gld(rp, j);
         ok = ok && tag_ok(qj, want);
         pj = qj;
+        nspin = spin;
         if (__all(ok)) break;
         if ((spin & 1023) == 1023) {
           if (ld_flag(abortw) != 0) break;
@@ -310,7 +335,7 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
         __builtin_amdgcn_s_sleep(1);
       }
     }
-    if (trace) trace[j * 8 + 1] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    if (trace) trace[j * 8 + 1] = (int64_t)__builtin_amdgcn_s_memrealtime() | ((int64_t)nspin << 48);
     // ---- w = tau p ; alpha = -tau/2 (w . v) ; w += alpha v  (dsytd2) -------------------
     double dot = 0.0;
 #pragma unroll
@@ -371,8 +396,8 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
     // ---- so the hand-off needs only a read of the stored rows; the rank-2 update of step
     // ---- j-1 is applied after the publish, overlapping the next column's hop.
     if (trace) trace[j * 8 + 4] = (int64_t)__builtin_amdgcn_s_memrealtime();
-    const __amdgpu_buffer_rsrc_t pw = rsrc8(a.pbuf + (int64_t)(j & 1) * n, n);
-    const __amdgpu_buffer_rsrc_t cw = rsrc8(a.rbuf + (int64_t)(j & 1) * n, n);
+    const __amdgpu_buffer_rsrc_t pw = rsrc8(hbuf(a.pbuf, 0, j & 1, n), 2 * NREP * n);
+    const __amdgpu_buffer_rsrc_t cw = rsrc8(hbuf(a.rbuf, 0, j & 1, n), 2 * NREP * n);
     const uint32_t tag = (uint32_t)(j + 1);
     const bool pubcol = t == ((j + 1) & (TT - 1));
     constexpr int RH = (SG > 0) ? 2 : ((RL % 4 == 0) ? 4 : ((RL % 2 == 0) ? 2 : 1));
@@ -449,11 +474,8 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
 #pragma unroll
         for (int q = 0; q < RH; ++q) {
           const int i = I0 + h * RH + q;
-          if (live[q])
-            gst(cw, g + G * i,
-                SG > 0 ? colv[q]
-                       : __builtin_fma(-rsv[i], p[K], __builtin_fma(-rsw[i], vp[K], colv[q])),
-                tag);
+          rcol[i] = SG > 0 ? colv[q]
+                           : __builtin_fma(-rsv[i], p[K], __builtin_fma(-rsw[i], vp[K], colv[q]));
         }
       }
       const double sum = rows_wave_sum(acc);
@@ -462,17 +484,20 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
     if (trace) trace[j * 8 + 5] = (int64_t)__builtin_amdgcn_s_memrealtime();
     __syncthreads();                                                               // B3
     if (trace) trace[j * 8 + 6] = (int64_t)__builtin_amdgcn_s_memrealtime();
-    if (t >= I0 && t < R) {
-      const int r = g + G * t;
-      if (r >= j + 1 && r < n) {
-        double sum = rr[t * 8], d1 = rr[R * 8], d2 = rr[(R + 1) * 8];
+    // publish p_j and column j+1 for this workgroup's rows, one (row, XCD copy) per thread
+    if (t < R * a.nrep) {
+      const int i = t % R, rep_ = t / R;
+      const int r = g + G * i;
+      if (i >= I0 && r >= j + 1 && r < n) {
+        double sum = rr[i * 8], d1 = rr[R * 8], d2 = rr[(R + 1) * 8];
 #pragma unroll
         for (int q = 1; q < 8; ++q) {
-          sum += rr[t * 8 + q];
+          sum += rr[i * 8 + q];
           d1 += rr[R * 8 + q];
           d2 += rr[(R + 1) * 8 + q];
         }
-        gst(pw, r, __builtin_fma(-rsw[t], d2, __builtin_fma(-rsv[t], d1, sum)), tag);
+        gst(pw, rep_ * 2 * n + r, __builtin_fma(-rsw[i], d2, __builtin_fma(-rsv[i], d1, sum)), tag);
+        gst(cw, rep_ * 2 * n + r, rcol[i], tag);
       }
     }
     // the writer's outputs leave after the hand-off so they never delay it
@@ -540,8 +565,8 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
     // tau_{n-2} = 0 (nothing below row n-1), v_{n-2} = e_{n-1}: d = a - 2 w[n-1]
     const int j = n - 1;
     if (t0 == (j & (TT - 1))) {
-      const __amdgpu_buffer_rsrc_t rp = rsrc8(a.pbuf + (int64_t)((j - 1) & 1) * n, n);
-      const __amdgpu_buffer_rsrc_t rc = rsrc8(a.rbuf + (int64_t)((j - 1) & 1) * n, n);
+      const __amdgpu_buffer_rsrc_t rp = rsrc8(hbuf(a.pbuf, 0, (j - 1) & 1, n), n);
+      const __amdgpu_buffer_rsrc_t rc = rsrc8(hbuf(a.rbuf, 0, (j - 1) & 1, n), n);
       double pv = 0.0, cv = 0.0;
       bool np = true, nc = true;
       for (int spin = 0; (np || nc) && spin <= SPIN_LIMIT; ++spin) {
@@ -975,7 +1000,7 @@ __global__ __launch_bounds__(256) void k_bt_apply(const double* __restrict__ V, 
 template <int R, int S, int K, int SG, int SL>
 static hipError_t launch_trd_t(const TrdArgs& a, hipStream_t st) {
   constexpr int I0 = (2 * K < R) ? 2 * K : R;
-  const size_t lds = ((size_t)SL * (R - I0) * TT + 16 + 4 + 4 * R + 8 * (R + 2)) * sizeof(double);
+  const size_t lds = ((size_t)SL * (R - I0) * TT + 16 + 4 + 4 * R + 8 * (R + 2) + R) * sizeof(double);
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_trd<R, S, K, SG, SL>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;

@@ -50,6 +50,7 @@ struct TrdArgs {
   double* Wm;        // per-workgroup slabs G x S x R x 512 (trd_plan's slab_doubles)
   double* pbuf;      // 2 x n tagged values: p = A v (double-buffered by column parity)
   double* rbuf;      // 2 x n tagged values: next column of A (zeroed before the launches)
+  int nrep;          // hand-off copies (1 or 8: one per XCD)
   uint32_t* flags;   // [0]: abort word (set if a hand-off wait timed out), zeroed
   double* D;         // n   diagonal of T
   double* E;         // n-1 off-diagonal of T

@@ -31,6 +31,8 @@ def main():
     for wg in wgs:
         tr = np.zeros((n, 8), dtype=np.int64)
         check(ctx.lib.pods_sytrd_trace(ctx.h, ptr(C), n, wg, ptr(tr)), "pods_sytrd_trace")
+        spins = tr[:, 1] >> 48
+        tr[:, 1] &= (1 << 48) - 1
         ok = tr[:, 0] > 0
         dt = np.diff(tr, axis=1) * 0.01  # 100 MHz -> us
         per = (tr[1:, 0] - tr[:-1, 0]) * 0.01
@@ -44,7 +46,7 @@ def main():
                 continue
             st = dt[sel].mean(axis=0)
             cyc = per[sel[:-1]].mean()
-            print(f"  cols {k:5d}+: per column {cyc:6.2f} us | " +
+            print(f"  cols {k:5d}+: spins {spins[sel].mean():5.2f} per column {cyc:6.2f} us | " +
                   " ".join(f"{nm} {v:5.2f}" for nm, v in zip(STAGES, st)), flush=True)
 
 
