@@ -694,15 +694,15 @@ int pods_syev(pods_ctx* c, const double* C, int n, int nvec, double* lam_desc, d
   PODS_HIP(pods::launch_tri_eigvals(D, E, n, bounds, lam_desc, c->stream));
   if (nvec > 0) {
     const int nblk = std::max((n - 1 + 63) / 64, 1);
-    const int nchunk = (n + 127) / 128;
     PODS_HIP(ensure(c->e_inv, (size_t)nvec * n * sizeof(double)));
     PODS_HIP(ensure(c->e_t, (size_t)nblk * 64 * 64 * sizeof(double)));
-    PODS_HIP(ensure(c->e_part, (size_t)nchunk * 64 * nvec * sizeof(double)));
-    PODS_HIP(ensure(c->e_w2, (size_t)64 * nvec * sizeof(double)));
+    PODS_HIP(ensure(c->e_part, pods::bt_part_bytes(n, nvec)));
+    PODS_HIP(ensure(c->e_w2, pods::bt_w2_bytes(nvec)));
     PODS_HIP(pods::launch_tri_eigvecs(D, E, n, lam_desc, bounds, nvec, c->e_inv.as<double>(), vec,
                                       c->stream));
     PODS_HIP(pods::launch_back_transform(c->e_v.as<double>(), n, tau, n, nvec, c->e_t.as<double>(),
-                                         c->e_part.as<double>(), c->e_w2.as<double>(), vec,
+                                         c->e_part.as<double>(), c->e_w2.as<double>(),
+                                         c->e_flags.as<uint32_t>() + 1, vec,
                                          c->stream));
   }
   return PODS_OK;
@@ -755,11 +755,12 @@ int pods_syev_status(pods_ctx* c) {
   PODS_TRY
   if (int e = check_ctx(c)) return e;
   if (!c->e_flags.p) return PODS_OK;
-  uint32_t abort_word = 0;
-  PODS_HIP(hipMemcpyAsync(&abort_word, c->e_flags.as<uint32_t>() + c->e_G, sizeof(uint32_t),
+  uint32_t abort_word[2] = {0, 0};  // [0]: tridiagonalisation, [1]: back-transformation
+  PODS_HIP(hipMemcpyAsync(abort_word, c->e_flags.as<uint32_t>(), sizeof(abort_word),
                           hipMemcpyDeviceToHost, c->stream));
   PODS_HIP(hipStreamSynchronize(c->stream));
-  if (abort_word) return fail(PODS_ERR_INTERNAL, "pods_syev: hand-off wait timed out (aborted)");
+  if (abort_word[0] || abort_word[1])
+    return fail(PODS_ERR_INTERNAL, "pods_syev: hand-off wait timed out (aborted)");
   return PODS_OK;
   PODS_CATCH
 }

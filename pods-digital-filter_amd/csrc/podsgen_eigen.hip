@@ -865,54 +865,59 @@ __global__ __launch_bounds__(256) void k_orth(const double* __restrict__ lam_des
 // -----------------------------------------------------------------------------------------
 constexpr int WB = 64;
 
+typedef double bt_f64x4 __attribute__((ext_vector_type(4)));
+
+// T_b of block b (one workgroup per block).  Gram matrix G = V_b V_b^T on fp64 MFMA
+// (wave w: rows 16w..16w+15 x all 64 columns, 4 v_mfma_f64_16x16x4 accumulators), V_b staged
+// through LDS 64 columns at a time with the next chunk's loads in flight; then the dlarft
+// recurrence T[0:i, i] = -tau_i T[0:i, 0:i] G[0:i, i], T[i][i] = tau_i.
 __global__ __launch_bounds__(256) void k_larft(const double* __restrict__ V, int64_t ldv,
                                                const double* __restrict__ tau, int n,
                                                double* __restrict__ Tg) {
-  __shared__ double vt[WB][WB + 1];
+  __shared__ double vs[WB][WB + 1];
   __shared__ double gm[WB][WB + 1];
   __shared__ double tm[WB][WB + 1];
   __shared__ double tmp[WB];
-  const int b = blockIdx.x, t = threadIdx.x;
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int j0 = b * WB;
   const int nb = min(WB, n - 1 - j0);
-  // Gram matrix of the block's vectors (upper triangle incl. diagonal): 2080 pairs
-  double acc[9];
-  int pp[9], qq[9];
+  bt_f64x4 acc[4];
 #pragma unroll
-  for (int s = 0; s < 9; ++s) {
-    acc[s] = 0.0;
-    int id = t + 256 * s, p = 0;
-    // pair id -> (p, q), q >= p, row-major over the upper triangle of a 64 x 64
-    while (id >= WB - p) {
-      id -= WB - p;
-      ++p;
-      if (p >= WB) break;
+  for (int q = 0; q < 4; ++q) acc[q] = bt_f64x4{0.0, 0.0, 0.0, 0.0};
+  double st[16];
+  auto load = [&](int cb) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + 256 * u, p = e >> 6, cc = e & 63, c = cb + cc;
+      st[u] = (p < nb && c < n) ? V[(int64_t)(j0 + p) * ldv + c] : 0.0;
     }
-    pp[s] = p;
-    qq[s] = p + id;
-  }
-  for (int c0 = j0 + 1; c0 < n; c0 += WB) {
-    for (int e = t; e < WB * WB; e += 256) {
-      const int p = e / WB, cc = e % WB;
-      vt[p][cc] = (p < nb && c0 + cc < n) ? V[(int64_t)(j0 + p) * ldv + c0 + cc] : 0.0;
-    }
+  };
+  const int cstart = j0 + 1;  // V_b is zero left of column j0 + 1
+  load(cstart);
+  for (int cb = cstart; cb < n; cb += WB) {
     __syncthreads();
 #pragma unroll
-    for (int s = 0; s < 9; ++s) {
-      if (pp[s] < WB) {
-        double a = acc[s];
-        for (int cc = 0; cc < WB; ++cc) a = __builtin_fma(vt[pp[s]][cc], vt[qq[s]][cc], a);
-        acc[s] = a;
+    for (int u = 0; u < 16; ++u) {
+      const int e = t + 256 * u;
+      vs[e >> 6][e & 63] = st[u];
+    }
+    __syncthreads();
+    if (cb + WB < n) load(cb + WB);
+#pragma unroll
+    for (int kk = 0; kk < WB; kk += 4) {
+      const double a = vs[16 * w + (lane & 15)][kk + (lane >> 4)];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double bq = vs[16 * q + (lane & 15)][kk + (lane >> 4)];
+        acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bq, acc[q], 0, 0, 0);
       }
     }
-    __syncthreads();
   }
+  // C/D layout: col = lane & 15, row = (lane >> 4) + 4 r
 #pragma unroll
-  for (int s = 0; s < 9; ++s)
-    if (pp[s] < WB) {
-      gm[pp[s]][qq[s]] = acc[s];
-      gm[qq[s]][pp[s]] = acc[s];
-    }
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) gm[16 * w + (lane >> 4) + 4 * r][16 * q + (lane & 15)] = acc[q][r];
   for (int e = t; e < WB * WB; e += 256) tm[e / WB][e % WB] = 0.0;
   __syncthreads();
   for (int i = 0; i < nb; ++i) {
@@ -930,70 +935,173 @@ __global__ __launch_bounds__(256) void k_larft(const double* __restrict__ V, int
   for (int e = t; e < WB * WB; e += 256) Tg[(int64_t)b * WB * WB + e] = tm[e / WB][e % WB];
 }
 
-constexpr int BT_ROWS = 128;  // rows of Z per workgroup in the back-transformation
-
-// W_part[chunk][p][k] = sum_{c in chunk} V[j0+p][c] Z[c][k]
-__global__ __launch_bounds__(256) void k_bt_w(const double* __restrict__ V, int64_t ldv, int n,
-                                              int j0, int nb, int ch0, const double* __restrict__ Z,
-                                              int ldz, int nvec, double* __restrict__ part) {
-  __shared__ double vs[WB][BT_ROWS + 1];
-  __shared__ double zs[BT_ROWS][65];
-  const int t = threadIdx.x;
-  const int ch = ch0 + blockIdx.x;
-  const int c0 = ch * BT_ROWS;
-  for (int e = t; e < WB * BT_ROWS; e += 256) {
-    const int p = e / BT_ROWS, cc = e % BT_ROWS, c = c0 + cc;
-    vs[p][cc] = (p < nb && c < n) ? V[(int64_t)(j0 + p) * ldv + c] : 0.0;
-  }
-  for (int e = t; e < BT_ROWS * nvec; e += 256) {
-    const int cc = e / nvec, k = e % nvec, c = c0 + cc;
-    zs[cc][k] = c < n ? Z[(int64_t)c * ldz + k] : 0.0;
-  }
-  __syncthreads();
-  for (int o = t; o < WB * nvec; o += 256) {
-    const int p = o / nvec, k = o % nvec;
-    double s = 0.0;
-    for (int cc = 0; cc < BT_ROWS; ++cc) s = __builtin_fma(vs[p][cc], zs[cc][k], s);
-    part[((int64_t)ch * WB + p) * nvec + k] = s;
-  }
+// ---- 16-byte {value, tag} granules for the back-transformation's hand-offs: no value bits
+// ---- are borrowed, the tag is the block iteration + 1 (the buffers are zeroed per call).
+typedef int bt_v4i __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc16(const double* base, int64_t count) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), 0, (int)(count * 16), 0x00020000);
+}
+__device__ __forceinline__ void gst16(__amdgpu_buffer_rsrc_t r, int idx, double v, uint32_t tag) {
+  const long long b = __double_as_longlong(v);
+  bt_v4i q;
+  q.x = (int)(b & 0xffffffffll);
+  q.y = (int)(b >> 32);
+  q.z = (int)tag;
+  q.w = 0;
+  __builtin_amdgcn_raw_buffer_store_b128(q, r, idx * 16, 0, 16u);
+}
+__device__ __forceinline__ bool gld16(__amdgpu_buffer_rsrc_t r, int idx, uint32_t tag, double& v) {
+  const bt_v4i q = __builtin_amdgcn_raw_buffer_load_b128(r, idx * 16, 0, (1u << 31) | 16u);
+  v = __hiloint2double(q.y, q.x);
+  return (uint32_t)q.z == tag;
 }
 
-// W = sum_chunks part (fixed order); W2 = T_b W.  One 64-thread workgroup per vector k.
-__global__ __launch_bounds__(64) void k_bt_reduce(const double* __restrict__ part, int nchunk,
-                                                  int chunk0, const double* __restrict__ Tb, int nvec,
-                                                  double* __restrict__ W2) {
-  __shared__ double ws[WB];
-  const int p = threadIdx.x, k = blockIdx.x;
-  double s = 0.0;
-#pragma unroll 8
-  for (int ch = chunk0; ch < nchunk; ++ch) s += part[((int64_t)ch * WB + p) * nvec + k];
-  ws[p] = s;
-  __syncthreads();
-  double w = 0.0;
-  for (int q = p; q < WB; ++q) w = __builtin_fma(Tb[p * WB + q], ws[q], w);
-  W2[p * nvec + k] = w;
-}
-
-// Z[c][k] -= sum_p V[j0+p][c] W2[p][k]
-__global__ __launch_bounds__(256) void k_bt_apply(const double* __restrict__ V, int64_t ldv, int n,
-                                                  int j0, int nb, int ch0, const double* __restrict__ W2,
-                                                  int nvec, double* __restrict__ Z, int ldz) {
-  __shared__ double vs[WB][BT_ROWS + 1];
-  __shared__ double w2[WB][65];
-  const int t = threadIdx.x;
-  const int c0 = (ch0 + blockIdx.x) * BT_ROWS;
-  for (int e = t; e < WB * BT_ROWS; e += 256) {
-    const int p = e / BT_ROWS, cc = e % BT_ROWS, c = c0 + cc;
-    vs[p][cc] = (p < nb && c < n) ? V[(int64_t)(j0 + p) * ldv + c] : 0.0;
+// One persistent launch for Z <- Q_0 Q_1 ... Q_{nblk-1} Z (blocks applied last to first).
+// Workgroup g owns rows [g*CR, g*CR + CR) of Z in LDS.  Per block: every workgroup with rows
+// below the block's first reflector forms its partial V_b Z (64 x nvec) and publishes it; the
+// workgroup owning vector k (k mod G) sums the partials in workgroup order, multiplies by T_b
+// and publishes column k of W2 = T_b V_b Z; every active workgroup then applies
+// Z -= V_b^T W2 to its rows.  Two hand-offs per block instead of three kernel boundaries.
+template <int CR>
+__global__ __launch_bounds__(256, 1) void k_bt_fused(const double* __restrict__ V, int64_t ldv,
+                                                     const double* __restrict__ Tg, int n, int nvec,
+                                                     int nblk, double* __restrict__ Z, int ldz,
+                                                     double* part, double* w2g, uint32_t* abortw) {
+  extern __shared__ double sm[];
+  const int G = gridDim.x, g = blockIdx.x, t = threadIdx.x;
+  const int c0 = g * CR;
+  const int rows = min(CR, n - c0);
+  const int ldvt = CR + 1;
+  double* zs = sm;                  // CR x nvec
+  double* vt = zs + CR * nvec;      // 64 x (CR + 1): V_b restricted to this workgroup's rows
+  double* wr = vt + 64 * ldvt;      // 64 x nvec: W2
+  double* wk = wr + 64 * nvec;      // 4 x 64: reducer partial sums
+  double* tl = wk + 256;            // 64 x 65: T_b (reducer workgroups)
+  for (int e = t; e < CR * nvec; e += 256) {
+    const int c = e / nvec, k = e - c * nvec;
+    zs[e] = c < rows ? Z[(int64_t)(c0 + c) * ldz + k] : 0.0;
   }
-  for (int o = t; o < WB * nvec; o += 256) w2[o / nvec][o % nvec] = W2[o];
+  const int PW = 64 * nvec;  // granules per workgroup partial
+  const __amdgpu_buffer_rsrc_t rp = rsrc16(part, (int64_t)2 * G * PW);
+  const __amdgpu_buffer_rsrc_t rw = rsrc16(w2g, (int64_t)2 * PW);
+  bool bad = false;
+  for (int it = 0; it < nblk && !bad; ++it) {
+    const int b = nblk - 1 - it, j0 = 64 * b, nb = min(64, n - 1 - j0);
+    const int gmin = (j0 + 1) / CR;
+    const uint32_t tag = (uint32_t)(it + 1);
+    const int par = it & 1;
+    const bool active = g >= gmin;
+    __syncthreads();  // the previous block's apply is done with vt and wr
+    if (g < nvec) {  // T_b for the reducer (all loads in flight together)
+      double tv[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) tv[u] = Tg[(int64_t)b * 64 * 64 + t + 256 * u];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int e = t + 256 * u;
+        tl[(e >> 6) * 65 + (e & 63)] = tv[u];
+      }
+    }
+    if (active) {
+      double vv[CR / 4];
+#pragma unroll
+      for (int u = 0; u < CR / 4; ++u) {
+        const int e = t + 256 * u, p = e / CR, c = e - p * CR;
+        vv[u] = (p < nb && c < rows) ? V[(int64_t)(j0 + p) * ldv + c0 + c] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < CR / 4; ++u) {
+        const int e = t + 256 * u, p = e / CR, c = e - p * CR;
+        vt[p * ldvt + c] = vv[u];
+      }
+      __syncthreads();
+      for (int o = t; o < PW; o += 256) {
+        const int p = o / nvec, k = o - p * nvec;
+        double s = 0.0;
+#pragma unroll 16
+        for (int c = 0; c < CR; ++c) s = __builtin_fma(vt[p * ldvt + c], zs[c * nvec + k], s);
+        gst16(rp, (par * G + g) * PW + o, s, tag);
+      }
+    }
+    // ---- reduction + T_b: vector k by workgroup k mod G, 4 threads per row p ------------------
+    for (int k = g; k < nvec; k += G) {
+      const int p = t & 63, qd = t >> 6;  // quarter qd sums workgroups gmin + qd, +4, +8, ...
+      double s = 0.0;
+      for (int gg0 = gmin + qd; gg0 < G && !bad; gg0 += 64) {
+        double v[16];
+        for (int spin = 0;; ++spin) {
+          bool ok = true;
+#pragma unroll
+          for (int u = 0; u < 16; ++u) {
+            const int gg = gg0 + 4 * u;
+            v[u] = 0.0;
+            if (gg < G) ok = gld16(rp, (par * G + gg) * PW + p * nvec + k, tag, v[u]) && ok;
+          }
+          if (ok) break;
+          if (spin > SPIN_LIMIT || __hip_atomic_load(abortw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            __hip_atomic_store(abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bad = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s += v[u];
+      }
+      wk[qd * 64 + p] = s;
+      __syncthreads();
+      if (t < 64) {
+        const double wsum = ((wk[p] + wk[64 + p]) + wk[128 + p]) + wk[192 + p];
+        wk[p] = wsum;
+      }
+      __syncthreads();
+      if (t < 64) {
+        const double* T = tl + p * 65;
+        double w = 0.0;
+        for (int q = p; q < 64; ++q) w = __builtin_fma(T[q], wk[q], w);
+        gst16(rw, par * PW + p * nvec + k, w, tag);
+      }
+      __syncthreads();
+    }
+    bad = __syncthreads_or(bad);
+    if (!active || bad) continue;
+    // ---- apply: Z -= V_b^T W2 on this workgroup's rows --------------------------------------
+    for (int o0 = 0; o0 < PW; o0 += 256 * 8) {  // up to 8 granules per lane in flight
+      double v[8];
+      for (int spin = 0;; ++spin) {
+        bool ok = true;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int o = o0 + t + 256 * u;
+          v[u] = 0.0;
+          if (o < PW) ok = gld16(rw, par * PW + o, tag, v[u]) && ok;
+        }
+        if (ok) break;
+        if (spin > SPIN_LIMIT || __hip_atomic_load(abortw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          __hip_atomic_store(abortw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          bad = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int o = o0 + t + 256 * u;
+        if (o < PW) wr[o] = v[u];
+      }
+    }
+    bad = __syncthreads_or(bad);
+    for (int o = t; o < rows * nvec; o += 256) {
+      const int c = o / nvec, k = o - c * nvec;
+      double s = 0.0;
+      for (int p = 0; p < 64; ++p) s = __builtin_fma(vt[p * ldvt + c], wr[p * nvec + k], s);
+      zs[o] -= s;
+    }
+  }
   __syncthreads();
-  for (int o = t; o < BT_ROWS * nvec; o += 256) {
-    const int cc = o / nvec, k = o % nvec, c = c0 + cc;
-    if (c >= n) continue;
-    double s = 0.0;
-    for (int p = 0; p < WB; ++p) s = __builtin_fma(vs[p][cc], w2[p][k], s);
-    Z[(int64_t)c * ldz + k] -= s;
+  for (int e = t; e < rows * nvec; e += 256) {
+    const int c = e / nvec, k = e - c * nvec;
+    Z[(int64_t)(c0 + c) * ldz + k] = zs[e];
   }
 }
 
@@ -1091,24 +1199,47 @@ hipError_t launch_tri_eigvecs(const double* D, const double* E, int n, const dou
 }
 
 hipError_t launch_back_transform(const double* V, int64_t ldv, const double* tau, int n, int nvec,
-                                 double* Tg, double* part, double* W2, double* Z, hipStream_t st) {
+                                 double* Tg, double* part, double* W2, uint32_t* abortw, double* Z,
+                                 hipStream_t st) {
   const int nref = n - 1;
-  if (nref <= 0) return hipSuccess;
+  if (nref <= 0 || nvec <= 0) return hipSuccess;
   const int nblk = (nref + eig::WB - 1) / eig::WB;
   hipLaunchKernelGGL(eig::k_larft, dim3(nblk), dim3(256), 0, st, V, ldv, tau, n, Tg);
-  const int nchunk = (n + eig::BT_ROWS - 1) / eig::BT_ROWS;
-  for (int b = nblk - 1; b >= 0; --b) {
-    const int j0 = b * eig::WB;
-    const int nb = std::min(eig::WB, nref - j0);
-    const int ch0 = (j0 + 1) / eig::BT_ROWS;  // rows below j0+1 are zero in V_b
-    hipLaunchKernelGGL(eig::k_bt_w, dim3(nchunk - ch0), dim3(256), 0, st, V, ldv, n, j0, nb, ch0,
-                       (const double*)Z, nvec, nvec, part);
-    hipLaunchKernelGGL(eig::k_bt_reduce, dim3(nvec), dim3(64), 0, st, (const double*)part, nchunk, ch0,
-                       (const double*)Tg + (int64_t)b * eig::WB * eig::WB, nvec, W2);
-    hipLaunchKernelGGL(eig::k_bt_apply, dim3(nchunk - ch0), dim3(256), 0, st, V, ldv, n, j0, nb, ch0,
-                       (const double*)W2, nvec, Z, nvec);
-  }
+  int CR = 0, G = 0;
+  bt_plan(n, nvec, &CR, &G);
+  hipError_t e = hipMemsetAsync(part, 0, bt_part_bytes(n, nvec), st);
+  if (e == hipSuccess) e = hipMemsetAsync(W2, 0, bt_w2_bytes(nvec), st);
+  if (e != hipSuccess) return e;
+  const size_t lds = ((size_t)CR * nvec + 64 * (CR + 1) + 64 * nvec + 256 + 64 * 65) * sizeof(double);
+  const void* fn = CR == 16 ? reinterpret_cast<const void*>(&eig::k_bt_fused<16>)
+                 : CR == 32 ? reinterpret_cast<const void*>(&eig::k_bt_fused<32>)
+                            : reinterpret_cast<const void*>(&eig::k_bt_fused<64>);
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  if (CR == 16)
+    hipLaunchKernelGGL(eig::k_bt_fused<16>, dim3(G), dim3(256), lds, st, V, ldv, (const double*)Tg, n,
+                       nvec, nblk, Z, nvec, part, W2, abortw);
+  else if (CR == 32)
+    hipLaunchKernelGGL(eig::k_bt_fused<32>, dim3(G), dim3(256), lds, st, V, ldv, (const double*)Tg, n,
+                       nvec, nblk, Z, nvec, part, W2, abortw);
+  else
+    hipLaunchKernelGGL(eig::k_bt_fused<64>, dim3(G), dim3(256), lds, st, V, ldv, (const double*)Tg, n,
+                       nvec, nblk, Z, nvec, part, W2, abortw);
   return hipGetLastError();
 }
+
+// rows of Z per workgroup (16, 32 or 64) and workgroups (<= 64) of the back-transformation
+void bt_plan(int n, int nvec, int* CR, int* G) {
+  (void)nvec;
+  const int cr = n <= 1024 ? 16 : (n <= 2048 ? 32 : 64);
+  *CR = cr;
+  *G = (n + cr - 1) / cr;
+}
+size_t bt_part_bytes(int n, int nvec) {
+  int CR = 0, G = 0;
+  bt_plan(n, nvec, &CR, &G);
+  return (size_t)2 * G * 64 * nvec * 16;
+}
+size_t bt_w2_bytes(int nvec) { return (size_t)2 * 64 * nvec * 16; }
 
 }  // namespace pods

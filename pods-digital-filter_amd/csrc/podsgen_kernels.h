@@ -68,9 +68,13 @@ hipError_t launch_tri_eigvals(const double* D, const double* E, int n, double* b
 // Z: n x nvec row-major eigenvectors of T for lam_desc[0..nvec); X: nvec x n scratch
 hipError_t launch_tri_eigvecs(const double* D, const double* E, int n, const double* lam_desc,
                               const double* bounds, int nvec, double* X, double* Z, hipStream_t st);
-// Z <- Q Z with Q = H_0 ... H_{n-2}; Tg: ceil((n-1)/64) x 64 x 64, part: ceil(n/128) x 64 x nvec,
-// W2: 64 x nvec
+// Z <- Q Z with Q = H_0 ... H_{n-2} (one k_larft launch + one persistent k_bt_fused launch);
+// Tg: ceil((n-1)/64) x 64 x 64, part: bt_part_bytes, W2: bt_w2_bytes, abortw: 0 on entry
 hipError_t launch_back_transform(const double* V, int64_t ldv, const double* tau, int n, int nvec,
-                                 double* Tg, double* part, double* W2, double* Z, hipStream_t st);
+                                 double* Tg, double* part, double* W2, uint32_t* abortw, double* Z,
+                                 hipStream_t st);
+void bt_plan(int n, int nvec, int* CR, int* G);
+size_t bt_part_bytes(int n, int nvec);
+size_t bt_w2_bytes(int nvec);
 
 }  // namespace pods
