@@ -632,24 +632,44 @@ __global__ __launch_bounds__(256) void k_tri_bounds(const double* __restrict__ D
   }
 }
 
-// Number of eigenvalues of T below sig (dlaebz's Sturm count, pivmin-guarded).
-__device__ __forceinline__ int sturm_count(const double2* __restrict__ de, int n, double sig,
-                                           double pivmin) {
-  int cnt = 0;
-  double q = 1.0;
-  for (int i = 0; i < n; ++i) {
-    const double2 v = de[i];
-    q = (v.x - sig) - v.y / q;
-    if (fabs(q) < pivmin) q = -pivmin;
-    cnt += q < 0.0 ? 1 : 0;
-  }
-  return cnt;
+// e / q with a refined hardware reciprocal (v_rcp_f64 + one Newton step, ~1 ulp): the
+// Sturm count only needs the sign of each pivot, and this keeps the recurrence's critical
+// path far shorter than an IEEE division.
+__device__ __forceinline__ double fast_div(double e, double q) {
+  double r = __builtin_amdgcn_rcp(q);
+  r = __builtin_fma(r, __builtin_fma(-q, r, 1.0), r);
+  return e * r;
 }
 
-constexpr int BL = 16;  // lanes (shifts) per eigenvalue
+// Numbers of eigenvalues of T below NC shifts at once (dlaebz's Sturm count, pivmin-guarded;
+// the NC recurrences are independent and interleave).
+template <int NC>
+__device__ __forceinline__ void sturm_counts(const double2* __restrict__ de, int n,
+                                             const double (&sig)[NC], double pivmin, int (&cnt)[NC]) {
+  double q[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    q[c] = 1.0;
+    cnt[c] = 0;
+  }
+  for (int i = 0; i < n; ++i) {
+    const double2 v = de[i];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      double qc = (v.x - sig[c]) - fast_div(v.y, q[c]);
+      if (fabs(qc) < pivmin) qc = -pivmin;
+      cnt[c] += qc < 0.0 ? 1 : 0;
+      q[c] = qc;
+    }
+  }
+}
 
-// Eigenvalue k (ascending) of T by multisection: 16 shifts per step split the bracket into 17.
-// Output lam_desc[n-1-k].  LDS: n x {d_i, e_{i-1}^2}.
+constexpr int BL = 16;  // lanes per eigenvalue
+constexpr int NCH = 1;  // shifts per lane: 16 shifts per step split the bracket into 17
+
+// Eigenvalue k (ascending) of T by multisection: shift s = c*BL + l (chain c of lane l) sits
+// at lo + (s+1) (hi-lo)/(BL*NCH+1).  Output lam_desc[n-1-k].  LDS: n x {d_i, e_{i-1}^2}.
+// (The kernel is fp64-issue bound, so fewer shifts per step -- less work per bit -- win.)
 __global__ __launch_bounds__(256) void k_bisect(const double* __restrict__ D,
                                                 const double* __restrict__ E, int n,
                                                 const double* __restrict__ bounds,
@@ -669,14 +689,21 @@ __global__ __launch_bounds__(256) void k_bisect(const double* __restrict__ D,
   for (int it = 0; it < 128; ++it) {
     const bool conv = !active || (hi - lo) <= fmax(atol, 2.0 * DBL_EPSILON * fmax(fabs(lo), fabs(hi)));
     if (__all(conv)) break;
-    const double step = (hi - lo) * (1.0 / (BL + 1));
-    const double sig = lo + step * (double)(l + 1);
-    const int cnt = sturm_count(de, n, sig, pivmin);
-    const unsigned long long m = __ballot(cnt >= k + 1);
-    const uint32_t gm = (uint32_t)((m >> (lane & ~(BL - 1))) & ((1u << BL) - 1));
+    const double step = (hi - lo) * (1.0 / (BL * NCH + 1));
+    double sig[NCH];
+    int cnt[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) sig[c] = lo + step * (double)(c * BL + l + 1);
+    sturm_counts<NCH>(de, n, sig, pivmin, cnt);
+    int f = BL * NCH;  // first shift with count >= k+1
+#pragma unroll
+    for (int c = NCH - 1; c >= 0; --c) {
+      const unsigned long long m = __ballot(cnt[c] >= k + 1);
+      const uint32_t gm = (uint32_t)((m >> (lane & ~(BL - 1))) & ((1u << BL) - 1));
+      if (gm) f = c * BL + __ffs(gm) - 1;
+    }
     if (!conv) {
-      const int f = gm ? __ffs(gm) - 1 : BL;  // first shift with count >= k+1
-      const double nhi = f < BL ? lo + step * (double)(f + 1) : hi;
+      const double nhi = f < BL * NCH ? lo + step * (double)(f + 1) : hi;
       const double nlo = f > 0 ? lo + step * (double)f : lo;
       lo = nlo;
       hi = nhi;
@@ -689,8 +716,11 @@ __global__ __launch_bounds__(256) void k_bisect(const double* __restrict__ D,
 // Eigenvector of T for lam_desc[k] by a twisted factorisation (LAPACK dlar1v's recurrences):
 // T - lam I = L+ D+ L+^T (top down) = U- D- U-^T (bottom up); the twist index r minimises
 // |gamma_r| = |D+_r + D-_r - (d_r - lam)|, then z_r = 1, z_i = -L+_i z_{i+1} (i < r),
-// z_{i+1} = -U-_i z_i (i >= r), normalised.  One workgroup per vector; thread 0 runs the
-// recurrences out of LDS (d - lam, e, D+ / z, L+, U-: 5n doubles = 160 KB at n = 4096).
+// z_{i+1} = -U-_i z_i (i >= r), normalised.  One workgroup per vector.  The two
+// factorisations run concurrently (lane 0 of waves 0 and 1), gamma and its argmin are
+// parallel, the multipliers L+_i = e_i / D+_i and U-_i = e_i / D-_{i+1} are formed in parallel
+// in place of the pivots, and the two halves of z are again two concurrent chains.
+// LDS: d - lam (then z), e, D+ (then L+), D- (then U- shifted by one): 4n doubles + 16.
 // -----------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_twisted(const double* __restrict__ D,
                                                  const double* __restrict__ E, int n,
@@ -699,14 +729,11 @@ __global__ __launch_bounds__(256) void k_twisted(const double* __restrict__ D,
                                                  double* __restrict__ G, double* __restrict__ Z,
                                                  int ldz) {
   extern __shared__ double sh[];
-  double* sa = sh;          // d - lam
+  double* sa = sh;          // d - lam, later z
   double* se = sh + n;      // e
-  double* dp = sh + 2 * n;  // D+, then z
-  double* sl = sh + 3 * n;  // L+
-  double* su = sh + 4 * n;  // U-
-  // after the two passes sa (d - lam) is dead: sa[0..3] / sa[4..7] hold the argmin
-  // reduction, sa[8] the twist index (the whole 160 KB of LDS is the five arrays)
-  double* scr = n >= 16 ? sa : sh + 5 * n;  // tiny n: 16 extra doubles are allocated
+  double* dp = sh + 2 * n;  // D+, later L+
+  double* dm = sh + 3 * n;  // D-, later U- (U-_i at dm[i+1])
+  double* scr = sh + 4 * n;  // 16 doubles of reduction scratch
   double* rv = scr;
   double* ri = scr + 4;
   const int k = blockIdx.x, t = threadIdx.x;
@@ -718,35 +745,85 @@ __global__ __launch_bounds__(256) void k_twisted(const double* __restrict__ D,
     se[i] = i < n - 1 ? E[i] : 0.0;
   }
   __syncthreads();
-  if (t == 0) {
+  // (the serial loops read their operands 16 at a time so one LDS latency covers 16 steps)
+  constexpr int CH = 16;
+  if (t == 0) {  // L+ D+ L+^T, top down
     double dpi = sa[0];
-    for (int i = 0; i < n - 1; ++i) {
-      if (fabs(dpi) < pivmin) dpi = -pivmin;
-      dp[i] = dpi;
-      const double li = se[i] / dpi;
-      sl[i] = li;
-      dpi = sa[i + 1] - li * se[i];
+    for (int i0 = 0; i0 < n - 1; i0 += CH) {
+      double ev[CH], av[CH];
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const int i = min(i0 + u, n - 2);
+        ev[u] = se[i];
+        av[u] = sa[i + 1];
+      }
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        if (i0 + u < n - 1) {
+          if (fabs(dpi) < pivmin) dpi = -pivmin;
+          dp[i0 + u] = dpi;
+          const double li = fast_div(ev[u], dpi);
+          dpi = av[u] - li * ev[u];
+        }
+      }
     }
     if (fabs(dpi) < pivmin) dpi = -pivmin;
     dp[n - 1] = dpi;
+  } else if (t == 64) {  // U- D- U-^T, bottom up
     double dmi = sa[n - 1];
     if (fabs(dmi) < pivmin) dmi = -pivmin;
-    int r = n - 1;
-    double gbest = fabs(dp[n - 1] + dmi - sa[n - 1]);
-    g[n - 1] = gbest;
-    for (int i = n - 2; i >= 0; --i) {
-      const double ui = se[i] / dmi;
-      su[i] = ui;
-      dmi = sa[i] - ui * se[i];
-      if (fabs(dmi) < pivmin) dmi = -pivmin;
-      const double gi = fabs(dp[i] + dmi - sa[i]);
-      g[i] = gi;
-      if (gi < gbest) {
-        gbest = gi;
-        r = i;
+    dm[n - 1] = dmi;
+    for (int i0 = n - 2; i0 >= 0; i0 -= CH) {
+      double ev[CH], av[CH];
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const int i = max(i0 - u, 0);
+        ev[u] = se[i];
+        av[u] = sa[i];
+      }
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        if (i0 - u >= 0) {
+          const double ui = fast_div(ev[u], dmi);
+          dmi = av[u] - ui * ev[u];
+          if (fabs(dmi) < pivmin) dmi = -pivmin;
+          dm[i0 - u] = dmi;
+        }
       }
     }
-    scr[8] = (double)r;
+  }
+  __syncthreads();
+  // |gamma| and its argmin (ties: the larger index, as the sequential bottom-up scan)
+  {
+    double bv = DBL_MAX;
+    int bi = -1;
+    for (int i = t; i < n; i += 256) {
+      const double gi = fabs(dp[i] + dm[i] - sa[i]);
+      g[i] = gi;
+      if (gi <= bv) {
+        bv = gi;
+        bi = i;
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov < bv || (ov == bv && oi > bi)) {
+        bv = ov;
+        bi = oi;
+      }
+    }
+    if ((t & 63) == 0) {
+      rv[t >> 6] = bv;
+      ri[t >> 6] = (double)bi;
+    }
+    __syncthreads();
+    if (t == 0) {
+      int best = 0;
+      for (int w = 1; w < 4; ++w)
+        if (rv[w] < rv[best] || (rv[w] == rv[best] && ri[w] > ri[best])) best = w;
+      scr[8] = ri[best];
+    }
   }
   // A numerically repeated eigenvalue (T split into blocks, e.g. zero or diagonal blocks):
   // the q-th member of such a cluster twists at the index with the (q+1)-th smallest
@@ -774,6 +851,7 @@ __global__ __launch_bounds__(256) void k_twisted(const double* __restrict__ D,
           bi = oi;
         }
       }
+      __syncthreads();
       if ((t & 63) == 0) {
         rv[t >> 6] = bv;
         ri[t >> 6] = (double)bi;
@@ -790,29 +868,58 @@ __global__ __launch_bounds__(256) void k_twisted(const double* __restrict__ D,
     }
   }
   __syncthreads();
+  const int r = (int)scr[8];
+  // multipliers in place: L+_i = e_i / D+_i at dp[i], U-_i = e_i / D-_{i+1} at dm[i+1]
+  for (int i = t; i < n - 1; i += 256) {
+    dp[i] = se[i] / dp[i];
+    dm[i + 1] = se[i] / dm[i + 1];
+  }
+  __syncthreads();
+  double* z = sa;
   if (t == 0) {
-    const int r = (int)scr[8];
-    double* z = dp;
     z[r] = 1.0;
-    for (int i = r - 1; i >= 0; --i) {
-      double zi = -sl[i] * z[i + 1];
-      // a zero component: use row i+1 of (T - lam I) z = 0 instead (dlar1v)
-      if (z[i + 1] == 0.0 && se[i] != 0.0 && i + 2 < n) zi = -(se[i + 1] / se[i]) * z[i + 2];
-      z[i] = zi;
+    double zn1 = 1.0, zn2 = 0.0;  // z[i+1], z[i+2]
+    for (int i0 = r - 1; i0 >= 0; i0 -= CH) {
+      double lv[CH];
+#pragma unroll
+      for (int u = 0; u < CH; ++u) lv[u] = dp[max(i0 - u, 0)];
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const int i = i0 - u;
+        if (i >= 0) {
+          double zi = -lv[u] * zn1;
+          // a zero component: use row i+1 of (T - lam I) z = 0 instead (dlar1v)
+          if (zn1 == 0.0 && se[i] != 0.0 && i + 2 < n) zi = -(se[i + 1] / se[i]) * zn2;
+          z[i] = zi;
+          zn2 = zn1;
+          zn1 = zi;
+        }
+      }
     }
-    for (int i = r; i < n - 1; ++i) {
-      double zn = -su[i] * z[i];
-      if (z[i] == 0.0 && se[i] != 0.0 && i >= 1) zn = -(se[i - 1] / se[i]) * z[i - 1];
-      z[i + 1] = zn;
+  } else if (t == 64) {
+    double zi = 1.0, zp = 0.0;  // z[i], z[i-1]
+    for (int i0 = r; i0 < n - 1; i0 += CH) {
+      double uv[CH];
+#pragma unroll
+      for (int u = 0; u < CH; ++u) uv[u] = dm[min(i0 + u, n - 2) + 1];
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const int i = i0 + u;
+        if (i < n - 1) {
+          double zn = -uv[u] * zi;
+          if (zi == 0.0 && se[i] != 0.0 && i >= 1) zn = -(se[i - 1] / se[i]) * zp;
+          z[i + 1] = zn;
+          zp = zi;
+          zi = zn;
+        }
+      }
     }
   }
   __syncthreads();
-  // unit 2-norm (sa reused as reduction scratch)
-  const double* z = dp;
+  // unit 2-norm
   double ss = 0.0;
   for (int i = t; i < n; i += 256) ss = __builtin_fma(z[i], z[i], ss);
   ss = wave_sum(ss);
-  __syncthreads();
   if ((t & 63) == 0) scr[t >> 6] = ss;
   __syncthreads();
   const double inv = 1.0 / sqrt((scr[0] + scr[1]) + (scr[2] + scr[3]));
@@ -1188,7 +1295,7 @@ hipError_t launch_tri_eigvals(const double* D, const double* E, int n, double* b
 
 hipError_t launch_tri_eigvecs(const double* D, const double* E, int n, const double* lam_desc,
                               const double* bounds, int nvec, double* X, double* Z, hipStream_t st) {
-  const size_t lds = ((size_t)n * 5 + (n < 16 ? 16 : 0)) * sizeof(double);
+  const size_t lds = ((size_t)n * 4 + 16) * sizeof(double);
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&eig::k_twisted),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
