@@ -217,7 +217,7 @@ struct pods_ctx {
   int64_t S = 0, Sl = 0, Pl = 0, rowlen = 0, rowpad = 0;  // rowpad: rowlen rounded up to 16
   RngLayout layout;
   RngBuffers rng;
-  DevBuf R, T1, A, mean, lund, taps, rot, prog_mean, prog_dft, tbuf, mag, lam, cwork, items;
+  DevBuf R, T1, A, mean, lund, taps, rot, prog_mean, prog_dft, tbuf, mag, lam, cwork, items, spwork;
   DevBuf e_wm, e_x, e_flags, e_det, e_v, e_t, e_part, e_w2, e_inv;  // pods_syev workspace
   int e_G = 0;
   int nitems = 0;
@@ -318,7 +318,7 @@ int pods_destroy(pods_ctx* c) {
   for (DevBuf* b : {&c->R, &c->T1, &c->A, &c->mean, &c->lund, &c->taps, &c->rot, &c->prog_mean,
                     &c->prog_dft, &c->tbuf, &c->mag, &c->lam, &c->cwork, &c->items, &c->e_wm,
                     &c->e_x, &c->e_flags, &c->e_det, &c->e_v, &c->e_t, &c->e_part, &c->e_w2,
-                    &c->e_inv})
+                    &c->e_inv, &c->spwork})
     release(*b);
   c->rng.free_all();
   delete c;
@@ -629,8 +629,10 @@ int pods_spatial_modes(pods_ctx* c, const double* T, int ldT, const double* lam,
   for (int m = 0; m < nm; ++m) c->stage[m] = 1.0 / lam[m];  // np.ones(nm)/energy (PODFS.py:1331)
   PODS_HIP(hipMemcpyAsync(c->lam.p, c->stage.data(), (size_t)nm * sizeof(double), hipMemcpyHostToDevice,
                           c->stream));
+  const size_t wb = pods::spatial_work_bytes(c->rowlen, c->p.ns);
+  if (wb) PODS_HIP(ensure(c->spwork, wb));
   PODS_HIP(pods::launch_spatial(c->A.as<double>(), c->rowlen, c->p.ns, c->mean.as<double>(), T, ldT, nm,
-                                c->lam.as<double>(), phi, c->stream));
+                                c->lam.as<double>(), phi, wb ? c->spwork.as<double>() : nullptr, c->stream));
   PODS_HIP(hipStreamSynchronize(c->stream));
   return PODS_OK;
   PODS_CATCH

@@ -34,9 +34,10 @@ hipError_t launch_syrk(int kernel, const double* AT, int64_t ld, int ns, int64_t
 hipError_t launch_divide(double* x, int64_t n, double d, hipStream_t st);
 hipError_t launch_temporal(const double* V, int64_t v_rs, int64_t v_cs, int ns, int ncols,
                            int nvalid, const double* lam, double* mag, double* T, hipStream_t st);
+size_t spatial_work_bytes(int64_t rowlen, int ns);
 hipError_t launch_spatial(const double* AT, int64_t rowlen, int ns, const double* mean,
                           const double* T, int ldT, int nm, const double* inv_lam, double* phi,
-                          hipStream_t st);
+                          double* work, hipStream_t st);
 hipError_t launch_dft(const double* T, int ldT, int nm, int ns, const double* t, double inv_period,
                       double inv_n, const int* prog, int nprog, float2* c, hipStream_t st);
 

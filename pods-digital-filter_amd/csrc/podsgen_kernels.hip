@@ -800,17 +800,42 @@ __global__ void k_divide(double* __restrict__ x, int64_t n, double d) {
 // -----------------------------------------------------------------------------------------
 // temporal modes: descending reorder + PODFS.py:1323-1325 scaling
 // -----------------------------------------------------------------------------------------
-__global__ void k_temporal_mag(const double* __restrict__ V, int64_t v_rs, int64_t v_cs, int ns,
-                               int ncols, double* __restrict__ mag) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+// Python's builtin sum(T[:, j]**2) is one sequential chain (PODFS.py:1324): the squares are
+// formed in parallel into LDS (coalescing the strided column), then lane 0 runs the chain with
+// its LDS reads issued eight ahead.  One workgroup per column.
+constexpr int TMAG_MAX = 8192;
+__global__ __launch_bounds__(256) void k_temporal_mag(const double* __restrict__ V, int64_t v_rs,
+                                                      int64_t v_cs, int ns, int ncols,
+                                                      double* __restrict__ mag) {
+  __shared__ __attribute__((aligned(16))) double sq[TMAG_MAX];
+  const int j = blockIdx.x;
   if (j >= ncols) return;
   const double* col = V + (int64_t)(ns - 1 - j) * v_cs;
-  double s = 0.0;
-  for (int i = 0; i < ns; ++i) {
-    const double x = col[(int64_t)i * v_rs];
-    s = s + x * x;
+  for (int i0 = 0; i0 < ns; i0 += TMAG_MAX) {
+    const int n = min(TMAG_MAX, ns - i0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += 256) {
+      const double x = col[(int64_t)(i0 + i) * v_rs];
+      sq[i] = x * x;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = i0 == 0 ? 0.0 : mag[j];
+      int i = 0;
+      for (; i + 8 <= n; i += 8) {
+        const double2 a = *reinterpret_cast<const double2*>(sq + i);
+        const double2 b = *reinterpret_cast<const double2*>(sq + i + 2);
+        const double2 c = *reinterpret_cast<const double2*>(sq + i + 4);
+        const double2 d = *reinterpret_cast<const double2*>(sq + i + 6);
+        s = s + a.x; s = s + a.y; s = s + b.x; s = s + b.y;
+        s = s + c.x; s = s + c.y; s = s + d.x; s = s + d.y;
+      }
+      for (; i < n; ++i) s = s + sq[i];
+      mag[j] = s;
+    }
   }
-  mag[j] = s / (double)ns;
+  __syncthreads();
+  if (threadIdx.x == 0) mag[j] = mag[j] / (double)ns;
 }
 
 __global__ void k_temporal_scale(const double* __restrict__ V, int64_t v_rs, int64_t v_cs, int ns,
@@ -826,42 +851,96 @@ __global__ void k_temporal_scale(const double* __restrict__ V, int64_t v_rs, int
 
 // -----------------------------------------------------------------------------------------
 // spatial modes Phi[r][m] = ((sum_i (A_T[i][r]-m_r) T[i][m]) * (1/lambda_m)) / ns
+// (PODFS.py:1330-1333).  Each thread owns two adjacent rows (one 16-B load per snapshot from
+// the K-tiled layout), the snapshot axis is split into KS chunks (blockIdx.y) so the launch
+// holds enough loads in flight to stream A at HBM rate, and the loads run one 8-snapshot
+// group ahead of the FMAs.  T is staged through LDS (broadcast reads).  KS > 1 writes
+// partial sums part[ks][r][m] that k_spatial_reduce folds in a fixed order.
 // -----------------------------------------------------------------------------------------
 template <int NMB>
 __global__ __launch_bounds__(256) void k_spatial_modes(const double* __restrict__ AT, int64_t rowlen,
                                                        int ns, const double* __restrict__ mean,
                                                        const double* __restrict__ T, int ldT, int col0,
                                                        int nm, const double* __restrict__ inv_lam,
-                                                       double* __restrict__ phi, int ldphi) {
-  constexpr int CH = 128;
+                                                       double* __restrict__ phi, int ldphi, int chunk,
+                                                       double* __restrict__ part) {
+  constexpr int CH = 64, U = 8;
   __shared__ __attribute__((aligned(16))) double Ts[CH][NMB];
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const bool valid = r < rowlen;
-  const double mr = valid ? mean[r] : 0.0;
-  double acc[NMB];
+  const int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
+  const int64_t rowpad = (rowlen + 15) & ~(int64_t)15;
+  const bool valid = r < rowpad;
+  const double m0 = r < rowlen ? mean[r] : 0.0;
+  const double m1 = r + 1 < rowlen ? mean[r + 1] : 0.0;
+  const int i0 = blockIdx.y * chunk;
+  const int i1 = min(ns, i0 + chunk);
+  double acc0[NMB], acc1[NMB];
 #pragma unroll
-  for (int m = 0; m < NMB; ++m) acc[m] = 0.0;
-  for (int i0 = 0; i0 < ns; i0 += CH) {
+  for (int m = 0; m < NMB; ++m) acc0[m] = acc1[m] = 0.0;
+  const double* base = AT + (valid ? at_off(r, 0, ns) : 0);
+  for (int c0 = i0; c0 < i1; c0 += CH) {
+    const int lim = min(CH, i1 - c0);
+    __syncthreads();
     for (int e = threadIdx.x; e < CH * NMB; e += 256) {
       const int ii = e / NMB, m = e % NMB;
-      Ts[ii][m] = (i0 + ii < ns && m < nm) ? T[(int64_t)(i0 + ii) * ldT + col0 + m] : 0.0;
+      Ts[ii][m] = (ii < lim && m < nm) ? T[(int64_t)(c0 + ii) * ldT + col0 + m] : 0.0;
     }
     __syncthreads();
-    if (valid) {
-      const int lim = min(CH, ns - i0);
-      for (int ii = 0; ii < lim; ++ii) {
-        const double a = AT[at_off(r, i0 + ii, ns)] - mr;
+    if (!valid) continue;
+    const double2* src = reinterpret_cast<const double2*>(base + (int64_t)c0 * 16);
+    double2 cur[U], nxt[U];
 #pragma unroll
-        for (int m = 0; m < NMB; ++m) acc[m] = __builtin_fma(a, Ts[ii][m], acc[m]);
+    for (int u = 0; u < U; ++u) cur[u] = u < lim ? src[u * 8] : make_double2(m0, m1);
+    for (int g = 0; g < lim; g += U) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        nxt[u] = (g + U + u < lim) ? src[(g + U + u) * 8] : make_double2(m0, m1);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const double a0 = cur[u].x - m0, a1 = cur[u].y - m1;  // zero past lim: Ts rows are 0 too
+        const double* tr = Ts[(g + u) & (CH - 1)];
+#pragma unroll
+        for (int m = 0; m < NMB; m += 2) {
+          const double2 tv = *reinterpret_cast<const double2*>(tr + m);
+          acc0[m] = __builtin_fma(a0, tv.x, acc0[m]);
+          acc1[m] = __builtin_fma(a1, tv.x, acc1[m]);
+          acc0[m + 1] = __builtin_fma(a0, tv.y, acc0[m + 1]);
+          acc1[m + 1] = __builtin_fma(a1, tv.y, acc1[m + 1]);
+        }
       }
+#pragma unroll
+      for (int u = 0; u < U; ++u) cur[u] = nxt[u];
     }
-    __syncthreads();
   }
   if (!valid) return;
+  if (part) {
+    double* pp = part + ((int64_t)blockIdx.y * rowpad + r) * NMB;
+#pragma unroll
+    for (int m = 0; m < NMB; m += 2) {
+      *reinterpret_cast<double2*>(pp + m) = make_double2(acc0[m], acc0[m + 1]);
+      *reinterpret_cast<double2*>(pp + NMB + m) = make_double2(acc1[m], acc1[m + 1]);
+    }
+    return;
+  }
   const double dn = (double)ns;
 #pragma unroll
-  for (int m = 0; m < NMB; ++m)
-    if (m < nm) phi[r * ldphi + col0 + m] = (acc[m] * inv_lam[col0 + m]) / dn;
+  for (int m = 0; m < NMB; ++m) {
+    if (m < nm && r < rowlen) phi[r * ldphi + col0 + m] = (acc0[m] * inv_lam[col0 + m]) / dn;
+    if (m < nm && r + 1 < rowlen) phi[(r + 1) * ldphi + col0 + m] = (acc1[m] * inv_lam[col0 + m]) / dn;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_spatial_reduce(const double* __restrict__ part, int ks, int nmb,
+                                                        int64_t rowlen, int col0, int nm,
+                                                        const double* __restrict__ inv_lam, int ns,
+                                                        double* __restrict__ phi, int ldphi) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t r = e / nm;
+  const int m = (int)(e - r * nm);
+  if (r >= rowlen) return;
+  const int64_t rowpad = (rowlen + 15) & ~(int64_t)15;
+  double s = 0.0;
+  for (int k = 0; k < ks; ++k) s += part[((int64_t)k * rowpad + r) * nmb + m];
+  phi[r * ldphi + col0 + m] = (s * inv_lam[col0 + m]) / (double)ns;
 }
 
 // -----------------------------------------------------------------------------------------
@@ -1161,8 +1240,7 @@ hipError_t launch_divide(double* x, int64_t n, double d, hipStream_t st) {
 
 hipError_t launch_temporal(const double* V, int64_t v_rs, int64_t v_cs, int ns, int ncols,
                            int nvalid, const double* lam, double* mag, double* T, hipStream_t st) {
-  hipLaunchKernelGGL(k_temporal_mag, dim3((ncols + 63) / 64), dim3(64), 0, st, V, v_rs, v_cs, ns,
-                     ncols, mag);
+  hipLaunchKernelGGL(k_temporal_mag, dim3(ncols), dim3(256), 0, st, V, v_rs, v_cs, ns, ncols, mag);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_temporal_scale, dim3((ncols + 255) / 256, ns), dim3(256), 0, st, V, v_rs, v_cs,
@@ -1170,26 +1248,50 @@ hipError_t launch_temporal(const double* V, int64_t v_rs, int64_t v_cs, int ns, 
   return hipGetLastError();
 }
 
+int spatial_split(int64_t rowlen, int ns) {
+  const int64_t blocks = ((rowlen + 15) / 16 * 16 / 2 + 255) / 256;
+  int ks = 1;
+  while (blocks * ks < 1536 && ks < 16 && ns / (ks * 2) >= 64) ks *= 2;
+  return ks;
+}
+
+size_t spatial_work_bytes(int64_t rowlen, int ns) {
+  const int ks = spatial_split(rowlen, ns);
+  return ks > 1 ? (size_t)ks * ((rowlen + 15) / 16 * 16) * 32 * sizeof(double) : 0;
+}
+
 hipError_t launch_spatial(const double* AT, int64_t rowlen, int ns, const double* mean,
                           const double* T, int ldT, int nm, const double* inv_lam, double* phi,
-                          hipStream_t st) {
-  const dim3 grid((unsigned)((rowlen + 255) / 256));
+                          double* work, hipStream_t st) {
+  const int64_t rowpad = (rowlen + 15) / 16 * 16;
+  const int ks = work ? spatial_split(rowlen, ns) : 1;
+  const int chunk = ((ns + ks - 1) / ks + 7) / 8 * 8;
+  const dim3 grid((unsigned)((rowpad / 2 + 255) / 256), (unsigned)ks);
+  double* part = ks > 1 ? work : nullptr;
   for (int col0 = 0; col0 < nm; col0 += 32) {
     const int nb = nm - col0 < 32 ? nm - col0 : 32;
-    if (nb <= 8)
+    const int nmb = nb <= 8 ? 8 : nb <= 16 ? 16 : nb <= 20 ? 20 : 32;
+    if (nmb == 8)
       hipLaunchKernelGGL(k_spatial_modes<8>, grid, dim3(256), 0, st, AT, rowlen, ns, mean, T, ldT, col0,
-                         nb, inv_lam, phi, nm);
-    else if (nb <= 16)
+                         nb, inv_lam, phi, nm, chunk, part);
+    else if (nmb == 16)
       hipLaunchKernelGGL(k_spatial_modes<16>, grid, dim3(256), 0, st, AT, rowlen, ns, mean, T, ldT, col0,
-                         nb, inv_lam, phi, nm);
-    else if (nb <= 20)
+                         nb, inv_lam, phi, nm, chunk, part);
+    else if (nmb == 20)
       hipLaunchKernelGGL(k_spatial_modes<20>, grid, dim3(256), 0, st, AT, rowlen, ns, mean, T, ldT, col0,
-                         nb, inv_lam, phi, nm);
+                         nb, inv_lam, phi, nm, chunk, part);
     else
       hipLaunchKernelGGL(k_spatial_modes<32>, grid, dim3(256), 0, st, AT, rowlen, ns, mean, T, ldT, col0,
-                         nb, inv_lam, phi, nm);
+                         nb, inv_lam, phi, nm, chunk, part);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (part) {
+      const int64_t tot = rowlen * nb;
+      hipLaunchKernelGGL(k_spatial_reduce, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, part, ks,
+                         nmb, rowlen, col0, nb, inv_lam, ns, phi, nm);
+      e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
   }
   return hipSuccess;
 }
