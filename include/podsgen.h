@@ -155,6 +155,16 @@ int pods_spatial_modes(pods_ctx* ctx, const double* T_dev, int ldT, const double
 int pods_fourier(pods_ctx* ctx, const double* T_dev, int ldT, int nm, int ns,
                  const double* t_host, double period, float* c_dev);
 
+/* Ranking and energy count of the Fourier coefficients (PODFS.py:1575-1593):
+ * per mode i, c_ind[i][:] = indices n ordered by (|c[n][i]| as float32, n) descending
+ * (sorted(zip(cmod, idx), reverse=True)), and c_count[i] = the number of leading
+ * coefficients whose float64 running sum of |c| first reaches float64(sum_f32 |c|) * et;
+ * 0 when that target is not positive, -1 when it is never reached (et > 1; the
+ * reference raises IndexError).  c_dev: pods_fourier's ns x nm complex64 output.
+ * c_ind_dev: nm x ns int32, c_count_dev: nm int64 (device).  ns <= 16384. */
+int pods_fourier_rank(pods_ctx* ctx, const float* c_dev, int nm, int ns, double et,
+                      int32_t* c_ind_dev, int64_t* c_count_dev);
+
 /* ---- unit-level entry points (reference operator API, one call each) ------------- */
 /* filter3DSciPy1D(x, y, ...) (:100-140) on one host block x of shape
  * (2nfx+1, 2nfy+J, 2nfz+K) C-order -> y (J, K). */

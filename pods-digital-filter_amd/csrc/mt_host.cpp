@@ -5,6 +5,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <utility>
 
 #include <immintrin.h>
@@ -265,12 +266,24 @@ const JumpTables& jump_tables(int64_t Bs, int G2, int G1_needed) {
     slot->Bs = Bs;
     slot->G2 = G2;
     slot->level2.assign((size_t)(G2 + 1) * N, 0);
-    Poly p = powmod_t((uint64_t)N * (uint64_t)(Bs - 1));
     const Poly step = powmod_t((uint64_t)N * (uint64_t)Bs);
-    for (int g2 = 1; g2 <= G2; ++g2) {
-      poly_to_words32(p, &slot->level2[(size_t)g2 * N]);
-      if (g2 < G2) p = mulmod(p, step);
+    // chunks of the sequence p_g = t^(624(g Bs - 1)) = p_{g-1} * step on host threads
+    const int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const int per = (G2 + nth - 1) / nth;
+    std::vector<std::thread> pool;
+    JumpTables* jt = slot.get();
+    for (int k = 0; k < nth; ++k) {
+      const int a = 1 + k * per, b = std::min(G2, k * per + per);
+      if (a > b) break;
+      pool.emplace_back([jt, a, b, Bs, &step] {
+        Poly p = powmod_t((uint64_t)N * (uint64_t)(a * Bs - 1));
+        for (int g2 = a; g2 <= b; ++g2) {
+          poly_to_words32(p, &jt->level2[(size_t)g2 * N]);
+          if (g2 < b) p = mulmod(p, step);
+        }
+      });
     }
+    for (auto& th : pool) th.join();
     slot->G1 = 1;
     slot->level1.assign(N, 0);
     slot->level1[0] = 1;  // identity polynomial (unused)

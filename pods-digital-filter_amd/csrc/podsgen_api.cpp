@@ -133,6 +133,9 @@ struct RngLayout {
   std::vector<int> j1_src, j1_poly, j1_dst, j2_src, j2_poly, j2_dst;
 };
 
+// One jump level: substream g >= 1 starts from mt^(1) jumped by t^(624(g*Bs - 1)) mod phi
+// (seed-independent polynomials, cached per layout), so every substream state is one
+// independent job of a single k_mt_jump launch.
 RngLayout make_layout(int64_t ntot) {
   RngLayout L;
   L.ntot = ntot;
@@ -142,15 +145,11 @@ RngLayout make_layout(int64_t ntot) {
   while (Bs < want) Bs *= 2;
   L.Bs = Bs;
   L.G = (int)std::max<int64_t>(1, (blocks + Bs - 1) / Bs);
-  L.G1 = L.G >= 2 ? (L.G - 1 + L.G2 - 1) / L.G2 : 1;
-  for (int g1 = 1; g1 < L.G1; ++g1) {
-    L.j1_src.push_back(0);
-    L.j1_poly.push_back(g1);
-    L.j1_dst.push_back(g1);
-  }
+  L.G1 = 1;
+  L.G2 = std::max(1, L.G - 1);
   for (int g = 1; g < L.G; ++g) {
-    L.j2_src.push_back((g - 1) / L.G2);
-    L.j2_poly.push_back((g - 1) % L.G2 + 1);
+    L.j2_src.push_back(0);
+    L.j2_poly.push_back(g);
     L.j2_dst.push_back(g);
   }
   return L;
@@ -159,12 +158,13 @@ RngLayout make_layout(int64_t ntot) {
 struct RngBuffers {
   DevBuf states, bases, poly1, poly2, j1, j2;
   int64_t Bs_loaded = 0;
-  int G1_loaded = 0;
+  int G1_loaded = 0, G2_loaded = 0;
   std::vector<uint32_t> seed_host;  // 2 x 624 staging (mt^(0), mt^(1))
   void free_all() {
     release(states); release(bases); release(poly1); release(poly2); release(j1); release(j2);
     Bs_loaded = 0;
     G1_loaded = 0;
+    G2_loaded = 0;
   }
 };
 
@@ -217,7 +217,7 @@ struct pods_ctx {
   int64_t S = 0, Sl = 0, Pl = 0, rowlen = 0, rowpad = 0;  // rowpad: rowlen rounded up to 16
   RngLayout layout;
   RngBuffers rng;
-  DevBuf R, T1, A, mean, lund, taps, rot, prog_mean, prog_dft, tbuf, mag, lam, cwork, items, spwork;
+  DevBuf R, T1, A, mean, lund, taps, rot, prog_mean, prog_dft, tbuf, mag, lam, cwork, items, spwork, prog_rank;
   DevBuf e_wm, e_x, e_flags, e_det, e_v, e_t, e_part, e_w2, e_inv;  // pods_syev workspace
   int e_G = 0;
   int nitems = 0;
@@ -236,7 +236,7 @@ int upload_rng(pods_ctx* c, const RngLayout& L, uint32_t seed, RngBuffers& rb) {
   const JumpTables& jt = jump_tables(L.Bs, L.G2, std::max(L.G1, 1));
   PODS_HIP(ensure(rb.states, (size_t)L.G * N * 4));
   PODS_HIP(ensure(rb.bases, (size_t)std::max(L.G1, 1) * N * 4));
-  if (rb.Bs_loaded != L.Bs || rb.G1_loaded < L.G1) {
+  if (rb.Bs_loaded != L.Bs || rb.G1_loaded < L.G1 || rb.G2_loaded != L.G2) {
     PODS_HIP(ensure(rb.poly1, (size_t)std::max(L.G1, 1) * N * 4));
     PODS_HIP(ensure(rb.poly2, (size_t)(L.G2 + 1) * N * 4));
     PODS_HIP(hipMemcpy(rb.poly1.p, jt.level1.data(), (size_t)std::max(L.G1, 1) * N * 4,
@@ -245,6 +245,7 @@ int upload_rng(pods_ctx* c, const RngLayout& L, uint32_t seed, RngBuffers& rb) {
                        hipMemcpyHostToDevice));
     rb.Bs_loaded = L.Bs;
     rb.G1_loaded = L.G1;
+    rb.G2_loaded = L.G2;
   }
   const size_t n1 = L.j1_src.size(), n2 = L.j2_src.size();
   std::vector<int> jobs;
@@ -318,7 +319,7 @@ int pods_destroy(pods_ctx* c) {
   for (DevBuf* b : {&c->R, &c->T1, &c->A, &c->mean, &c->lund, &c->taps, &c->rot, &c->prog_mean,
                     &c->prog_dft, &c->tbuf, &c->mag, &c->lam, &c->cwork, &c->items, &c->e_wm,
                     &c->e_x, &c->e_flags, &c->e_det, &c->e_v, &c->e_t, &c->e_part, &c->e_w2,
-                    &c->e_inv, &c->spwork})
+                    &c->e_inv, &c->spwork, &c->prog_rank})
     release(*b);
   c->rng.free_all();
   delete c;
@@ -783,6 +784,25 @@ int pods_fourier(pods_ctx* c, const double* T, int ldT, int nm, int ns, const do
                             c->prog_dft.as<int>(), (int)prog.size() / 2,
                             reinterpret_cast<float2*>(c_dev), c->stream));
   PODS_HIP(hipStreamSynchronize(c->stream));  // host vectors above go out of scope
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_fourier_rank(pods_ctx* c, const float* c_dev, int nm, int ns, double et, int32_t* c_ind_dev,
+                      int64_t* c_count_dev) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!c_dev || !c_ind_dev || !c_count_dev || nm <= 0 || ns <= 0) return fail(PODS_ERR_ARG, "bad arguments");
+  if (ns > pods::rank_max_ns())
+    return fail(PODS_ERR_UNSUPPORTED, "pods_fourier_rank: ns > " + std::to_string(pods::rank_max_ns()));
+  PODS_HIP(hipSetDevice(c->device));
+  std::vector<int> prog = pairwise_program(ns);
+  PODS_HIP(ensure(c->prog_rank, prog.size() * sizeof(int)));
+  PODS_HIP(hipMemcpyAsync(c->prog_rank.p, prog.data(), prog.size() * sizeof(int), hipMemcpyHostToDevice,
+                          c->stream));
+  PODS_HIP(pods::launch_rank(c_dev, ns, nm, et, c->prog_rank.as<int>(), (int)prog.size() / 2, c_ind_dev,
+                             c_count_dev, c->stream));
+  PODS_HIP(hipStreamSynchronize(c->stream));  // the host program goes out of scope
   return PODS_OK;
   PODS_CATCH
 }

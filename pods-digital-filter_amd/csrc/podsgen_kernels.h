@@ -38,6 +38,9 @@ size_t spatial_work_bytes(int64_t rowlen, int ns);
 hipError_t launch_spatial(const double* AT, int64_t rowlen, int ns, const double* mean,
                           const double* T, int ldT, int nm, const double* inv_lam, double* phi,
                           double* work, hipStream_t st);
+int rank_max_ns();
+hipError_t launch_rank(const float* c, int ns, int nm, double et, const int* prog, int nprog,
+                       int32_t* c_ind, int64_t* c_count, hipStream_t st);
 hipError_t launch_dft(const double* T, int ldT, int nm, int ns, const double* t, double inv_period,
                       double inv_n, const int* prog, int nprog, float2* c, hipStream_t st);
 

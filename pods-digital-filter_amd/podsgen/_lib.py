@@ -57,6 +57,7 @@ SIGNATURES = {
     "pods_sytrd_trace": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "pods_spatial_modes": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "pods_fourier": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_dbl, c_void_p]),
+    "pods_fourier_rank": (c_int, [c_void_p, c_void_p, c_int, c_int, c_dbl, c_void_p, c_void_p]),
     "pods_filter_block": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                   c_void_p, c_void_p, c_void_p]),
     "pods_rng_uniform": (c_int, [c_void_p, c_u32, c_i64, c_dbl, c_dbl, c_void_p]),

@@ -3,7 +3,7 @@
     DFSetup (host, tiny) -> Generator.generate()          RNG + x/y/z filters + Lund + rotation
                          -> run_pod()                     mean, C = A'^T A'/ns (+ RCCL all-reduce),
                                                           eigensolve, temporal + spatial modes
-                         -> run_fourier()                 shifted DFT on the GPU, ranking/count on host
+                         -> run_fourier()                 shifted DFT + ranking/count on the GPU
 
 Multi-GPU: one process per GPU.  Each rank owns a contiguous slab of inlet rows
 (host.row_slab); its partial correlation is summed with ONE torch.distributed
@@ -283,8 +283,26 @@ def host_rank_and_count(c, et):
     return c_ind, c_count, FC
 
 
+def fc_rows(c, c_ind, c_count):
+    """FC rows [n - ns//2, Re c, Im c] (float64), mode-major in rank order (PODFS.py:1627-1639)."""
+    ns = c.shape[0]
+    idx = np.concatenate([c_ind[i, :int(c_count[i])] for i in range(len(c_count))]) if len(c_count) else \
+        np.zeros(0, np.int64)
+    modes = np.repeat(np.arange(len(c_count)), c_count.astype(np.int64))
+    FC = np.empty((len(idx), 3), dtype=np.float64)
+    FC[:, 0] = idx - ns // 2
+    vals = c[idx, modes]
+    FC[:, 1] = vals.real
+    FC[:, 2] = vals.imag
+    return FC
+
+
+RANK_MAX_NS = 16384  # pods_fourier_rank's LDS limit
+
+
 def run_fourier(ctx: Context, T, nm, ns, dt, et, timer=None):
-    """fourier_coefficients (PODFS.py:1523-1659): DFT on the GPU, ranking/count on host."""
+    """fourier_coefficients (PODFS.py:1523-1659): DFT and ranking/count on the GPU
+    (pods_fourier + pods_fourier_rank); FC assembled on the host from the ranked indices."""
     tm = timer or (lambda name: _NullCtx())
     time_, period = time_axis(ns, dt)
     dev = torch.device("cuda", ctx.device)
@@ -297,8 +315,20 @@ def run_fourier(ctx: Context, T, nm, ns, dt, et, timer=None):
         check(ctx.lib.pods_fourier(ctx.h, ptr(T), T.stride(0), nm, ns, ptr(np.ascontiguousarray(time_)),
                                    float(period), ptr(cbuf)), "pods_fourier")
     with tm("rank"):
-        c = cbuf.cpu().numpy().view(np.complex64).reshape(ns, nm)
-        c_ind, c_count, FC = host_rank_and_count(c, et)
+        if ns <= RANK_MAX_NS:
+            ind = torch.empty((nm, ns), dtype=torch.int32, device=dev)
+            cnt = torch.empty(nm, dtype=torch.int64, device=dev)
+            check(ctx.lib.pods_fourier_rank(ctx.h, ptr(cbuf), nm, ns, float(et), ptr(ind), ptr(cnt)),
+                  "pods_fourier_rank")
+            c = cbuf.cpu().numpy().view(np.complex64).reshape(ns, nm)
+            c_ind = ind.cpu().numpy()
+            c_count = cnt.cpu().numpy()
+            if np.any(c_count < 0):
+                raise IndexError("energy target not reachable (et = %r > 1?)" % et)
+            FC = fc_rows(c, c_ind, c_count)
+        else:
+            c = cbuf.cpu().numpy().view(np.complex64).reshape(ns, nm)
+            c_ind, c_count, FC = host_rank_and_count(c, et)
     return FourierResult(c=c, c_ind=c_ind, c_count=c_count, FC=FC, period=period, time=time_)
 
 

@@ -127,6 +127,41 @@ def test_fourier_vs_oracle_same_T(ctx, golden_dir, name):
     assert np.array_equal(c_ind, ref["c_ind"])
 
 
+def _rank_cases():
+    rng = np.random.default_rng(11)
+    for ns, nm in [(4096, 20), (17, 3), (64, 20), (1, 1), (5000, 4), (16384, 2), (8, 5)]:
+        c = (rng.standard_normal((ns, nm)) + 1j * rng.standard_normal((ns, nm)) *
+             rng.random((ns, nm)) ** 3).astype(np.complex64)
+        if ns > 8:
+            h = ns // 2
+            c[h + 1:] = np.conj(c[1:ns - h][::-1])       # exact conjugate pairs -> ties
+            c[3] = c[5]                                   # plain ties
+            c[7] = 0                                      # zeros
+            c[:4, 0] = (rng.standard_normal(4) * 1e-30).astype(np.complex64)
+        yield ns, nm, c
+
+
+@pytest.mark.parametrize("et", [0.9, 0.5, 1.0])
+def test_fourier_rank_matches_host(ctx, et):
+    """pods_fourier_rank == the host restatement of PODFS.py:1575-1593 (numpy f32 abs,
+    lexsort ties, pairwise f32 sum, float64 running count), exactly."""
+    for ns, nm, c in _rank_cases():
+        cdev = torch.from_numpy(np.ascontiguousarray(c).view(np.float32).reshape(ns, nm, 2)).cuda()
+        ind = torch.empty((nm, ns), dtype=torch.int32, device="cuda")
+        cnt = torch.empty(nm, dtype=torch.int64, device="cuda")
+        podsgen.check(ctx.lib.pods_fourier_rank(ctx.h, E.ptr(cdev), nm, ns, float(et), E.ptr(ind),
+                                                E.ptr(cnt)), "pods_fourier_rank")
+        ci, cc = ind.cpu().numpy(), cnt.cpu().numpy()
+        if np.any(cc < 0):  # et = 1: the f64 running sum can stay below f64(f32 sum)
+            with pytest.raises(IndexError):
+                E.host_rank_and_count(c, et)
+            continue
+        ref_ind, ref_cnt, ref_FC = E.host_rank_and_count(c, et)
+        assert np.array_equal(cc, ref_cnt), (ns, cc, ref_cnt)
+        assert np.array_equal(ci, ref_ind), ns
+        assert np.array_equal(E.fc_rows(c, ci, cc), ref_FC), ns
+
+
 def test_syrk_mfma_layout(ctx):
     """Asymmetric data through pods_set_snapshots: catches row/col swaps in the MFMA C map."""
     rng = np.random.default_rng(3)
