@@ -779,17 +779,43 @@ __global__ __launch_bounds__(512, 1) void k_syrk_glds(const double* __restrict__
 }
 
 // C[i][j] = (sum_s part_s[max][min]) [/ ns], splits summed in order.
-__global__ void k_syrk_reduce(const double* __restrict__ part, int nsplit, int64_t slab, int ns,
-                              int64_t ldc, double* __restrict__ C, int divide) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  const int i = blockIdx.y;
-  if (j >= ns) return;
-  const int a = i >= j ? i : j, b = i >= j ? j : i;
-  const int64_t off = (int64_t)a * ldc + b;
-  double v = part[off];
-  for (int s = 1; s < nsplit; ++s) v = v + part[(int64_t)s * slab + off];
-  if (divide) v = v / (double)ns;
-  C[(int64_t)i * ldc + j] = v;
+// Sum of the split-K slabs (split order: v = ((p0 + p1) + p2) + ...) over 64x64 tiles of the
+// lower triangle; each tile is written to C and, through LDS, transposed into the upper
+// triangle, so every global access is row-contiguous.
+__global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ part, int nsplit,
+                                                     int64_t slab, int ns, int64_t ldc,
+                                                     double* __restrict__ C, int divide) {
+  __shared__ double tile[64][65];
+  // linear lower-triangle tile index -> (ti >= tj)
+  const int L = blockIdx.x;
+  int ti = (int)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
+  while ((ti + 1) * (ti + 2) / 2 <= L) ++ti;
+  while (ti * (ti + 1) / 2 > L) --ti;
+  const int tj = L - ti * (ti + 1) / 2;
+  const int c = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+  const double dn = (double)ns;
+#pragma unroll 4
+  for (int r = r0; r < 64; r += 4) {
+    const int i = ti * 64 + r, j = tj * 64 + c;
+    const bool ok = i < ns && j < ns && (ti > tj || c <= r);
+    double v = 0.0;
+    if (ok) {
+      const int64_t off = (int64_t)i * ldc + j;
+      v = part[off];
+      for (int sp = 1; sp < nsplit; ++sp) v = v + part[(int64_t)sp * slab + off];
+      if (divide) v = v / dn;
+      C[off] = v;
+    }
+    tile[r][c] = v;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int r = r0; r < 64; r += 4) {
+    // upper element (tj*64 + r, ti*64 + c) = lower element (ti*64 + c, tj*64 + r)
+    const int i = tj * 64 + r, j = ti * 64 + c;
+    const bool ok = i < ns && j < ns && (ti > tj || r < c);
+    if (ok) C[(int64_t)i * ldc + j] = tile[c][r];
+  }
 }
 
 __global__ void k_divide(double* __restrict__ x, int64_t n, double d) {
@@ -1216,7 +1242,7 @@ hipError_t launch_syrk(int kernel, const double* AT, int64_t ld, int ns, int64_t
                        mean, reinterpret_cast<const int4*>(items), nitems, ksplit, work, ldc, slab);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_syrk_reduce, dim3((ns + 255) / 256, ns), dim3(256), 0, st, work, nsplit, slab,
+    hipLaunchKernelGGL(k_syrk_reduce, dim3(((ns + 63) / 64) * ((ns + 63) / 64 + 1) / 2), dim3(256), 0, st, work, nsplit, slab,
                        ns, ldc, C, divide);
     return hipGetLastError();
   } else {
@@ -1227,7 +1253,7 @@ hipError_t launch_syrk(int kernel, const double* AT, int64_t ld, int ns, int64_t
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || final_write) return e;
-  hipLaunchKernelGGL(k_syrk_reduce, dim3((ns + 255) / 256, ns), dim3(256), 0, st, work, nsplit, slab,
+  hipLaunchKernelGGL(k_syrk_reduce, dim3(((ns + 63) / 64) * ((ns + 63) / 64 + 1) / 2), dim3(256), 0, st, work, nsplit, slab,
                      ns, ldc, C, divide);
   return hipGetLastError();
 }
