@@ -133,6 +133,92 @@ def adapt1d_loops(yu, yv, yw, uin, uuin, vvin, wwin, uwin, jma, kma):
             yw[j, k] = A[2, 0] * xu + A[2, 1] * xv + A[2, 2] * xw
 
 
+PROFILES_2D = ("double-hyperbolic-tangent", "circular-hyperbolic-tangent", "ring-hyperbolic-tangent")
+
+
+def _clamped_factor(R00, R11, R22, R20):
+    """adapt2d's factor for one point (digitalfilters.py:278-299 / :365-385 / :457-477):
+    R10 = R21 = 0; A00 = sqrt(R00) unclamped (the clamped temp1 before it is never used)."""
+    A = np.ones((3, 3))
+    A[0, 0] = np.sqrt(R00)
+    A[0, 1] = 0.0
+    A[0, 2] = 0.0
+    A[1, 0] = 0.0 / (A[0, 0] + 1e-20)
+    t = R11 - A[1, 0] * A[1, 0]
+    if t < 0:
+        t = 0.0
+    A[1, 1] = np.sqrt(t)
+    A[1, 2] = 0.0
+    A[2, 0] = R20 / (A[0, 0] + 1e-20)
+    A[2, 1] = (0.0 - A[1, 0] * A[2, 0]) / (A[1, 1] + 1e-20)
+    t = R22 - A[2, 0] * A[2, 0] - A[2, 1] * A[2, 1]
+    if t < 0:
+        t = 0.0
+    A[2, 2] = np.sqrt(t)
+    return A
+
+
+def adapt2d_point_coeffs(mean_profile, inner_d, uin, uuin, vvin, wwin, uwin, jma, kma):
+    """adapt2d (digitalfilters.py:233-485) evaluated point by point with scalar splev, as the
+    reference does inside its step loop.  Returns ((a00,a10,a11,a20,a21,a22), Umean), (J, K)
+    arrays; the transform itself is apply_lund with these per-point factors (V/W None)."""
+    from scipy import interpolate
+    J, K = jma, kma
+    prof = [np.array(np.broadcast_to(np.asarray(v, dtype=np.float64), (K,))) for v in (uin, uuin, vvin, wwin, uwin)]
+    co = np.zeros((6, J, K))
+    um = np.zeros((J, K))
+    with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
+        if mean_profile == "double-hyperbolic-tangent":                  # :238-307
+            zA = np.linspace(-1., 1, K)
+            zi = np.linspace(-1., 1, J)
+            inj = [interpolate.splev(zi, interpolate.splrep(zA, v, s=0), der=0) for v in prof]
+            for v, src in zip(inj, prof):
+                v[0], v[-1] = src[0], src[-1]
+            for j in range(J):
+                for v in inj[1:4]:
+                    if v[j] < 0.:
+                        v[j] = 0.0
+                for k in range(K):
+                    R00 = np.sqrt(prof[1][k] * inj[1][j])
+                    R11 = np.sqrt(prof[2][k] * inj[2][j])
+                    R22 = np.sqrt(prof[3][k] * inj[3][j])
+                    R20 = np.sign(prof[4][k] + inj[4][j]) * np.sqrt(abs(prof[4][k] * inj[4][j]))
+                    A = _clamped_factor(R00, R11, R22, R20)
+                    co[:, j, k] = (A[0, 0], A[1, 0], A[1, 1], A[2, 0], A[2, 1], A[2, 2])
+                    um[j, k] = np.sqrt(prof[0][k] * inj[0][j])
+        elif mean_profile in ("circular-hyperbolic-tangent", "ring-hyperbolic-tangent"):
+            x = np.linspace(-1., 1., J)
+            y = np.linspace(-1., 1., K)
+            ring = mean_profile == "ring-hyperbolic-tangent"
+            if ring:                                                     # :395-485
+                zA = np.linspace(inner_d, 1., K)
+                tck = [interpolate.splrep(zA, v, s=0) for v in prof]
+                r_lo, lo = inner_d, [v[0] for v in prof]
+            else:                                                        # :309-393
+                ci = np.argmax(prof[0])
+                zA = np.linspace(0, 1, len(prof[0]) - ci)
+                tck = [interpolate.splrep(zA, v[ci:], s=0) for v in prof]
+                r_lo, lo = 0.0, [v[ci] for v in prof]
+            for j in range(J):
+                for k in range(K):
+                    r = np.sqrt(x[j] ** 2 + y[k] ** 2)
+                    val = [interpolate.splev(r, t, der=0) for t in tck]
+                    if r == r_lo:
+                        val = list(lo)
+                    if r == 1.0:
+                        val = [v[-1] for v in prof]
+                    if r > 1.0:
+                        val = [0.0] * 5
+                    if ring and r < inner_d:
+                        val = [0.0] * 5
+                    A = _clamped_factor(val[1], val[2], val[3], val[4])
+                    co[:, j, k] = (A[0, 0], A[1, 0], A[1, 1], A[2, 0], A[2, 1], A[2, 2])
+                    um[j, k] = val[0]
+        else:
+            raise ValueError("adapt2d: unknown mean_profile %r" % (mean_profile,))
+    return tuple(co), um
+
+
 def rotation_matrix(nx, ny, nz):
     """prof_rotation_matrix, digitalfilters.py:1064-1116 (R = Ra(azimuth) . Rp(polar))."""
     n = np.sqrt(nx ** 2 + ny ** 2 + nz ** 2)
@@ -345,6 +431,8 @@ class DFConfig:
     et: float = 0.9
     normal: tuple = (1.0, 0.0, 0.0)
     prf: Optional[dict] = None
+    mean_profile: str = "hyperbolic-tangent"   # -p (:1146); the 2-D ones go through adapt2d
+    inner_d: float = 0.5                       # --ring (:1275)
     # derived
     nfx: int = 0
     nfy: int = 0
@@ -365,7 +453,7 @@ class DFConfig:
         self.n_unit = (n1[0] / nrm, n1[1] / nrm, n1[2] / nrm)
         V = W = 0
         if self.prf is None:
-            U, uu, vv, ww, uw = build_profile("hyperbolic-tangent", "top-hat",
+            U, uu, vv, ww, uw = build_profile(self.mean_profile, "top-hat",
                                               self.bulk_velocity, self.u_dash, self.kma)
             self.profile = dict(U=U, uu=uu, vv=vv, ww=ww, uw=uw)
         else:
@@ -434,6 +522,13 @@ def lund_point_coeffs(cfg):
     rows a00,a10,a11,a20,a21,a22,U,V,W (V,W = 0 and unused for the 1-D form)."""
     J, K = cfg.jma, cfg.kma
     pr = cfg.profile
+    if cfg.prf is None and cfg.mean_profile in PROFILES_2D:
+        co, um = adapt2d_point_coeffs(cfg.mean_profile, cfg.inner_d, pr["U"], pr["uu"], pr["vv"], pr["ww"],
+                                      pr["uw"], J, K)
+        out = np.zeros((9, J, K))
+        out[:6] = np.stack(co)
+        out[6] = um
+        return out.reshape(9, J * K)
     if cfg.prf is None:
         co = lund1d_coeffs(pr["uu"], pr["vv"], pr["ww"], pr["uw"])
         rows = [np.broadcast_to(np.asarray(c, dtype=np.float64), (K,)) for c in co]
@@ -477,7 +572,12 @@ def generate(cfg, loops=False, steps=None, stream=None):
             ys = [filter_block_scipy(x, bx, by, bz) for x in xs]
         else:
             ys = [filter_block(x, bx, by, bz) for x in xs]
-        if cfg.prf is None:
+        if cfg.prf is None and cfg.mean_profile in PROFILES_2D:   # main() :1447-1449
+            if coeffs is None:
+                coeffs = adapt2d_point_coeffs(cfg.mean_profile, cfg.inner_d, pr["U"], pr["uu"], pr["vv"],
+                                              pr["ww"], pr["uw"], J, K)
+            u, v, w = apply_lund(ys[0], ys[1], ys[2], coeffs[0], coeffs[1])
+        elif cfg.prf is None:
             if loops:
                 adapt1d_loops(ys[0], ys[1], ys[2], pr["U"], pr["uu"], pr["vv"], pr["ww"], pr["uw"], J, K)
                 u, v, w = ys

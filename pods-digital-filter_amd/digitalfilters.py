@@ -162,8 +162,14 @@ def adapt2prf(yu, yv, yw, uin, vin, win, uuin, vvin, wwin, uvin, uwin, vwin, jma
 
 
 def adapt2d(yu, yv, yw, uin, uuin, vvin, wwin, uwin, jma, kma, mean_profile, inner_d):
-    raise NotImplementedError("adapt2d (double/circular/ring hyperbolic-tangent profiles, "
-                              "digitalfilters.py:233-485) is not on the GPU path yet (SURVEY.md 8(f) row 3)")
+    """:233-485 -- double/circular/ring hyperbolic-tangent profiles: the per-point factor and
+    mean velocity are evaluated on the host (podsgen.profiles2d), the transform on the GPU."""
+    from podsgen.profiles2d import adapt2d_factor
+    fac = adapt2d_factor(mean_profile, inner_d, uin, uuin, vvin, wwin, uwin, jma, kma)
+    rows = np.zeros((9, jma * kma))
+    for r in range(7):
+        rows[r] = np.asarray(fac[r], dtype=np.float64).reshape(jma * kma)
+    _apply(yu, yv, yw, np.ascontiguousarray(rows), 0, None)
 
 
 def rotate_velocity(A, nx, ny, nz):
@@ -233,7 +239,7 @@ def make_parser():
     a = parser.add_option
     a("-i", "--inputfile", dest="profilefile", default="none", help="1d turbulent profile file", metavar="FILE")
     a("-p", "--mean_profile", dest="mean_profile", default="hyperbolic-tangent",
-      help="hyperbolic-tangent (GPU path); double-/ring-/circular-hyperbolic-tangent are not on the GPU path yet",
+      help="hyperbolic-tangent, double-hyperbolic-tangent, circular-hyperbolic-tangent, ring-hyperbolic-tangent",
       metavar="STRING")
     a("--turb_profile", dest="turb_profile", default="top-hat", help="top-hat, none", metavar="STRING")
     a("--U0", "--bulk_velocity", type="float", dest="bulk_velocity", default=1.0, metavar="NUM")
@@ -278,7 +284,7 @@ def setup_from_options(options):
               fwidth=options.fwidth, dt=options.dt, res=options.res, bulk_velocity=options.bulk_velocity,
               u_dash=options.turbulence_intensity, nm=options.nm, et=options.et,
               normal=(options.nx, options.ny, options.nz), mean_profile=options.mean_profile,
-              turb_profile=options.turb_profile)
+              turb_profile=options.turb_profile, inner_d=options.ring)
     if profilefile != "none" and os.path.isfile(profilefile):
         U, uu, vv, ww, uw = read_profile(profilefile, options.kma)
         kw["profile1d"] = dict(U=U, uu=uu, vv=vv, ww=ww, uw=uw)

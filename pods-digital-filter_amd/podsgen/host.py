@@ -77,6 +77,29 @@ def lundprf_factor(uu, vv, ww, uv, uw, vw):
     return a00, a10, a11, a20, a21, a22
 
 
+PROFILES_2D = ("double-hyperbolic-tangent", "circular-hyperbolic-tangent", "ring-hyperbolic-tangent")
+
+
+def _adapt2d_lund(R00, R11, R22, R20):
+    """adapt2d's clamped factor (digitalfilters.py:278-299, same at :365-385 and :457-477).
+    R10 = R21 = 0 (never assigned; R starts zero); A00 = sqrt(R00) is NOT clamped (the
+    clamped temp1 above it is unused), so a negative R00 gives NaN exactly like the reference."""
+    zero = np.zeros_like(R00)
+    with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
+        a00 = np.sqrt(R00)
+        a10 = zero / (a00 + 1e-20)
+        t = R11 - a10 * a10
+        a11 = np.sqrt(np.where(t < 0, 0.0, t))
+        a20 = R20 / (a00 + 1e-20)
+        a21 = (zero - a10 * a20) / (a11 + 1e-20)
+        t = R22 - a20 * a20 - a21 * a21
+        a22 = np.sqrt(np.where(t < 0, 0.0, t))
+    return a00, a10, a11, a20, a21, a22
+
+
+PROFILES_2D = ("double-hyperbolic-tangent", "circular-hyperbolic-tangent", "ring-hyperbolic-tangent")
+
+
 def prof_rotation_matrix(nx, ny, nz):
     n = np.sqrt(nx ** 2 + ny ** 2 + nz ** 2)
     n_proj = np.sqrt(nx ** 2 + ny ** 2)
@@ -119,7 +142,8 @@ class DFSetup:
     normal: tuple = (1.0, 0.0, 0.0)
     mean_profile: str = "hyperbolic-tangent"
     turb_profile: str = "top-hat"
-    prf: Optional[dict] = None          # (jma,kma) arrays U,V,W,uu,vv,ww,uv,uw,vw -> adapt2prf
+    inner_d: float = 0.5                # --ring (:1275): inner radius of the ring profile
+    prf: Optional[dict] = None         # (jma,kma) arrays U,V,W,uu,vv,ww,uv,uw,vw -> adapt2prf
     profile1d: Optional[dict] = None    # (kma,) arrays U,uu,vv,ww,uw from read_profile -> adapt1d
     nfx: int = field(default=0, init=False)
     nfy: int = field(default=0, init=False)
@@ -132,9 +156,6 @@ class DFSetup:
     profile: dict = field(default_factory=dict, init=False)
 
     def __post_init__(self):
-        if self.mean_profile in ("double-hyperbolic-tangent", "circular-hyperbolic-tangent",
-                                 "ring-hyperbolic-tangent") and self.prf is None:
-            raise NotImplementedError("adapt2d profiles (%s) are not on the GPU path yet" % self.mean_profile)
         self.lnx = self.lny = self.lnz = float(self.lengthscale)
         nf = int(math.ceil(self.fwidth * self.lengthscale))
         self.nfx = self.nfy = self.nfz = nf
@@ -192,7 +213,14 @@ class DFSetup:
         J, K = self.jma, self.kma
         pr = self.profile
         out = np.zeros((9, J, K))
-        if self.prf is None:
+        if self.prf is None and self.mean_profile in PROFILES_2D:
+            # main() :1447-1449: adapt2d for the 2-D built (or 1-D file) profiles
+            from .profiles2d import adapt2d_factor
+            fac = adapt2d_factor(self.mean_profile, self.inner_d, pr["U"], pr["uu"], pr["vv"], pr["ww"],
+                                 pr["uw"], J, K)
+            for r in range(7):
+                out[r] = fac[r]
+        elif self.prf is None:
             fac = lund1d_factor(*(np.broadcast_to(np.asarray(pr[k], dtype=np.float64), (K,))
                                   for k in ("uu", "vv", "ww", "uw")))
             for r, v in enumerate(fac):

@@ -27,6 +27,7 @@ Functions executed from the reference (file:line):
   digitalfilters.py:100-140  filter3DSciPy1D
   digitalfilters.py:143-178  adapt1d
   digitalfilters.py:180-231  adapt2prf
+  digitalfilters.py:233-485  adapt2d (needs scipy.interpolate in the namespace)
   digitalfilters.py:1038-1062 build_profile
   digitalfilters.py:1064-1131 prof_rotation_matrix / rotate_velocity
   PODFS.py:1409-1427          write_eigenvalues
@@ -71,8 +72,9 @@ SEMANTIC_PATCHES = {
     "rotate_velocity": [("len(A)/3", "len(A)//3")],
 }
 
-DF_FUNCS = ["calccoeff", "filter3DSciPy1D", "adapt1d", "adapt2prf", "build_profile",
+DF_FUNCS = ["calccoeff", "filter3DSciPy1D", "adapt1d", "adapt2prf", "adapt2d", "build_profile",
             "prof_rotation_matrix", "rotate_velocity"]
+PROFILES_2D = ("double-hyperbolic-tangent", "circular-hyperbolic-tangent", "ring-hyperbolic-tangent")
 POD_FUNCS = ["write_eigenvalues", "sort_eigenvalues", "calculate_correlation_matrix",
              "fourier_coefficients"]
 
@@ -103,7 +105,9 @@ def _extract(src, names):
 
 
 def load_reference():
-    ns = {"np": np, "scSig": scSig, "math": math, "Pi": np.pi, "linalg": np.linalg}
+    from scipy import interpolate
+    ns = {"np": np, "scSig": scSig, "math": math, "Pi": np.pi, "linalg": np.linalg,
+          "interpolate": interpolate}
     for path, names in ((os.path.join(REF, "digitalfilters.py"), DF_FUNCS),
                         (os.path.join(REF, "PODFS.py"), POD_FUNCS)):
         funcs = _extract(_translate(path), names)
@@ -121,10 +125,12 @@ class Obj(object):
 
 def run_reference_pipeline(ref, *, jma, kma, ns, seed, lengthscale=3.0, fwidth=2.0, dt=0.0,
                            res=0.1, bulk_velocity=1.0, u_dash=0.02, nm=20, et=0.9,
-                           normal=(1.0, 0.0, 0.0), prf=None, workdir=None):
+                           normal=(1.0, 0.0, 0.0), prf=None, workdir=None,
+                           mean_profile="hyperbolic-tangent", inner_d=0.5):
     """Replay digitalfilters.py main() (:1244-1510) + PODFS.POD (:1294-1393) with the
-    reference's own functions.  prf=None -> built profile (adapt1d + rotation);
-    prf=dict(U,V,W,uu,vv,ww,uv,uw,vw) of (jma,kma) arrays -> adapt2prf path (no rotation)."""
+    reference's own functions.  prf=None -> built profile (adapt1d, or adapt2d for the 2-D
+    mean profiles, + rotation); prf=dict(U,V,W,uu,vv,ww,uv,uw,vw) of (jma,kma) arrays ->
+    adapt2prf path (no rotation)."""
     out = {}
     np.random.seed(seed)                                  # extension: reference never seeds
     lnx = lny = lnz = lengthscale                         # :1262-1264
@@ -136,7 +142,7 @@ def run_reference_pipeline(ref, *, jma, kma, ns, seed, lengthscale=3.0, fwidth=2
     nz = n1[2] / np.sqrt(n1[0]**2 + n1[1]**2 + n1[2]**2)
     V = W = 0
     if prf is None:
-        U, uu, vv, ww, uw = ref["build_profile"]("hyperbolic-tangent", "top-hat",
+        U, uu, vv, ww, uw = ref["build_profile"](mean_profile, "top-hat",
                                                  bulk_velocity, u_dash, kma)      # :1305
     else:
         U, V, W = prf["U"], prf["V"], prf["W"]
@@ -171,6 +177,8 @@ def run_reference_pipeline(ref, *, jma, kma, ns, seed, lengthscale=3.0, fwidth=2
             filt.append(np.stack([yu.copy(), yv.copy(), yw.copy()]))
         if prf is not None:                               # :1445-1451
             ref["adapt2prf"](yu, yv, yw, U, V, W, uu, vv, ww, uv, uw, vw, jma, kma)
+        elif mean_profile in PROFILES_2D:
+            ref["adapt2d"](yu, yv, yw, U, uu, vv, ww, uw, jma, kma, mean_profile, inner_d)
         else:
             ref["adapt1d"](yu, yv, yw, U, uu, vv, ww, uw, jma, kma)
         xu = np.roll(xu, -1, axis=0); xv = np.roll(xv, -1, axis=0); xw = np.roll(xw, -1, axis=0)
@@ -275,11 +283,46 @@ CASES = {
     "odd_12x9x17_aniso": dict(jma=12, kma=9, ns=17, seed=3, dt=0.05),        # odd ns, -t => nfx != nfy
     "prf_8x12x9": dict(jma=8, kma=12, ns=9, seed=11, prf="synthetic"),       # adapt2prf path
     "rot_6x7x6": dict(jma=6, kma=7, ns=6, seed=5, normal=(1.0, 1.0, 0.5)),   # non-identity rotation
+    # adapt2d paths (digitalfilters.py:233-485), built profile + rotation as main() does
+    "dtanh_9x12x7": dict(jma=9, kma=12, ns=7, seed=21, mean_profile="double-hyperbolic-tangent"),
+    "circ_11x10x6": dict(jma=11, kma=10, ns=6, seed=22, mean_profile="circular-hyperbolic-tangent",
+                         normal=(1.0, 0.5, -0.25)),
+    "ring_12x13x6": dict(jma=12, kma=13, ns=6, seed=23, mean_profile="ring-hyperbolic-tangent", inner_d=0.3),
 }
 
 
+def unit_adapt2d(ref):
+    """adapt2d on raw random fields for each 2-D profile, odd/even/non-square grids."""
+    rs = np.random.RandomState(77)
+    out = {}
+    for tag, (prof, J, K, inner) in {
+            "dtanh": ("double-hyperbolic-tangent", 17, 14, 0.5),
+            "circ": ("circular-hyperbolic-tangent", 15, 16, 0.5),
+            "circ_odd": ("circular-hyperbolic-tangent", 13, 13, 0.5),
+            "ring": ("ring-hyperbolic-tangent", 16, 15, 0.5),
+            "ring_thin": ("ring-hyperbolic-tangent", 14, 18, 0.8)}.items():
+        U, uu, vv, ww, uw = ref["build_profile"](prof, "top-hat", 1.3, 0.05, K)
+        uw = 0.3 * np.sqrt(uu * ww) * np.sin(np.linspace(0.0, 3.0, K))      # exercise R20 != 0
+        y = [rs.uniform(-2.0, 2.0, (J, K)) for _ in range(3)]
+        out[tag + "_in"] = np.stack(y)
+        out[tag + "_prof"] = np.stack([U, uu, vv, ww, uw])
+        out[tag + "_cfg"] = np.array([J, K, inner])
+        out[tag + "_name"] = np.array(prof)
+        ref["adapt2d"](y[0], y[1], y[2], U, uu, vv, ww, uw, J, K, prof, inner)
+        out[tag + "_out"] = np.stack(y)
+    return out
+
+
 def main():
+    only = set(sys.argv[1:])
     ref = load_reference()
+    if only:
+        if "unit_adapt2d" in only:
+            np.savez_compressed(os.path.join(HERE, "unit_adapt2d.npz"), **unit_adapt2d(ref))
+        for name, kw in CASES.items():
+            if name in only:
+                _write_case(ref, name, kw)
+        return
     # unit fixtures for the filter on a raw random block (anisotropic taps) -----------------------
     rs = np.random.RandomState(2024)
     x = rs.uniform(-np.sqrt(3), np.sqrt(3), (2*9+1, 2*6+7, 2*4+5))
@@ -295,20 +338,25 @@ def main():
         n = n / np.linalg.norm(n)
         Rs.append(ref["prof_rotation_matrix"](n[0], n[1], n[2]))
     np.savez_compressed(os.path.join(HERE, "unit_rotation.npz"), normals=normals, R=np.array(Rs))
+    np.savez_compressed(os.path.join(HERE, "unit_adapt2d.npz"), **unit_adapt2d(ref))
     for name, kw in CASES.items():
-        kw = dict(kw)
-        if kw.get("prf") == "synthetic":
-            kw["prf"] = synthetic_prf(kw["jma"], kw["kma"], kw["seed"])
-            extra = {"prf_" + k: v for k, v in kw["prf"].items()}
-        else:
-            extra = {}
-        res = run_reference_pipeline(ref, **kw)
-        meta = {k: np.array(v) for k, v in kw.items() if k != "prf"}
-        res.update({"cfg_" + k: v for k, v in meta.items()})
-        res.update(extra)
-        path = os.path.join(HERE, "%s.npz" % name)
-        np.savez_compressed(path, **res)
-        print("wrote", path, "nm=%d valid=%d" % (res["nm"], res["num_valid_modes"]))
+        _write_case(ref, name, kw)
+
+
+def _write_case(ref, name, kw):
+    kw = dict(kw)
+    if kw.get("prf") == "synthetic":
+        kw["prf"] = synthetic_prf(kw["jma"], kw["kma"], kw["seed"])
+        extra = {"prf_" + k: v for k, v in kw["prf"].items()}
+    else:
+        extra = {}
+    res = run_reference_pipeline(ref, **kw)
+    meta = {k: np.array(v) for k, v in kw.items() if k != "prf"}
+    res.update({"cfg_" + k: v for k, v in meta.items()})
+    res.update(extra)
+    path = os.path.join(HERE, "%s.npz" % name)
+    np.savez_compressed(path, **res)
+    print("wrote", path, "nm=%d valid=%d" % (res["nm"], res["num_valid_modes"]))
 
 
 if __name__ == "__main__":

@@ -21,7 +21,8 @@ from oracle import pods_oracle as O  # noqa: E402
 import podsgen  # noqa: E402
 from podsgen import engine as E  # noqa: E402
 
-CASES = ["c1_32x32x64", "cli_10x11x5", "odd_12x9x17_aniso", "prf_8x12x9", "rot_6x7x6"]
+CASES = ["c1_32x32x64", "cli_10x11x5", "odd_12x9x17_aniso", "prf_8x12x9", "rot_6x7x6",
+         "dtanh_9x12x7", "circ_11x10x6", "ring_12x13x6"]
 
 
 def load(golden_dir, name):
@@ -36,7 +37,33 @@ def setup_from(g):
         kw["normal"] = tuple(g["cfg_normal"])
     if "prf_U" in g.files:
         kw["prf"] = {k[4:]: np.array(g[k]) for k in g.files if k.startswith("prf_")}
+    if "cfg_mean_profile" in g.files:
+        kw["mean_profile"] = str(g["cfg_mean_profile"])
+    if "cfg_inner_d" in g.files:
+        kw["inner_d"] = float(g["cfg_inner_d"])
     return podsgen.DFSetup(**kw)
+
+
+@pytest.mark.parametrize("profile", ["double-hyperbolic-tangent", "circular-hyperbolic-tangent",
+                                     "ring-hyperbolic-tangent"])
+def test_generate_adapt2d_large_vs_oracle(ctx, profile):
+    """adapt2d at a non-square 96 x 70 inlet (j-varying Lund table through the fused y/z
+    kernel, rotated normal): bit-exact against the oracle's per-point loop."""
+    kw = dict(jma=96, kma=70, ns=5, seed=61, mean_profile=profile, normal=(1.0, -0.4, 0.2), inner_d=0.35)
+    gen = E.Generator(podsgen.DFSetup(**kw), ctx=ctx)
+    A = gen.generate().to_host()
+    assert np.array_equal(A, O.generate(O.DFConfig(**kw)))
+
+
+def test_adapt2d_operator_golden(golden_dir):
+    """digitalfilters.adapt2d (drop-in operator, GPU transform) on the reference's fixture."""
+    import digitalfilters as df
+    g = np.load(os.path.join(golden_dir, "unit_adapt2d.npz"))
+    for tag in ["dtanh", "circ", "circ_odd", "ring", "ring_thin"]:
+        J, K, inner = g[tag + "_cfg"]
+        y = [np.array(v) for v in g[tag + "_in"]]
+        df.adapt2d(y[0], y[1], y[2], *g[tag + "_prof"], int(J), int(K), str(g[tag + "_name"]), float(inner))
+        assert np.array_equal(np.stack(y), g[tag + "_out"], equal_nan=True), tag
 
 
 @pytest.fixture(scope="module")

@@ -36,7 +36,13 @@ def test_host_mt_jump_math(seed, nblocks):
 
 @pytest.mark.parametrize("kw", [dict(jma=12, kma=9, ns=17, seed=3, dt=0.05),
                                 dict(jma=10, kma=11, ns=5, seed=7),
-                                dict(jma=6, kma=7, ns=6, seed=5, normal=(1.0, 1.0, 0.5))])
+                                dict(jma=6, kma=7, ns=6, seed=5, normal=(1.0, 1.0, 0.5)),
+                                dict(jma=9, kma=12, ns=7, seed=21, mean_profile="double-hyperbolic-tangent"),
+                                dict(jma=11, kma=10, ns=6, seed=22, mean_profile="circular-hyperbolic-tangent"),
+                                dict(jma=12, kma=13, ns=6, seed=23, mean_profile="ring-hyperbolic-tangent",
+                                     inner_d=0.3),
+                                dict(jma=31, kma=40, ns=6, seed=2, mean_profile="circular-hyperbolic-tangent"),
+                                dict(jma=64, kma=33, ns=6, seed=2, mean_profile="ring-hyperbolic-tangent")])
 def test_setup_matches_oracle(kw):
     import podsgen
     s = podsgen.DFSetup(**kw)
@@ -47,6 +53,19 @@ def test_setup_matches_oracle(kw):
         assert np.array_equal(a, b)
     assert np.array_equal(s.lund_rows(), O.lund_point_coeffs(c))
     assert np.array_equal(s.rotation(), O.rotation_matrix(*c.n_unit))
+
+
+@pytest.mark.parametrize("tag", ["dtanh", "circ", "circ_odd", "ring", "ring_thin"])
+def test_adapt2d_host_factor_matches_oracle_loop(golden_dir, tag):
+    """podsgen.profiles2d (vectorised, once per run) == the reference's per-point loop."""
+    from podsgen.profiles2d import adapt2d_factor
+    g = np.load(os.path.join(golden_dir, "unit_adapt2d.npz"))
+    J, K, inner = g[tag + "_cfg"]
+    name, prof = str(g[tag + "_name"]), g[tag + "_prof"]
+    fac = adapt2d_factor(name, float(inner), *prof, int(J), int(K))
+    co, um = O.adapt2d_point_coeffs(name, float(inner), *prof, int(J), int(K))
+    for a, b in zip(fac, tuple(co) + (um,)):
+        assert np.array_equal(a, b, equal_nan=True)
 
 
 def test_lund_rows_slab():

@@ -7,7 +7,9 @@ import pytest
 
 from oracle import pods_oracle as O
 
-CASES = ["c1_32x32x64", "cli_10x11x5", "odd_12x9x17_aniso", "prf_8x12x9", "rot_6x7x6"]
+CASES = ["c1_32x32x64", "cli_10x11x5", "odd_12x9x17_aniso", "prf_8x12x9", "rot_6x7x6",
+         "dtanh_9x12x7", "circ_11x10x6", "ring_12x13x6"]
+UNIT_2D = ["dtanh", "circ", "circ_odd", "ring", "ring_thin"]
 
 
 def load(golden_dir, name):
@@ -22,7 +24,27 @@ def cfg_from(g):
         kw["normal"] = tuple(g["cfg_normal"])
     if "prf_U" in g.files:
         kw["prf"] = {k[4:]: np.array(g[k]) for k in g.files if k.startswith("prf_")}
+    if "cfg_mean_profile" in g.files:
+        kw["mean_profile"] = str(g["cfg_mean_profile"])
+    if "cfg_inner_d" in g.files:
+        kw["inner_d"] = float(g["cfg_inner_d"])
     return O.DFConfig(**kw)
+
+
+def unit_2d(golden_dir, tag):
+    g = np.load(os.path.join(golden_dir, "unit_adapt2d.npz"))
+    J, K, inner = g[tag + "_cfg"]
+    return (str(g[tag + "_name"]), int(J), int(K), float(inner), g[tag + "_prof"], g[tag + "_in"],
+            g[tag + "_out"])
+
+
+@pytest.mark.parametrize("tag", UNIT_2D)
+def test_unit_adapt2d(golden_dir, tag):
+    """adapt2d (digitalfilters.py:233-485) on raw fields: oracle point loop == reference."""
+    name, J, K, inner, prof, yin, yout = unit_2d(golden_dir, tag)
+    co, um = O.adapt2d_point_coeffs(name, inner, *prof, J, K)
+    u, v, w = O.apply_lund(yin[0], yin[1], yin[2], co, um)
+    assert np.array_equal(np.stack([u, v, w]), yout, equal_nan=True)
 
 
 @pytest.mark.parametrize("name", CASES)
