@@ -119,17 +119,22 @@ __global__ __launch_bounds__(256) void k_mt_jump(const uint32_t* __restrict__ sr
                                                  const int* __restrict__ poly_idx,
                                                  uint32_t* __restrict__ dst_base,
                                                  const int* __restrict__ dst_idx, int njobs) {
-  __shared__ uint32_t x[2 * MTN];
+  // x[0, 2N): the window source; x[2N, 3N): zeros, read by the padding slots of a 4-bit batch
+  constexpr int ZR = 2 * MTN;
+  __shared__ uint32_t x[3 * MTN];
   __shared__ uint32_t acc[MTN];
+  __shared__ uint32_t g[MTN];  // the jump polynomial's coefficient bits (read wave-uniformly)
   const int job = blockIdx.x;
   if (job >= njobs) return;
   const uint32_t* s = src_base + (size_t)src_idx[job] * MTN;
-  const uint32_t* g = polys + (size_t)poly_idx[job] * MTN;
+  const uint32_t* gsrc = polys + (size_t)poly_idx[job] * MTN;
   for (int i = threadIdx.x; i < MTN; i += 256) {
     const uint32_t v = s[i];
     x[i] = v;
     x[MTN + i] = v;
+    x[ZR + i] = 0u;
     acc[i] = 0u;
+    g[i] = gsrc[i];
   }
   __syncthreads();
   twist_block256(x + MTN);
@@ -145,13 +150,18 @@ __global__ __launch_bounds__(256) void k_mt_jump(const uint32_t* __restrict__ sr
       if (sh && wi + 1 < MTN) bits |= g[wi + 1] << (32 - sh);
       if (rb + 32 > MTN) bits &= (1u << (MTN - rb)) - 1u;
       bits = __builtin_amdgcn_readfirstlane(bits);
+      // four set bits per iteration (missing ones read the zero block): 12 independent LDS
+      // loads in flight instead of a load-use chain per bit; XOR order does not matter
       while (bits) {
-        const int b = __builtin_ctz(bits);
-        bits &= bits - 1u;
-        const int r = rb + b;
-        v0 ^= x[r + w0];
-        v1 ^= x[r + w1];
-        if (has2) v2 ^= x[r + w2];
+        int r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          r[u] = bits ? rb + __builtin_ctz(bits) : ZR;
+          bits &= bits - 1u;
+        }
+        v0 ^= (x[r[0] + w0] ^ x[r[1] + w0]) ^ (x[r[2] + w0] ^ x[r[3] + w0]);
+        v1 ^= (x[r[0] + w1] ^ x[r[1] + w1]) ^ (x[r[2] + w1] ^ x[r[3] + w1]);
+        if (has2) v2 ^= (x[r[0] + w2] ^ x[r[1] + w2]) ^ (x[r[2] + w2] ^ x[r[3] + w2]);
       }
     }
     acc[w0] ^= v0;
@@ -219,6 +229,51 @@ __global__ __launch_bounds__(256) void k_mt_generate(const uint32_t* __restrict_
         ++q;
       }
     }
+  }
+}
+
+// Whole-plane generator (one GPU: the slab holds every row, so double D of the stream goes to
+// out[D]).  One 256-thread workgroup per substream; the state is double-buffered in LDS, so
+// the twist producing block b (cur -> nxt, three dependent phases) and the tempering + 16-B
+// stores of block b-1 (reading cur) run in the same phases: 4 barriers per 624-word block
+// and four waves per substream to hide the LDS and store latency.
+__global__ __launch_bounds__(256) void k_mt_generate_full(const uint32_t* __restrict__ states, int G,
+                                                          int64_t Bs, int64_t ntot, double low,
+                                                          double range, double* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t buf[2][MTN];
+  const int g = blockIdx.x, t = threadIdx.x;
+  if (g >= G) return;
+  for (int i = t; i < MTN; i += 256) buf[0][i] = states[(size_t)g * MTN + i];
+  __syncthreads();
+  const int64_t D0 = (int64_t)g * Bs * 312;
+  int64_t nb = (ntot - D0 + 311) / 312;
+  nb = nb < Bs ? nb : Bs;
+  // iteration b: nxt = twist(cur) = state of block b (if b < nb); temper cur = block b-1 (b >= 1)
+  for (int64_t b = 0; b <= nb; ++b) {
+    const uint32_t* cur = buf[b & 1];
+    uint32_t* nxt = buf[(b + 1) & 1];
+    const bool tw = b < nb;
+    if (tw && t < 227) nxt[t] = mt_mix(cur[t], cur[t + 1], cur[t + 397]);
+    if (b >= 1 && t < 156) {
+      const uint4 w = reinterpret_cast<const uint4*>(cur)[t];
+      const uint32_t a0 = mt_temper(w.x) >> 5, b0 = mt_temper(w.y) >> 6;
+      const uint32_t a1 = mt_temper(w.z) >> 5, b1 = mt_temper(w.w) >> 6;
+      const double u0 = ((double)a0 * 67108864.0 + (double)b0) / 9007199254740992.0;
+      const double u1 = ((double)a1 * 67108864.0 + (double)b1) / 9007199254740992.0;
+      const int64_t D = D0 + (b - 1) * 312 + 2 * t;
+      if (D + 1 < ntot)
+        *reinterpret_cast<double2*>(out + D) = make_double2(low + range * u0, low + range * u1);
+      else if (D < ntot)
+        out[D] = low + range * u0;
+    }
+    if (!tw) break;
+    __syncthreads();
+    if (t < 227) nxt[227 + t] = mt_mix(cur[227 + t], cur[228 + t], nxt[t]);
+    __syncthreads();
+    if (t < 169) nxt[454 + t] = mt_mix(cur[454 + t], cur[455 + t], nxt[227 + t]);
+    __syncthreads();
+    if (t == 0) nxt[623] = mt_mix(cur[623], nxt[0], nxt[396]);
+    __syncthreads();
   }
 }
 
@@ -794,19 +849,34 @@ __global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ 
   const int tj = L - ti * (ti + 1) / 2;
   const int c = threadIdx.x & 63, r0 = threadIdx.x >> 6;
   const double dn = (double)ns;
-#pragma unroll 4
-  for (int r = r0; r < 64; r += 4) {
+  // the thread's 16 rows advance through the slabs together: 16 independent loads per slab
+  // keep the memory pipe full (a per-element chain over the slabs would be latency bound)
+  double v[16];
+  int64_t off[16];
+  bool ok[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int r = r0 + 4 * q;
     const int i = ti * 64 + r, j = tj * 64 + c;
-    const bool ok = i < ns && j < ns && (ti > tj || c <= r);
-    double v = 0.0;
-    if (ok) {
-      const int64_t off = (int64_t)i * ldc + j;
-      v = part[off];
-      for (int sp = 1; sp < nsplit; ++sp) v = v + part[(int64_t)sp * slab + off];
-      if (divide) v = v / dn;
-      C[off] = v;
+    ok[q] = i < ns && j < ns && (ti > tj || c <= r);
+    off[q] = ok[q] ? (int64_t)i * ldc + j : 0;
+    v[q] = ok[q] ? part[off[q]] : 0.0;
+  }
+  for (int sp = 1; sp < nsplit; ++sp) {
+    const double* ps = part + (int64_t)sp * slab;
+    double t[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t[q] = ok[q] ? ps[off[q]] : 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = v[q] + t[q];
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    if (ok[q]) {
+      if (divide) v[q] = v[q] / dn;
+      C[off[q]] = v[q];
     }
-    tile[r][c] = v;
+    tile[r0 + 4 * q][c] = ok[q] ? v[q] : 0.0;
   }
   __syncthreads();
 #pragma unroll 4
@@ -1072,6 +1142,11 @@ hipError_t launch_mt_generate(const uint32_t* states, int G, int64_t Bs, int64_t
                               int Kp, int rlo, int rhi, int64_t Sl, double low, double range,
                               double* out, hipStream_t st) {
   if (G <= 0) return hipSuccess;
+  if (rlo == 0 && (int64_t)rhi * Kp == S && Sl == S && ((uintptr_t)out & 15) == 0 && Bs % 2 == 0) {
+    // whole planes: out[D] for stream double D (even block starts keep the 16-B stores aligned)
+    hipLaunchKernelGGL(k_mt_generate_full, dim3(G), dim3(256), 0, st, states, G, Bs, ntot, low, range, out);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_mt_generate, dim3((G + 3) / 4), dim3(256), 0, st, states, G, Bs, ntot, S, Kp,
                      rlo, rhi, Sl, low, range, out);
   return hipGetLastError();
