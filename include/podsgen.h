@@ -151,7 +151,9 @@ int pods_spatial_modes(pods_ctx* ctx, const double* T_dev, int ldT, const double
 
 /* Shifted direct DFT of the temporal modes (PODFS.py:1562-1571):
  * c[n][i] = sum_m T[m][i] exp(-1j 2 k pi t_m / period) / ns,  k = n - ns//2,
- * complex64 interleaved (re, im), row-major ns x nm.  t_host: ns sample times. */
+ * complex64 interleaved (re, im), row-major ns x nm.  t_host: ns sample times.
+ * Asynchronous: enqueued on the bound stream and returns (the summation program and t are
+ * kept on the device and re-uploaded only when ns or t change). */
 int pods_fourier(pods_ctx* ctx, const double* T_dev, int ldT, int nm, int ns,
                  const double* t_host, double period, float* c_dev);
 
@@ -161,7 +163,8 @@ int pods_fourier(pods_ctx* ctx, const double* T_dev, int ldT, int nm, int ns,
  * coefficients whose float64 running sum of |c| first reaches float64(sum_f32 |c|) * et;
  * 0 when that target is not positive, -1 when it is never reached (et > 1; the
  * reference raises IndexError).  c_dev: pods_fourier's ns x nm complex64 output.
- * c_ind_dev: nm x ns int32, c_count_dev: nm int64 (device).  ns <= 16384. */
+ * c_ind_dev: nm x ns int32, c_count_dev: nm int64 (device).  ns <= 16384.
+ * Asynchronous, like pods_fourier. */
 int pods_fourier_rank(pods_ctx* ctx, const float* c_dev, int nm, int ns, double et,
                       int32_t* c_ind_dev, int64_t* c_count_dev);
 

@@ -673,7 +673,7 @@ constexpr int NCH = 1;  // shifts per lane: 16 shifts per step split the bracket
 __global__ __launch_bounds__(256) void k_bisect(const double* __restrict__ D,
                                                 const double* __restrict__ E, int n,
                                                 const double* __restrict__ bounds,
-                                                double* __restrict__ lam_desc) {
+                                                double* __restrict__ lam_desc, int k0, int k1) {
   extern __shared__ double2 de[];
   const int t = threadIdx.x, lane = t & 63;
   for (int i = t; i < n; i += 256) {
@@ -683,8 +683,8 @@ __global__ __launch_bounds__(256) void k_bisect(const double* __restrict__ D,
   __syncthreads();
   const double gl = bounds[0], gu = bounds[1], pivmin = bounds[2], atol = bounds[3];
   const int l = t % BL;
-  const int k = blockIdx.x * (256 / BL) + t / BL;
-  const bool active = k < n;
+  const int k = k0 + blockIdx.x * (256 / BL) + t / BL;  // ascending index, [k0, k1) this launch
+  const bool active = k < k1;
   double lo = gl, hi = gu;
   for (int it = 0; it < 128; ++it) {
     const bool conv = !active || (hi - lo) <= fmax(atol, 2.0 * DBL_EPSILON * fmax(fabs(lo), fabs(hi)));
@@ -1280,17 +1280,31 @@ hipError_t launch_trd(const TrdArgs& a, int R, hipStream_t st) {
   return e;
 }
 
-hipError_t launch_tri_eigvals(const double* D, const double* E, int n, double* bounds,
-                              double* lam_desc, hipStream_t st) {
+hipError_t launch_tri_bounds(const double* D, const double* E, int n, double* bounds, hipStream_t st) {
   hipLaunchKernelGGL(eig::k_tri_bounds, dim3(1), dim3(256), 0, st, D, E, n, bounds);
+  return hipGetLastError();
+}
+
+// Eigenvalues with ascending indices [k0, k1) (written to lam_desc[n-1-k]); bounds from
+// launch_tri_bounds.
+hipError_t launch_tri_bisect(const double* D, const double* E, int n, const double* bounds,
+                             double* lam_desc, int k0, int k1, hipStream_t st) {
+  if (k1 <= k0) return hipSuccess;
   const size_t lds = (size_t)n * sizeof(double2);
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&eig::k_bisect),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   const int per = 256 / eig::BL;
-  hipLaunchKernelGGL(eig::k_bisect, dim3((n + per - 1) / per), dim3(256), lds, st, D, E, n,
-                     (const double*)bounds, lam_desc);
+  hipLaunchKernelGGL(eig::k_bisect, dim3((k1 - k0 + per - 1) / per), dim3(256), lds, st, D, E, n,
+                     bounds, lam_desc, k0, k1);
   return hipGetLastError();
+}
+
+hipError_t launch_tri_eigvals(const double* D, const double* E, int n, double* bounds,
+                              double* lam_desc, hipStream_t st) {
+  hipError_t e = launch_tri_bounds(D, E, n, bounds, st);
+  if (e != hipSuccess) return e;
+  return launch_tri_bisect(D, E, n, bounds, lam_desc, 0, n, st);
 }
 
 hipError_t launch_tri_eigvecs(const double* D, const double* E, int n, const double* lam_desc,

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "podsgen_kernels.h"
 
@@ -327,8 +328,8 @@ __global__ __launch_bounds__(256) void k_filter_x(const double* __restrict__ R,
 __device__ __forceinline__ int kpad(int k) { return k + (k >> 4); }
 
 // NZC: compile-time z width (0: runtime NZ <= 25, the generic instance)
-template <int TJ, int NY, int NZC>
-__global__ __launch_bounds__(512) void k_filter_yz(
+template <int TJ, int NY, int NZC, int NT>
+__global__ __launch_bounds__(NT) void k_filter_yz(
     const double* __restrict__ T1, const double* __restrict__ by, const double* __restrict__ bz,
     int NZr, int ns, int jl, int K, int Kp, int64_t Sl, int ncomp,
     const double* __restrict__ lund, int64_t lund_sj, int lund_mode, const double* __restrict__ rot,
@@ -344,7 +345,7 @@ __global__ __launch_bounds__(512) void k_filter_yz(
   const int rows = min(TJ, jl - jt);
   const int64_t Pl = (int64_t)jl * K;
   const int kch = (K + 15) >> 4;       // 16-wide output chunks per row
-  const int zitems = TJ * kch;         // <= 512 (host guarantees)
+  const int zitems = TJ * kch;         // <= NT (host guarantees)
   double byr[NY];
 #pragma unroll
   for (int b = 0; b < NY; ++b) byr[b] = by[NY - 1 - b];
@@ -359,7 +360,7 @@ __global__ __launch_bounds__(512) void k_filter_yz(
   if (lsh) {
     const int ne = lund_mode == 1 ? 9 : 7;
     for (int e = 0; e < ne; ++e)
-      for (int k = tid0; k < K; k += 512) lt[e * ldl + kpad(k)] = lund[(int64_t)e * Pl + k];
+      for (int k = tid0; k < K; k += NT) lt[e * ldl + kpad(k)] = lund[(int64_t)e * Pl + k];
   }
   // NSB consecutive steps per block: each thread's stores for one snapshot-row group then
   // land on consecutive 128-B lines of the K-tiled layout (steps are contiguous there)
@@ -386,10 +387,10 @@ __global__ __launch_bounds__(512) void k_filter_yz(
       const double* src = T1i + ((int64_t)c * ns + i) * Sl + (int64_t)jt * Kp;
       // main items: (column, YR-row group) for the first cmain columns, one per thread;
       // the remaining halo columns as single-output mini items spread over all threads
-      // (2*Kp items on 512 threads would leave a few threads a second full item)
+      // (2*Kp items on NT threads would leave a few threads a second full item)
       constexpr int GRP = TJ / YR;
-      const int cmain = min(Kp, 512 / GRP);
-      for (int it = tid; it < GRP * cmain; it += 512) {
+      const int cmain = min(Kp, NT / GRP);
+      for (int it = tid; it < GRP * cmain; it += NT) {
         const int grp = it / cmain, col = it - grp * cmain;
         const int r0 = grp * YR;
         if (r0 >= rows) continue;
@@ -415,7 +416,7 @@ __global__ __launch_bounds__(512) void k_filter_yz(
         for (int jj = 0; jj < YR; ++jj)
           if (r0 + jj < rows) t2[(r0 + jj) * ldt + kpad(col)] = acc[jj];
       }
-      for (int it = tid; it < (Kp - cmain) * TJ; it += 512) {
+      for (int it = tid; it < (Kp - cmain) * TJ; it += NT) {
         const int col = cmain + it / TJ, jj = it - (it / TJ) * TJ;
         if (jj >= rows) continue;
         double v[NY];
@@ -1178,15 +1179,23 @@ hipError_t launch_filter_x(int NX, const double* R, const double* bx, int ns, in
 }
 
 // Row-tile height for the y/z kernel: 32 rows when 32 x ceil(K/16) z items fit 512 threads.
+// y/z tile: TJ rows x NT threads.  16 rows on 256 threads where the 16-wide output chunks
+// fit (K <= 256): two workgroups per CU (LDS ~58 KB each), so one block's loads overlap the
+// other's filter arithmetic -- worth more than the 32-row tile's smaller halo (1.375 vs
+// 1.75 reads per output row), whose 97 KB of LDS allowed one block per CU.
+// PODS_YZ_TILE=32 selects the 32 x 512 tile.
 static int yz_tj(int K) {
   const int kch = (K + 15) / 16;
+  const char* env = std::getenv("PODS_YZ_TILE");
+  const bool force32 = env && env[0] == '3';
+  if (!force32 && 16 * kch <= 256) return 16256;
   if (32 * kch <= 512) return 32;
   if (16 * kch <= 512) return 16;
   if (8 * kch <= 512) return 8;
   return 0;
 }
 
-template <int TJ, int NY, int NZC>
+template <int TJ, int NY, int NZC, int NT>
 static hipError_t launch_fyz_t(const double* T1, const double* by, const double* bz, int NZ, int ns,
                                int jl, int K, int Kp, int64_t Sl, int ncomp, const double* lund,
                                int64_t lund_sj, int lund_mode, const double* rot, int rotate,
@@ -1194,28 +1203,28 @@ static hipError_t launch_fyz_t(const double* T1, const double* by, const double*
   const int ldt = (Kp + 16) + ((Kp + 16) >> 4) + 1;
   const int ldl = K + (K >> 4) + 1;
   const size_t lds = ((size_t)TJ * ldt + (lund_sj == 0 ? 9 * (size_t)ldl : 0)) * sizeof(double);
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_filter_yz<TJ, NY, NZC>),
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_filter_yz<TJ, NY, NZC, NT>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   // enough blocks to fill the chip twice over, at most 16 steps each
   const int tiles = (jl + TJ - 1) / TJ;
   const int nsb = (int)std::max<int64_t>(1, std::min<int64_t>(16, (int64_t)tiles * ns / 512));
   const dim3 grid((unsigned)tiles, (unsigned)((ns + nsb - 1) / nsb));
-  hipLaunchKernelGGL((k_filter_yz<TJ, NY, NZC>), grid, dim3(512), lds, st, T1, by, bz, NZ, ns, jl, K,
+  hipLaunchKernelGGL((k_filter_yz<TJ, NY, NZC, NT>), grid, dim3(NT), lds, st, T1, by, bz, NZ, ns, jl, K,
                      Kp, Sl, ncomp, lund, lund_sj, lund_mode, rot, rotate, AT, nsb);
   return hipGetLastError();
 }
 
-template <int TJ, int NY>
+template <int TJ, int NY, int NT>
 static hipError_t launch_fyz_tj(const double* T1, const double* by, const double* bz, int NZ, int ns,
                                 int jl, int K, int Kp, int64_t Sl, int ncomp, const double* lund,
                                 int64_t lund_sj, int lund_mode, const double* rot, int rotate,
                                 double* AT, hipStream_t st) {
   if (NZ == NY)  // isotropic y/z widths: the z taps are compile-time too
-    return launch_fyz_t<TJ, NY, NY>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj, lund_mode,
-                                    rot, rotate, AT, st);
-  return launch_fyz_t<TJ, NY, 0>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj, lund_mode,
-                                 rot, rotate, AT, st);
+    return launch_fyz_t<TJ, NY, NY, NT>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj, lund_mode,
+                                        rot, rotate, AT, st);
+  return launch_fyz_t<TJ, NY, 0, NT>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj, lund_mode,
+                                     rot, rotate, AT, st);
 }
 
 template <int NY>
@@ -1225,11 +1234,13 @@ static hipError_t launch_fyz(const double* T1, const double* by, const double* b
                              double* AT, hipStream_t st) {
   if (NZ > 25) return hipErrorInvalidValue;
   switch (yz_tj(K)) {
-    case 32: return launch_fyz_tj<32, NY>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj,
+    case 16256: return launch_fyz_tj<16, NY, 256>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj,
+                                                 lund_mode, rot, rotate, AT, st);
+    case 32: return launch_fyz_tj<32, NY, 512>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj,
                                           lund_mode, rot, rotate, AT, st);
-    case 16: return launch_fyz_tj<16, NY>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj,
+    case 16: return launch_fyz_tj<16, NY, 512>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj,
                                           lund_mode, rot, rotate, AT, st);
-    case 8: return launch_fyz_tj<8, NY>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj,
+    case 8: return launch_fyz_tj<8, NY, 512>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj,
                                         lund_mode, rot, rotate, AT, st);
     default: return hipErrorInvalidConfiguration;
   }

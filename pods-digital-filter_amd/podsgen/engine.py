@@ -56,6 +56,13 @@ class Context:
         check(self.lib.pods_create(ctypes.byref(h), self.device), "pods_create")
         self.h = h
         check(self.lib.pods_set_stream(self.h, ctypes.c_void_p(self.stream.cuda_stream)), "pods_set_stream")
+        self._side = None
+
+    def side_stream(self):
+        """A second stream on the device for work that may overlap the main stream's."""
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
 
     def close(self):
         if getattr(self, "h", None):
@@ -209,8 +216,12 @@ def eigen_modes(ctx: Context, C, ns, nm, tol_CN, full_temporal, tm=None):
 
 
 def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=False,
-            keep_C=False, timer=None):
-    """PODFS.POD (PODFS.py:1294-1393) with correct_for_cell_volumes='false'."""
+            keep_C=False, timer=None, on_temporal=None):
+    """PODFS.POD (PODFS.py:1294-1393) with correct_for_cell_volumes='false'.
+
+    on_temporal(T, nm_trunc), if given, is called on rank 0 as soon as the scaled temporal
+    modes exist, before the spatial modes are enqueued (pipeline() starts the Fourier
+    stage there on a side stream, so it runs beside the spatial-mode pass)."""
     ctx, lib = snap.ctx, snap.ctx.lib
     ns = snap.ns
     dist, rank, world = _dist_info(dist)
@@ -231,6 +242,8 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
     T = None
     if rank == 0:
         lam_desc, nvalid, nmt, T = eigen_modes(ctx, C, ns, nm, tol_CN, full_temporal, tm)
+        if on_temporal is not None:
+            on_temporal(T, nmt)
         lam_desc_t.copy_(torch.from_numpy(lam_desc).to(dev))
         meta[0], meta[1] = nvalid, nmt
     if world > 1:
@@ -303,33 +316,63 @@ RANK_MAX_NS = 16384  # pods_fourier_rank's LDS limit
 def run_fourier(ctx: Context, T, nm, ns, dt, et, timer=None):
     """fourier_coefficients (PODFS.py:1523-1659): DFT and ranking/count on the GPU
     (pods_fourier + pods_fourier_rank); FC assembled on the host from the ranked indices."""
+    return launch_fourier(ctx, T, nm, ns, dt, et, timer)()
+
+
+def launch_fourier(ctx: Context, T, nm, ns, dt, et, timer=None, side=False):
+    """Enqueue the DFT and the ranking kernels; returns finish() -> FourierResult.
+
+    side=True runs them on the context's side stream (forked from the current stream, so it
+    sees T), concurrently with what the caller enqueues next on the current stream (the
+    spatial modes: an HBM-bound pass beside this VALU-bound one).  finish() copies on that
+    stream and the pods context is bound back to the current stream before returning."""
     tm = timer or (lambda name: _NullCtx())
     time_, period = time_axis(ns, dt)
     dev = torch.device("cuda", ctx.device)
     nm = int(nm)
     if nm == 0:
-        return FourierResult(np.zeros((ns, 0), np.complex64), np.zeros((0, ns), np.int32),
-                             np.zeros(0, np.int64), np.zeros((0, 3)), period, time_)
-    cbuf = torch.empty((ns, nm, 2), dtype=torch.float32, device=dev)
-    with tm("dft"):
-        check(ctx.lib.pods_fourier(ctx.h, ptr(T), T.stride(0), nm, ns, ptr(np.ascontiguousarray(time_)),
-                                   float(period), ptr(cbuf)), "pods_fourier")
-    with tm("rank"):
-        if ns <= RANK_MAX_NS:
-            ind = torch.empty((nm, ns), dtype=torch.int32, device=dev)
-            cnt = torch.empty(nm, dtype=torch.int64, device=dev)
-            check(ctx.lib.pods_fourier_rank(ctx.h, ptr(cbuf), nm, ns, float(et), ptr(ind), ptr(cnt)),
-                  "pods_fourier_rank")
+        res = FourierResult(np.zeros((ns, 0), np.complex64), np.zeros((0, ns), np.int32),
+                            np.zeros(0, np.int64), np.zeros((0, 3)), period, time_)
+        return lambda: res
+    main = torch.cuda.current_stream(dev)
+    stream = main
+    if side:
+        stream = ctx.side_stream()
+        stream.wait_stream(main)
+        T.record_stream(stream)
+    with torch.cuda.stream(stream):
+        if side:
+            check(ctx.lib.pods_set_stream(ctx.h, ctypes.c_void_p(stream.cuda_stream)), "pods_set_stream")
+        try:
+            cbuf = torch.empty((ns, nm, 2), dtype=torch.float32, device=dev)
+            with tm("dft"):
+                check(ctx.lib.pods_fourier(ctx.h, ptr(T), T.stride(0), nm, ns,
+                                           ptr(np.ascontiguousarray(time_)), float(period), ptr(cbuf)),
+                      "pods_fourier")
+            ind = cnt = None
+            if ns <= RANK_MAX_NS:
+                with tm("rank"):
+                    ind = torch.empty((nm, ns), dtype=torch.int32, device=dev)
+                    cnt = torch.empty(nm, dtype=torch.int64, device=dev)
+                    check(ctx.lib.pods_fourier_rank(ctx.h, ptr(cbuf), nm, ns, float(et), ptr(ind), ptr(cnt)),
+                          "pods_fourier_rank")
+        finally:
+            if side:
+                check(ctx.lib.pods_set_stream(ctx.h, ctypes.c_void_p(main.cuda_stream)), "pods_set_stream")
+
+    def finish():
+        with torch.cuda.stream(stream):
             c = cbuf.cpu().numpy().view(np.complex64).reshape(ns, nm)
-            c_ind = ind.cpu().numpy()
-            c_count = cnt.cpu().numpy()
-            if np.any(c_count < 0):
-                raise IndexError("energy target not reachable (et = %r > 1?)" % et)
-            FC = fc_rows(c, c_ind, c_count)
-        else:
-            c = cbuf.cpu().numpy().view(np.complex64).reshape(ns, nm)
-            c_ind, c_count, FC = host_rank_and_count(c, et)
-    return FourierResult(c=c, c_ind=c_ind, c_count=c_count, FC=FC, period=period, time=time_)
+            if ind is not None:
+                c_ind = ind.cpu().numpy()
+                c_count = cnt.cpu().numpy()
+                if np.any(c_count < 0):
+                    raise IndexError("energy target not reachable (et = %r > 1?)" % et)
+                FC = fc_rows(c, c_ind, c_count)
+            else:
+                c_ind, c_count, FC = host_rank_and_count(c, et)
+        return FourierResult(c=c, c_ind=c_ind, c_count=c_count, FC=FC, period=period, time=time_)
+    return finish
 
 
 class _NullCtx:
@@ -381,10 +424,14 @@ def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=Non
     gen = gen or Generator(setup, device=device, rank=rank, world=world)
     with tm("generate"):
         snap = gen.generate()
-    pod = run_pod(snap, setup.nm, dist=dist_, full_temporal=full_temporal, timer=timer)
-    fo = None
-    if rank == 0:
-        fo = run_fourier(gen.ctx, pod.T, pod.nm, setup.ns, setup.dt_eff, setup.et, timer=timer)
+    pending = []
+
+    def start_fourier(T, nmt):
+        pending.append(launch_fourier(gen.ctx, T, nmt, setup.ns, setup.dt_eff, setup.et, timer=timer,
+                                      side=True))
+    pod = run_pod(snap, setup.nm, dist=dist_, full_temporal=full_temporal, timer=timer,
+                  on_temporal=start_fourier)
+    fo = pending[0]() if pending else None
     return gen, pod, fo
 
 
