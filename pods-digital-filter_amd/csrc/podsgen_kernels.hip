@@ -278,6 +278,71 @@ __global__ __launch_bounds__(256) void k_mt_generate_full(const uint32_t* __rest
   }
 }
 
+// Row-slab generator (multi-GPU: this rank's rows [rlo, rhi) of every padded plane, the
+// 2nfy halo included).  Same structure as k_mt_generate_full; every substream still twists
+// through all of its blocks (the stream is sequential), but blocks with no double in the
+// slab skip the tempering, conversion and stores -- at 8 ranks that is ~85% of them.
+// Double D of the stream: plane q = D / S, offset o = D % S, row o / Kp; it goes to
+// out[q * Sl + o - rlo * Kp] when rlo <= row < rhi.  Needs S >= 312 (a block spans at most
+// two planes).
+__global__ __launch_bounds__(256) void k_mt_generate_slab(const uint32_t* __restrict__ states, int G,
+                                                          int64_t Bs, int64_t ntot, int64_t S, int Kp,
+                                                          int rlo, int rhi, int64_t Sl, double low,
+                                                          double range, double* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t buf[2][MTN];
+  const int g = blockIdx.x, t = threadIdx.x;
+  if (g >= G) return;
+  for (int i = t; i < MTN; i += 256) buf[0][i] = states[(size_t)g * MTN + i];
+  __syncthreads();
+  const int64_t D0 = (int64_t)g * Bs * 312;
+  int64_t nb = (ntot - D0 + 311) / 312;
+  nb = nb < Bs ? nb : Bs;
+  const int64_t olo = (int64_t)rlo * Kp, ohi = (int64_t)rhi * Kp;  // slab offsets within a plane
+  // plane and offset of the current block's first double, advanced by 312 per block
+  int64_t q0 = D0 / S, o0 = D0 - (D0 / S) * S;
+  for (int64_t b = 0; b <= nb; ++b) {
+    const uint32_t* cur = buf[b & 1];
+    uint32_t* nxt = buf[(b + 1) & 1];
+    const bool tw = b < nb;
+    if (tw && t < 227) nxt[t] = mt_mix(cur[t], cur[t + 1], cur[t + 397]);
+    if (b >= 1) {
+      // block b-1 spans offsets [o0, o0 + 312) of plane q0 (wrapping into plane q0 + 1)
+      const int64_t e0 = o0 + 311;
+      const bool any = (o0 < ohi && e0 >= olo) || (e0 >= S && e0 - S >= olo);
+      if (any && t < 156) {
+        const uint4 w = reinterpret_cast<const uint4*>(cur)[t];
+        const uint32_t a0 = mt_temper(w.x) >> 5, b0 = mt_temper(w.y) >> 6;
+        const uint32_t a1 = mt_temper(w.z) >> 5, b1 = mt_temper(w.w) >> 6;
+        const double u0 = ((double)a0 * 67108864.0 + (double)b0) / 9007199254740992.0;
+        const double u1 = ((double)a1 * 67108864.0 + (double)b1) / 9007199254740992.0;
+        const int64_t Db = D0 + (b - 1) * 312 + 2 * t;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          int64_t q = q0, o = o0 + 2 * t + h;
+          if (o >= S) {
+            o -= S;
+            ++q;
+          }
+          if (Db + h < ntot && o >= olo && o < ohi) out[q * Sl + o - olo] = low + range * (h ? u1 : u0);
+        }
+      }
+      o0 += 312;
+      if (o0 >= S) {
+        o0 -= S;
+        ++q0;
+      }
+    }
+    if (!tw) break;
+    __syncthreads();
+    if (t < 227) nxt[227 + t] = mt_mix(cur[227 + t], cur[228 + t], nxt[t]);
+    __syncthreads();
+    if (t < 169) nxt[454 + t] = mt_mix(cur[454 + t], cur[455 + t], nxt[227 + t]);
+    __syncthreads();
+    if (t == 0) nxt[623] = mt_mix(cur[623], nxt[0], nxt[396]);
+    __syncthreads();
+  }
+}
+
 // -----------------------------------------------------------------------------------------
 // separable filter
 // -----------------------------------------------------------------------------------------
@@ -310,6 +375,42 @@ __global__ __launch_bounds__(256) void k_filter_x(const double* __restrict__ R,
 #pragma unroll
     for (int a = 0; a < NX; ++a) acc = acc + w[a] * b[a];
     T1[((int64_t)c * ns + i) * Sl + pt] = acc;
+#pragma unroll
+    for (int a = 0; a < NX - 1; ++a) w[a] = w[a + 1];
+  }
+}
+
+// The same x pass on two adjacent points per thread (16-B loads and stores; Sl even, so every
+// plane starts 16-B aligned).  Per point the arithmetic is identical to k_filter_x.
+template <int NX>
+__global__ __launch_bounds__(256) void k_filter_x2(const double* __restrict__ R,
+                                                   const double* __restrict__ bx, int ns,
+                                                   int64_t Sl, int steps_per_chunk,
+                                                   double* __restrict__ T1) {
+  const int64_t pp = (int64_t)blockIdx.x * 256 + threadIdx.x;  // point pair
+  const int c = blockIdx.y;
+  if (2 * pp >= Sl) return;
+  const int i0 = blockIdx.z * steps_per_chunk;
+  const int i1 = min(ns, i0 + steps_per_chunk);
+  if (i0 >= i1) return;
+  double b[NX];
+#pragma unroll
+  for (int a = 0; a < NX; ++a) b[a] = bx[NX - 1 - a];
+  const int64_t Sl2 = Sl >> 1;
+  const double2* R2 = reinterpret_cast<const double2*>(R);
+  double2* T2 = reinterpret_cast<double2*>(T1);
+  double2 w[NX];
+#pragma unroll
+  for (int a = 0; a < NX - 1; ++a) w[a] = R2[stream_plane(c, i0 + a, NX) * Sl2 + pp];
+  for (int i = i0; i < i1; ++i) {
+    w[NX - 1] = R2[stream_plane(c, i + NX - 1, NX) * Sl2 + pp];
+    double ax = 0.0, ay = 0.0;
+#pragma unroll
+    for (int a = 0; a < NX; ++a) {
+      ax = ax + w[a].x * b[a];
+      ay = ay + w[a].y * b[a];
+    }
+    T2[((int64_t)c * ns + i) * Sl2 + pp] = make_double2(ax, ay);
 #pragma unroll
     for (int a = 0; a < NX - 1; ++a) w[a] = w[a + 1];
   }
@@ -1148,6 +1249,11 @@ hipError_t launch_mt_generate(const uint32_t* states, int G, int64_t Bs, int64_t
     hipLaunchKernelGGL(k_mt_generate_full, dim3(G), dim3(256), 0, st, states, G, Bs, ntot, low, range, out);
     return hipGetLastError();
   }
+  if (S >= 312 && std::getenv("PODS_MT_GENERIC") == nullptr) {
+    hipLaunchKernelGGL(k_mt_generate_slab, dim3(G), dim3(256), 0, st, states, G, Bs, ntot, S, Kp, rlo, rhi,
+                       Sl, low, range, out);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_mt_generate, dim3((G + 3) / 4), dim3(256), 0, st, states, G, Bs, ntot, S, Kp,
                      rlo, rhi, Sl, low, range, out);
   return hipGetLastError();
@@ -1156,6 +1262,15 @@ hipError_t launch_mt_generate(const uint32_t* states, int G, int64_t Bs, int64_t
 template <int NX>
 static hipError_t launch_fx(const double* R, const double* bx, int ns, int64_t Sl, int ncomp,
                             int chunk, double* T1, hipStream_t st) {
+  if (Sl % 2 == 0 && ((uintptr_t)R & 15) == 0 && ((uintptr_t)T1 & 15) == 0 &&
+      std::getenv("PODS_FX_SCALAR") == nullptr) {
+    // point pairs: half the threads, so twice the step chunks keep the same parallelism
+    const int chunk2 = std::max(1, (chunk + 1) / 2);
+    const int nch = (ns + chunk2 - 1) / chunk2;
+    dim3 grid((unsigned)((Sl / 2 + 255) / 256), (unsigned)ncomp, (unsigned)nch);
+    hipLaunchKernelGGL(k_filter_x2<NX>, grid, dim3(256), 0, st, R, bx, ns, Sl, chunk2, T1);
+    return hipGetLastError();
+  }
   const int nch = (ns + chunk - 1) / chunk;
   dim3 grid((unsigned)((Sl + 255) / 256), (unsigned)ncomp, (unsigned)nch);
   hipLaunchKernelGGL(k_filter_x<NX>, grid, dim3(256), 0, st, R, bx, ns, Sl, chunk, T1);
