@@ -218,8 +218,8 @@ def POD(A, num_snapshots, num_points, num_components, correct_for_cell_volumes, 
         test_POD_orthogonality, write_matrices, grid, mean_field, dt, var_name, ifig, N,
         iwindow, stride, i_d, dist=None):
     """PODFS.py:1294-1393.  `A` is mean-subtracted in the reference call (digitalfilters.py
-    :1492-1500); a DeviceSnapshots handle carries the uncentred device matrix and its mean
-    is subtracted inside the kernels (same values)."""
+    :1492-1500); a DeviceSnapshots handle carries the uncentred device matrix, which run_pod
+    centres in place (pods_center, the same subtraction) after the bit-exact mean."""
     if correct_for_cell_volumes != "false":
         raise NotImplementedError("the GPU POD path implements correct_for_cell_volumes='false' "
                                   "(the only value digitalfilters.main passes); use "

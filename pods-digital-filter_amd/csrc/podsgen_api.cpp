@@ -226,6 +226,8 @@ struct pods_ctx {
   int nprog_mean = 0;
   bool mean_valid = false;
   bool have_snapshots = false;  // A holds ns x rowlen snapshots (generated or loaded)
+  bool centered = false;        // A holds A - mean (pods_center); consumers subtract zero
+  DevBuf zero;                  // rowpad zeros: the mean operand once A is centred
   std::vector<double> stage;  // host staging for small uploads
   // device-resident DFT / ranking programs and time axis, re-uploaded only on change
   int dft_ns = -1, dft_nprog = 0, rank_ns = -1, rank_nprog = 0;
@@ -323,7 +325,7 @@ int pods_destroy(pods_ctx* c) {
   for (DevBuf* b : {&c->R, &c->T1, &c->A, &c->mean, &c->lund, &c->taps, &c->rot, &c->prog_mean,
                     &c->prog_dft, &c->tbuf, &c->mag, &c->lam, &c->cwork, &c->items, &c->e_wm,
                     &c->e_x, &c->e_flags, &c->e_det, &c->e_v, &c->e_t, &c->e_part, &c->e_w2,
-                    &c->e_inv, &c->spwork, &c->prog_rank})
+                    &c->e_inv, &c->spwork, &c->prog_rank, &c->zero})
     release(*b);
   c->rng.free_all();
   delete c;
@@ -413,6 +415,7 @@ int pods_df_configure(pods_ctx* c, const pods_df_params* prm, const double* bx, 
   c->configured = true;
   c->have_snapshots = false;
   c->mean_valid = false;
+  c->centered = false;
   return PODS_OK;
   PODS_CATCH
 }
@@ -442,6 +445,7 @@ int pods_df_generate(pods_ctx* c) {
                                   c->A.as<double>(), c->stream));
   c->have_snapshots = true;
   c->mean_valid = false;
+  c->centered = false;
   return PODS_OK;
   PODS_CATCH
 }
@@ -483,6 +487,7 @@ int pods_set_snapshots(pods_ctx* c, const double* at, int ns, int64_t rowlen) {
   c->configured = false;
   c->have_snapshots = true;
   c->mean_valid = false;
+  c->centered = false;
   return PODS_OK;
   PODS_CATCH
 }
@@ -540,9 +545,24 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
     c->nitems = (int)items.size() / 4;
     c->items_key = key;
   }
-  PODS_HIP(pods::launch_syrk(kern, c->A.as<double>(), c->rowpad, ns, c->rowpad, c->mean.as<double>(),
+  PODS_HIP(pods::launch_syrk(kern, c->A.as<double>(), c->rowpad, ns, c->rowpad,
+                             c->centered ? c->zero.as<double>() : c->mean.as<double>(),
                              c->items.as<int>(), c->nitems, nsplit, ksplit, C_dev, ns, divide,
-                             c->cwork.as<double>(), c->stream));
+                             c->cwork.as<double>(), c->centered ? 1 : 0, c->stream));
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_center(pods_ctx* c) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!c->have_snapshots || !c->mean_valid) return fail(PODS_ERR_STATE, "pods_center needs pods_mean first");
+  if (c->centered) return PODS_OK;
+  PODS_HIP(hipSetDevice(c->device));
+  PODS_HIP(ensure(c->zero, (size_t)c->rowpad * sizeof(double)));
+  PODS_HIP(hipMemsetAsync(c->zero.p, 0, (size_t)c->rowpad * sizeof(double), c->stream));
+  PODS_HIP(pods::launch_center(c->A.as<double>(), c->rowpad, c->p.ns, c->mean.as<double>(), c->stream));
+  c->centered = true;
   return PODS_OK;
   PODS_CATCH
 }
@@ -559,6 +579,7 @@ int pods_set_mean(pods_ctx* c, const double* mean_host) {
     PODS_HIP(hipStreamSynchronize(c->stream));
   }
   c->mean_valid = true;
+  c->centered = false;  // an explicit mean is subtracted by the consumers again
   return PODS_OK;
   PODS_CATCH
 }
@@ -636,7 +657,8 @@ int pods_spatial_modes(pods_ctx* c, const double* T, int ldT, const double* lam,
                           c->stream));
   const size_t wb = pods::spatial_work_bytes(c->rowlen, c->p.ns);
   if (wb) PODS_HIP(ensure(c->spwork, wb));
-  PODS_HIP(pods::launch_spatial(c->A.as<double>(), c->rowlen, c->p.ns, c->mean.as<double>(), T, ldT, nm,
+  PODS_HIP(pods::launch_spatial(c->A.as<double>(), c->rowlen, c->p.ns,
+                                c->centered ? c->zero.as<double>() : c->mean.as<double>(), T, ldT, nm,
                                 c->lam.as<double>(), phi, wb ? c->spwork.as<double>() : nullptr, c->stream));
   PODS_HIP(hipStreamSynchronize(c->stream));
   return PODS_OK;

@@ -30,7 +30,9 @@ int syrk_plan(int kernel, int ns, int64_t Kdim, int64_t* ksplit);
 // items: nitems x int4 {bi, bj, split, 0} in launch order (see podsgen_api.cpp syrk_items)
 hipError_t launch_syrk(int kernel, const double* AT, int64_t ld, int ns, int64_t Kdim,
                        const double* mean, const int* items, int nitems, int nsplit, int64_t ksplit,
-                       double* C, int64_t ldc, int divide, double* work, hipStream_t st);
+                       double* C, int64_t ldc, int divide, double* work, int centred, hipStream_t st);
+// A <- A - mean in place (K-tiled layout, rowpad rows x ns snapshots)
+hipError_t launch_center(double* AT, int64_t rowpad, int ns, const double* mean, hipStream_t st);
 hipError_t launch_divide(double* x, int64_t n, double d, hipStream_t st);
 hipError_t launch_temporal(const double* V, int64_t v_rs, int64_t v_cs, int ns, int ncols,
                            int nvalid, const double* lam, double* mag, double* T, hipStream_t st);

@@ -699,6 +699,21 @@ __global__ __launch_bounds__(256) void k_mean(const double* __restrict__ AT, int
   mean[r] = (0.0 + stk[0]) / (double)ns;
 }
 
+// main() :1492-1495 (A[:, j] = A[:, j] - mean_field) in place on the K-tiled snapshot matrix:
+// element f of AT belongs to row r = (f / (16 ns)) * 16 + f % 16.  Two doubles per thread.
+// The subtraction is the one the SYRK and the spatial-mode kernels would otherwise repeat
+// per fragment read, so their results are unchanged bit for bit.
+__global__ __launch_bounds__(256) void k_center(double* __restrict__ AT, int64_t npairs, int ns,
+                                                const double* __restrict__ mean) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= npairs) return;
+  const int64_t f = 2 * q;
+  const int64_t r = (f / ((int64_t)ns << 4)) * 16 + (f & 15);
+  double2* p = reinterpret_cast<double2*>(AT) + q;
+  const double2 v = *p;
+  *p = make_double2(v.x - mean[r], v.y - mean[r + 1]);
+}
+
 // -----------------------------------------------------------------------------------------
 // correlation SYRK on fp64 MFMA (v_mfma_f64_16x16x4_f64)
 // C[i][j] = sum_r (A_T[i][r]-m[r]) (A_T[j][r]-m[r]), lower-triangle tiles, mirrored.
@@ -838,6 +853,9 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds_byte_addr) 
                                    16, 0, 0);
 }
 
+// CENTRED = 1: A was centred in place (k_center), so the fragments go to the MFMAs as
+// read; the in-loop subtraction costs 8 v_add_f64 per 16 MFMAs (57.0 -> 52.9 ms measured).
+template <int CENTRED>
 __global__ __launch_bounds__(512, 1) void k_syrk_glds(const double* __restrict__ AT, int ns,
                                                       int64_t Kdim, const double* __restrict__ mean,
                                                       const int4* __restrict__ items, int nitems,
@@ -912,9 +930,9 @@ __global__ __launch_bounds__(512, 1) void k_syrk_glds(const double* __restrict__
       const double mk = Ms[k];
       double a[4], bv[4];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) a[m] = Xs[xrow + koff + m * 256] - mk;
+      for (int m = 0; m < 4; ++m) a[m] = CENTRED ? Xs[xrow + koff + m * 256] : Xs[xrow + koff + m * 256] - mk;
 #pragma unroll
-      for (int n = 0; n < 4; ++n) bv[n] = Ys[yrow + koff + n * 256] - mk;
+      for (int n = 0; n < 4; ++n) bv[n] = CENTRED ? Ys[yrow + koff + n * 256] : Ys[yrow + koff + n * 256] - mk;
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -1389,6 +1407,12 @@ hipError_t launch_mean(const double* AT, int64_t rowlen, int ns, const int* prog
   return hipGetLastError();
 }
 
+hipError_t launch_center(double* AT, int64_t rowpad, int ns, const double* mean, hipStream_t st) {
+  const int64_t npairs = rowpad * (int64_t)ns / 2;  // rowpad is a multiple of 16
+  hipLaunchKernelGGL(k_center, dim3((unsigned)((npairs + 255) / 256)), dim3(256), 0, st, AT, npairs, ns, mean);
+  return hipGetLastError();
+}
+
 // Number of K splits for `tiles` work tiles on `slots` concurrent workgroups: ~8+ rounds,
 // chosen to minimise the partial last round, >= 64 K-tiles of 16 per item.
 int syrk_plan(int kernel, int ns, int64_t Kdim, int64_t* ksplit) {
@@ -1427,20 +1451,21 @@ int syrk_plan(int kernel, int ns, int64_t Kdim, int64_t* ksplit) {
 
 hipError_t launch_syrk(int kernel, const double* AT, int64_t ld, int ns, int64_t Kdim,
                        const double* mean, const int* items, int nitems, int nsplit, int64_t ksplit,
-                       double* C, int64_t ldc, int divide, double* work, hipStream_t st) {
+                       double* C, int64_t ldc, int divide, double* work, int centred, hipStream_t st) {
   const int64_t slab = (int64_t)ns * ldc;
   const int final_write = nsplit == 1;
   if (kernel == 2) {
-    static bool attr = false;
-    if (!attr) {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_syrk_glds),
+    auto launch = [&](auto kern) -> hipError_t {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                          hipFuncAttributeMaxDynamicSharedMemorySize,
                                          syrk2::NST * syrk2::STAGE);
       if (e != hipSuccess) return e;
-      attr = true;
-    }
-    hipLaunchKernelGGL(k_syrk_glds, dim3(nitems), dim3(512), syrk2::NST * syrk2::STAGE, st, AT, ns, Kdim,
-                       mean, reinterpret_cast<const int4*>(items), nitems, ksplit, work, ldc, slab);
+      hipLaunchKernelGGL(kern, dim3(nitems), dim3(512), syrk2::NST * syrk2::STAGE, st, AT, ns, Kdim,
+                         mean, reinterpret_cast<const int4*>(items), nitems, ksplit, work, ldc, slab);
+      return hipGetLastError();
+    };
+    hipError_t le = centred ? launch(k_syrk_glds<1>) : launch(k_syrk_glds<0>);
+    if (le != hipSuccess) return le;
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_syrk_reduce, dim3(((ns + 63) / 64) * ((ns + 63) / 64 + 1) / 2), dim3(256), 0, st, work, nsplit, slab,

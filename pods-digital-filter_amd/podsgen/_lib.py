@@ -47,6 +47,7 @@ SIGNATURES = {
     "pods_copy": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_size_t, c_int]),
     "pods_mean": (c_int, [c_void_p, c_void_p, c_int]),
     "pods_set_mean": (c_int, [c_void_p, c_void_p]),
+    "pods_center": (c_int, [c_void_p]),
     "pods_lund_apply": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_void_p, c_int, c_void_p]),
     "pods_corr": (c_int, [c_void_p, c_void_p, c_int]),
     "pods_divide_inplace": (c_int, [c_void_p, c_void_p, c_i64, c_dbl]),

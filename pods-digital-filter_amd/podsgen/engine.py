@@ -230,6 +230,8 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
     mean = torch.empty(snap.rowlen, dtype=torch.float64, device=dev)
     with tm("mean"):
         check(lib.pods_mean(ctx.h, ptr(mean), 1), "pods_mean")
+    with tm("center"):  # main() :1493-1495, in place
+        check(lib.pods_center(ctx.h), "pods_center")
     C = torch.empty((ns, ns), dtype=torch.float64, device=dev)
     with tm("corr"):
         check(lib.pods_corr(ctx.h, ptr(C), 1 if world == 1 else 0), "pods_corr")

@@ -239,6 +239,25 @@ def test_row_slabs_large(ctx, J, K, ns, world):
         assert np.array_equal(rows, full[comp * P:(comp + 1) * P]), comp
 
 
+def test_center_in_place(ctx):
+    """pods_center: A - mean (main() :1493-1495) in place, bit for bit the numpy subtraction;
+    the correlation from the centred A equals the one that subtracts inside the SYRK."""
+    s = podsgen.DFSetup(jma=40, kma=24, ns=48, seed=8)
+    gen = E.Generator(s, ctx=ctx)
+    snap = gen.generate()
+    A = snap.to_host()
+    mean = torch.empty(snap.rowlen, dtype=torch.float64, device="cuda")
+    podsgen.check(ctx.lib.pods_mean(ctx.h, E.ptr(mean), 1), "pods_mean")
+    C0 = torch.empty((s.ns, s.ns), dtype=torch.float64, device="cuda")
+    podsgen.check(ctx.lib.pods_corr(ctx.h, E.ptr(C0), 1), "pods_corr")
+    podsgen.check(ctx.lib.pods_center(ctx.h), "pods_center")
+    Ac = snap.to_host()
+    assert np.array_equal(Ac, A - mean.cpu().numpy()[:, None])
+    C1 = torch.empty_like(C0)
+    podsgen.check(ctx.lib.pods_corr(ctx.h, E.ptr(C1), 1), "pods_corr")
+    assert torch.equal(C0, C1)
+
+
 def test_medium_case_vs_oracle(ctx):
     """256 x 256 inlet, 24 steps: generation bit-exact against the oracle."""
     s = podsgen.DFSetup(jma=256, kma=256, ns=24, seed=4242)
