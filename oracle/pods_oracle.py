@@ -433,6 +433,7 @@ class DFConfig:
     prf: Optional[dict] = None
     mean_profile: str = "hyperbolic-tangent"   # -p (:1146); the 2-D ones go through adapt2d
     inner_d: float = 0.5                       # --ring (:1275)
+    ln_prf: Optional[float] = None             # lnx from read_prf (:1301-1305)
     # derived
     nfx: int = 0
     nfy: int = 0
@@ -448,6 +449,8 @@ class DFConfig:
         self.lnx = self.lny = self.lnz = self.lengthscale
         nf = int(math.ceil(self.fwidth * self.lengthscale))
         self.nfx = self.nfy = self.nfz = nf
+        if self.ln_prf is not None:
+            self.lnx = self.lny = self.lnz = self.ln_prf
         n1 = np.asarray(self.normal, dtype=np.float64)
         nrm = np.sqrt(n1[0] ** 2 + n1[1] ** 2 + n1[2] ** 2)
         self.n_unit = (n1[0] / nrm, n1[1] / nrm, n1[2] / nrm)

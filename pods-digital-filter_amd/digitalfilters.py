@@ -10,7 +10,9 @@ Keeps the reference's entry points (digitalfilters.py) and their meaning:
   filter3DSciPy1D(x, y, a, jma, kma, lnx, lny, lnz, nfx, nfy, nfz)   :100-140
   adapt1d(yu, yv, yw, uin, uuin, vvin, wwin, uwin, jma, kma)          :143-178
   adapt2prf(yu, yv, yw, uin, vin, win, uuin, vvin, wwin, uvin, uwin, vwin, jma, kma)  :180-231
+  adapt2d(yu, yv, yw, uin, uuin, vvin, wwin, uwin, jma, kma, mean_profile, inner_d)  :233-485
   read_profile(profilefile, kma)                        :487-522
+  read_prf(profilefile, res, mdot, den, bulk_velocity, non_dim, TestGrad)   :524-1035
   build_profile(...), prof_rotation_matrix(...), rotate_velocity(A, nx, ny, nz)  :1038-1131
   main()                                                :1134-1510
 
@@ -274,9 +276,6 @@ def make_parser():
 
 def setup_from_options(options):
     profilefile = options.profilefile
-    if profilefile.endswith(".prf"):
-        raise NotImplementedError("read_prf (.prf inlet profiles, digitalfilters.py:524-1035) is "
-                                  "SURVEY.md 8(f) row 2; not on the GPU path yet")
     seed = options.seed
     if seed is None:
         seed = int.from_bytes(os.urandom(4), "little")
@@ -286,9 +285,24 @@ def setup_from_options(options):
               normal=(options.nx, options.ny, options.nz), mean_profile=options.mean_profile,
               turb_profile=options.turb_profile, inner_d=options.ring)
     if profilefile != "none" and os.path.isfile(profilefile):
-        U, uu, vv, ww, uw = read_profile(profilefile, options.kma)
-        kw["profile1d"] = dict(U=U, uu=uu, vv=vv, ww=ww, uw=uw)
+        if profilefile.endswith(".prf"):  # :1299-1305 -- plane, grid and stresses from the file
+            (U, V, W, uu, vv, ww, uv, uw, vw, lnx, kma, jma, nx, ny, nz, ox, oy, oz) = read_prf(
+                profilefile, options.res, options.mdot, options.den, options.bulk_velocity,
+                options.non_dim, options.TestGrad)
+            kw.update(jma=jma, kma=kma, ln_prf=lnx, normal=(nx, ny, nz),
+                      prf=dict(U=U, V=V, W=W, uu=uu, vv=vv, ww=ww, uv=uv, uw=uw, vw=vw))
+            options.nx, options.ny, options.nz = nx, ny, nz      # the plane of the file
+            options.ox, options.oy, options.oz = ox, oy, oz
+        else:
+            U, uu, vv, ww, uw = read_profile(profilefile, options.kma)
+            kw["profile1d"] = dict(U=U, uu=uu, vv=vv, ww=ww, uw=uw)
     return _H.DFSetup(**kw)
+
+
+def read_prf(profilefile, res, mdot, den, bulk_velocity, non_dim, TestGrad):
+    """:524-1035 -- see podsgen/prf.py (host setup; the contour plots are not drawn)."""
+    from podsgen.prf import read_prf as _read_prf
+    return _read_prf(profilefile, res, mdot, den, bulk_velocity, non_dim, TestGrad)
 
 
 def main(argv=None):
@@ -313,8 +327,11 @@ def main(argv=None):
         else:
             print("Lengthscale in x-direction set to: ", s.lnx, "grid points")
             print("Filter width in x-direction set to: ", s.nfx, "grid points")
-    n1 = np.array([options.nx, options.ny, options.nz], dtype=np.float64)
-    nx, ny, nz = (n1 / np.sqrt(np.sum(n1 ** 2))).tolist()
+    if s.prf is not None and options.profilefile.endswith(".prf"):
+        nx, ny, nz = options.nx, options.ny, options.nz          # read_prf's unit normal (:1301)
+    else:
+        n1 = np.array([options.nx, options.ny, options.nz], dtype=np.float64)
+        nx, ny, nz = (n1 / np.sqrt(np.sum(n1 ** 2))).tolist()
     i_d = obj()
     i_d.kma, i_d.jma, i_d.ns, i_d.dt, i_d.nm, i_d.et = s.kma, s.jma, s.ns, s.dt_eff, s.nm, s.et
     i_d.rot = options.rot

@@ -97,9 +97,6 @@ def _adapt2d_lund(R00, R11, R22, R20):
     return a00, a10, a11, a20, a21, a22
 
 
-PROFILES_2D = ("double-hyperbolic-tangent", "circular-hyperbolic-tangent", "ring-hyperbolic-tangent")
-
-
 def prof_rotation_matrix(nx, ny, nz):
     n = np.sqrt(nx ** 2 + ny ** 2 + nz ** 2)
     n_proj = np.sqrt(nx ** 2 + ny ** 2)
@@ -143,6 +140,7 @@ class DFSetup:
     mean_profile: str = "hyperbolic-tangent"
     turb_profile: str = "top-hat"
     inner_d: float = 0.5                # --ring (:1275): inner radius of the ring profile
+    ln_prf: Optional[float] = None      # lnx = lny = lnz returned by read_prf (:1301-1305)
     prf: Optional[dict] = None         # (jma,kma) arrays U,V,W,uu,vv,ww,uv,uw,vw -> adapt2prf
     profile1d: Optional[dict] = None    # (kma,) arrays U,uu,vv,ww,uw from read_profile -> adapt1d
     nfx: int = field(default=0, init=False)
@@ -157,8 +155,10 @@ class DFSetup:
 
     def __post_init__(self):
         self.lnx = self.lny = self.lnz = float(self.lengthscale)
-        nf = int(math.ceil(self.fwidth * self.lengthscale))
+        nf = int(math.ceil(self.fwidth * self.lengthscale))  # :1282, from the CLI length scale
         self.nfx = self.nfy = self.nfz = nf
+        if self.ln_prf is not None:  # a .prf file replaces the taps' length scale, not nf
+            self.lnx = self.lny = self.lnz = float(self.ln_prf)
         n1 = np.asarray(self.normal, dtype=np.float64)
         nrm = np.sqrt(n1[0] ** 2 + n1[1] ** 2 + n1[2] ** 2)
         self.n_unit = (n1[0] / nrm, n1[1] / nrm, n1[2] / nrm)

@@ -28,6 +28,7 @@ Functions executed from the reference (file:line):
   digitalfilters.py:143-178  adapt1d
   digitalfilters.py:180-231  adapt2prf
   digitalfilters.py:233-485  adapt2d (needs scipy.interpolate in the namespace)
+  digitalfilters.py:524-1035 read_prf (plots dropped, see DROP_LINES)
   digitalfilters.py:1038-1062 build_profile
   digitalfilters.py:1064-1131 prof_rotation_matrix / rotate_velocity
   PODFS.py:1409-1427          write_eigenvalues
@@ -73,7 +74,12 @@ SEMANTIC_PATCHES = {
 }
 
 DF_FUNCS = ["calccoeff", "filter3DSciPy1D", "adapt1d", "adapt2prf", "adapt2d", "build_profile",
-            "prof_rotation_matrix", "rotate_velocity"]
+            "prof_rotation_matrix", "rotate_velocity", "read_prf"]
+# read_prf (digitalfilters.py:524-1035): Python 2 `3/2 == 1` (:758, :767, :779, :788), and its
+# nplotlib contour plots (:851-872, :1011-1022; VTK/matplotlib, side effects only) dropped
+# line by line (regex below) -- nothing they draw feeds the returned profile.
+SEMANTIC_PATCHES["read_prf"] = [("(3/2)", "(3//2)")]
+DROP_LINES = {"read_prf": r"^(\s*)plt\.(contourf|close)\(.*$"}
 PROFILES_2D = ("double-hyperbolic-tangent", "circular-hyperbolic-tangent", "ring-hyperbolic-tangent")
 POD_FUNCS = ["write_eigenvalues", "sort_eigenvalues", "calculate_correlation_matrix",
              "fourier_coefficients"]
@@ -115,6 +121,10 @@ def load_reference():
             for old, new in SEMANTIC_PATCHES.get(name, []):
                 assert old in text, (name, old)
                 text = text.replace(old, new)
+            if name in DROP_LINES:
+                import re
+                text, ndrop = re.subn(DROP_LINES[name], r"\1pass", text, flags=re.M)
+                assert ndrop == 34, ndrop
             exec(compile(text, "<reference:%s>" % name, "exec"), ns)
     return ns
 
@@ -126,7 +136,7 @@ class Obj(object):
 def run_reference_pipeline(ref, *, jma, kma, ns, seed, lengthscale=3.0, fwidth=2.0, dt=0.0,
                            res=0.1, bulk_velocity=1.0, u_dash=0.02, nm=20, et=0.9,
                            normal=(1.0, 0.0, 0.0), prf=None, workdir=None,
-                           mean_profile="hyperbolic-tangent", inner_d=0.5):
+                           mean_profile="hyperbolic-tangent", inner_d=0.5, ln_prf=None):
     """Replay digitalfilters.py main() (:1244-1510) + PODFS.POD (:1294-1393) with the
     reference's own functions.  prf=None -> built profile (adapt1d, or adapt2d for the 2-D
     mean profiles, + rotation); prf=dict(U,V,W,uu,vv,ww,uv,uw,vw) of (jma,kma) arrays ->
@@ -136,6 +146,8 @@ def run_reference_pipeline(ref, *, jma, kma, ns, seed, lengthscale=3.0, fwidth=2
     lnx = lny = lnz = lengthscale                         # :1262-1264
     nf = int(math.ceil(fwidth * lengthscale))             # :1267
     nfx = nfy = nfz = nf
+    if ln_prf is not None:                                # :1301-1305 (read_prf's lnx)
+        lnx = lny = lnz = ln_prf
     n1 = np.asarray(normal, dtype=np.float64)
     nx = n1[0] / np.sqrt(n1[0]**2 + n1[1]**2 + n1[2]**2)  # :1276-1278
     ny = n1[1] / np.sqrt(n1[0]**2 + n1[1]**2 + n1[2]**2)
@@ -291,6 +303,68 @@ CASES = {
 }
 
 
+def write_synthetic_prf(path, seed=5):
+    """A CFD-style .prf plane (CFDCodeIntegration.rst format): 25 x 19 points on a tilted
+    rectangle, smooth u, v, w, k, e (k = e = 0 on one edge)."""
+    r = np.random.RandomState(seed)
+    e1 = np.array([0.2, 0.9, 0.1]); e1 /= np.linalg.norm(e1)
+    e2 = np.cross(np.array([0.95, 0.1, 0.3]), e1); e2 /= np.linalg.norm(e2)
+    o = np.array([0.3, -0.4, 0.25])
+    rows = []
+    for a in np.linspace(0.0, 1.2, 25):
+        for b in np.linspace(0.0, 0.9, 19):
+            x = o + a * e1 + b * e2
+            u = 1.0 + 0.2 * np.sin(3 * a) * np.cos(2 * b)
+            v, w = 0.05 * a, -0.03 * b
+            k = 0.0 if b == 0.0 else 0.01 * (1 + 0.5 * a * b) * (1 + 0.01 * r.rand())
+            e = 0.0 if b == 0.0 else 0.05 * (1 + a)
+            rows.append((x[0], x[1], x[2], u, v, w, k, e))
+    with open(path, "w") as f:
+        f.write("# synthetic inlet # name of the profile\n# turbulence model, k-e\n")
+        f.write("type, xyz # type of profile (rad or xyz)\n")
+        f.write("data,x,y,z,u,v,w,k,e\n")
+        for row in rows:
+            f.write(",".join("%0.12f" % v for v in row) + "\n")
+
+
+def unit_read_prf(ref):
+    """read_prf on the synthetic plane: plain, bulk-velocity rescaled, mass-flow rescaled."""
+    out = {}
+    tmp = tempfile.mkdtemp(prefix="pods_prf_")
+    try:
+        path = os.path.join(tmp, "inlet.prf")
+        write_synthetic_prf(path)
+        with open(path) as f:
+            out["prf_text"] = np.array(f.read())
+        for tag, (mdot, den, bulk) in {"plain": (0.0, 0.0, 1.0), "bulk": (0.0, 0.0, 2.5),
+                                       "mdot": (0.7, 1.2, 1.0)}.items():
+            _stdout = sys.stdout
+            sys.stdout = io.StringIO()
+            try:
+                res = ref["read_prf"](path, 0.1, mdot, den, bulk, False, False)
+            finally:
+                sys.stdout = _stdout
+            for name, v in zip(("U", "V", "W", "uu", "vv", "ww", "uv", "uw", "vw"), res[:9]):
+                out["%s_%s" % (tag, name)] = np.asarray(v)
+            out[tag + "_scalars"] = np.array([float(x) for x in res[9:]])
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    return out
+
+
+def prf_case(ref, ns=6, seed=31):
+    """End-to-end main() on the read_prf path: profile from the file, adapt2prf, no rotation."""
+    u = unit_read_prf(ref)
+    prf = {k: u["plain_" + k] for k in ("U", "V", "W", "uu", "vv", "ww", "uv", "uw", "vw")}
+    lnx, kma, jma = u["plain_scalars"][:3]
+    kw = dict(jma=int(jma), kma=int(kma), ns=ns, seed=seed, prf=prf, ln_prf=float(lnx))
+    res = run_reference_pipeline(ref, **kw)
+    res.update({"cfg_jma": np.array(int(jma)), "cfg_kma": np.array(int(kma)), "cfg_ns": np.array(ns),
+                "cfg_seed": np.array(seed), "cfg_ln_prf": np.array(float(lnx))})
+    res.update({"prf_" + k: v for k, v in prf.items()})
+    return res
+
+
 def unit_adapt2d(ref):
     """adapt2d on raw random fields for each 2-D profile, odd/even/non-square grids."""
     rs = np.random.RandomState(77)
@@ -319,6 +393,10 @@ def main():
     if only:
         if "unit_adapt2d" in only:
             np.savez_compressed(os.path.join(HERE, "unit_adapt2d.npz"), **unit_adapt2d(ref))
+        if "unit_read_prf" in only:
+            np.savez_compressed(os.path.join(HERE, "unit_read_prf.npz"), **unit_read_prf(ref))
+        if "readprf_case" in only:
+            np.savez_compressed(os.path.join(HERE, "readprf_case.npz"), **prf_case(ref))
         for name, kw in CASES.items():
             if name in only:
                 _write_case(ref, name, kw)
@@ -339,6 +417,8 @@ def main():
         Rs.append(ref["prof_rotation_matrix"](n[0], n[1], n[2]))
     np.savez_compressed(os.path.join(HERE, "unit_rotation.npz"), normals=normals, R=np.array(Rs))
     np.savez_compressed(os.path.join(HERE, "unit_adapt2d.npz"), **unit_adapt2d(ref))
+    np.savez_compressed(os.path.join(HERE, "unit_read_prf.npz"), **unit_read_prf(ref))
+    np.savez_compressed(os.path.join(HERE, "readprf_case.npz"), **prf_case(ref))
     for name, kw in CASES.items():
         _write_case(ref, name, kw)
 

@@ -55,6 +55,27 @@ def test_main_end_to_end_cli_case(golden_dir, tmp_path, monkeypatch):
     assert i_d.nm == 4
 
 
+def test_main_prf_inlet(golden_dir, tmp_path, monkeypatch):
+    """python digitalfilters.py -i inlet.prf -n 6 --seed 31: read_prf sizes the grid and the
+    per-point stresses (adapt2prf, no rotation); the snapshots' mean and the eigenvalues
+    match the reference replay of the same file (tests/golden/readprf_case.npz)."""
+    import digitalfilters as df
+    g = np.load(os.path.join(golden_dir, "readprf_case.npz"))
+    u = np.load(os.path.join(golden_dir, "unit_read_prf.npz"))
+    monkeypatch.chdir(tmp_path)
+    with open("inlet.prf", "w") as f:
+        f.write(str(u["prf_text"]))
+    i_d = df.main(["-i", "inlet.prf", "-n", "6", "--seed", "31"])
+    assert (i_d.jma, i_d.kma) == (int(g["cfg_jma"]), int(g["cfg_kma"]))
+    assert np.array_equal(i_d.mean_field, g["mean_field"])
+    lam = i_d.energy
+    ref = g["energy"].real
+    assert np.max(np.abs(lam - ref)) <= 1e-12 * ref[0]
+    assert i_d.nm == int(g["nm"])
+    scal = u["plain_scalars"]
+    assert np.array_equal(np.array(i_d.n), scal[3:6])
+
+
 def test_operator_api_bit_exact(golden_dir):
     import digitalfilters as df
     g = np.load(os.path.join(golden_dir, "unit_filter.npz"))

@@ -22,7 +22,7 @@ import podsgen  # noqa: E402
 from podsgen import engine as E  # noqa: E402
 
 CASES = ["c1_32x32x64", "cli_10x11x5", "odd_12x9x17_aniso", "prf_8x12x9", "rot_6x7x6",
-         "dtanh_9x12x7", "circ_11x10x6", "ring_12x13x6"]
+         "dtanh_9x12x7", "circ_11x10x6", "ring_12x13x6", "readprf_case"]
 
 
 def load(golden_dir, name):
@@ -41,6 +41,8 @@ def setup_from(g):
         kw["mean_profile"] = str(g["cfg_mean_profile"])
     if "cfg_inner_d" in g.files:
         kw["inner_d"] = float(g["cfg_inner_d"])
+    if "cfg_ln_prf" in g.files:
+        kw["ln_prf"] = float(g["cfg_ln_prf"])
     return podsgen.DFSetup(**kw)
 
 

@@ -68,6 +68,21 @@ def test_adapt2d_host_factor_matches_oracle_loop(golden_dir, tag):
         assert np.array_equal(a, b, equal_nan=True)
 
 
+@pytest.mark.parametrize("tag,mdot,den,bulk", [("plain", 0.0, 0.0, 1.0), ("bulk", 0.0, 0.0, 2.5),
+                                              ("mdot", 0.7, 1.2, 1.0)])
+def test_read_prf_matches_reference(golden_dir, tmp_path, tag, mdot, den, bulk):
+    """read_prf (digitalfilters.py:524-1035) on a synthetic CFD plane == the reference's
+    output (griddata, gradients, eddy-viscosity stresses, rescaling), bit for bit."""
+    from podsgen.prf import read_prf
+    g = np.load(os.path.join(golden_dir, "unit_read_prf.npz"))
+    path = tmp_path / "inlet.prf"
+    path.write_text(str(g["prf_text"]))
+    res = read_prf(str(path), 0.1, mdot, den, bulk, False, False)
+    for name, v in zip(("U", "V", "W", "uu", "vv", "ww", "uv", "uw", "vw"), res[:9]):
+        assert np.array_equal(np.asarray(v), g["%s_%s" % (tag, name)]), name
+    assert np.array_equal(np.array([float(x) for x in res[9:]]), g[tag + "_scalars"])
+
+
 def test_lund_rows_slab():
     import podsgen
     s = podsgen.DFSetup(jma=9, kma=5, ns=3)

@@ -8,7 +8,7 @@ import pytest
 from oracle import pods_oracle as O
 
 CASES = ["c1_32x32x64", "cli_10x11x5", "odd_12x9x17_aniso", "prf_8x12x9", "rot_6x7x6",
-         "dtanh_9x12x7", "circ_11x10x6", "ring_12x13x6"]
+         "dtanh_9x12x7", "circ_11x10x6", "ring_12x13x6", "readprf_case"]
 UNIT_2D = ["dtanh", "circ", "circ_odd", "ring", "ring_thin"]
 
 
@@ -28,6 +28,8 @@ def cfg_from(g):
         kw["mean_profile"] = str(g["cfg_mean_profile"])
     if "cfg_inner_d" in g.files:
         kw["inner_d"] = float(g["cfg_inner_d"])
+    if "cfg_ln_prf" in g.files:
+        kw["ln_prf"] = float(g["cfg_ln_prf"])
     return O.DFConfig(**kw)
 
 
