@@ -9,6 +9,7 @@ gen = E.Generator(s, device=0); snap = gen.generate()
 ctx = gen.ctx
 mean = torch.empty(snap.rowlen, dtype=torch.float64, device="cuda")
 podsgen.check(ctx.lib.pods_mean(ctx.h, E.ptr(mean), 1))
+podsgen.check(ctx.lib.pods_center(ctx.h))  # the production path: A centred in place
 C = torch.empty((NS, NS), dtype=torch.float64, device="cuda")
 flops = 3 * J * K * NS * (NS + 1)
 for r in range(reps):
