@@ -1266,7 +1266,7 @@ hipError_t launch_trd(const TrdArgs& a, int R, hipStream_t st) {
       break;
     case 16:
       PODS_TRD(16, 8, 0, 1, 2);
-      PODS_TRD(16, 8, 1, 1, 2);
+      PODS_TRD(16, 8, 1, 0, 2);
       PODS_TRD(16, 8, 2, 0, 2);
       PODS_TRD(16, 8, 3, 0, 1);
       PODS_TRD(16, 8, 4, 0, 0);
