@@ -38,7 +38,7 @@ def fct_welch(x, fs, N, iwindow):
             M += 1
         else:
             break
-    f = np.linspace(-N / 2, N / 2 - 1, N) / N * fs
+    f = np.linspace(-N // 2, N // 2 - 1, N) / N * fs   # Py2 int division: -N/2 == (-N)//2
     Sxx = np.zeros(N, dtype=np.complex64)
     Sxxsum = np.zeros(N, dtype=np.float64)
     for j in range(1, M + 1):

@@ -35,6 +35,8 @@ Functions executed from the reference (file:line):
   PODFS.py:1430-1447          sort_eigenvalues
   PODFS.py:1451-1464          calculate_correlation_matrix
   PODFS.py:1523-1659          fourier_coefficients (writes PODFS/PODFS.dat)
+  PODFS.py:1468-1482          write_temporal_modes (verbose output)
+  nsigproclib_no_mpi.py:10-68 fct_welch (verbose PSD of a temporal mode)
 
 main() (digitalfilters.py:1134-1510) and POD() (PODFS.py:1294-1393) are monolithic and
 reach VTK (make_inflow_plane, write_mean_field2); their glue lines (RNG draws, roll,
@@ -82,7 +84,10 @@ SEMANTIC_PATCHES["read_prf"] = [("(3/2)", "(3//2)")]
 DROP_LINES = {"read_prf": r"^(\s*)plt\.(contourf|close)\(.*$"}
 PROFILES_2D = ("double-hyperbolic-tangent", "circular-hyperbolic-tangent", "ring-hyperbolic-tangent")
 POD_FUNCS = ["write_eigenvalues", "sort_eigenvalues", "calculate_correlation_matrix",
-             "fourier_coefficients"]
+             "fourier_coefficients", "write_temporal_modes"]
+SIG_FUNCS = ["fct_welch"]
+# Python 2 integer division in the frequency axis (nsigproclib_no_mpi.py:53): -N/2 == (-N)//2
+SEMANTIC_PATCHES["fct_welch"] = [("np.linspace(-N/2,N/2-1,N)", "np.linspace(-N//2,N//2-1,N)")]
 
 
 def _translate(path):
@@ -113,9 +118,10 @@ def _extract(src, names):
 def load_reference():
     from scipy import interpolate
     ns = {"np": np, "scSig": scSig, "math": math, "Pi": np.pi, "linalg": np.linalg,
-          "interpolate": interpolate}
+          "interpolate": interpolate, "sys": sys}
     for path, names in ((os.path.join(REF, "digitalfilters.py"), DF_FUNCS),
-                        (os.path.join(REF, "PODFS.py"), POD_FUNCS)):
+                        (os.path.join(REF, "PODFS.py"), POD_FUNCS),
+                        (os.path.join(REF, "nsigproclib_no_mpi.py"), SIG_FUNCS)):
         funcs = _extract(_translate(path), names)
         for name, text in funcs.items():
             for old, new in SEMANTIC_PATCHES.get(name, []):
@@ -387,10 +393,43 @@ def unit_adapt2d(ref):
     return out
 
 
+def unit_verbose(ref):
+    """The verbose outputs: fct_welch on temporal-mode-like signals for
+    each window and odd/even block sizes, and write_temporal_modes' text for a small T."""
+    import contextlib
+    rs = np.random.RandomState(91)
+    out = {}
+    cases = [(64, 16, 1, 100.0), (64, 16, 2, 100.0), (64, 16, 3, 100.0), (101, 15, 2, 37.5),
+             (50, 50, 3, 2.0), (33, 8, 1, 10.0)]
+    with open(os.devnull, "w") as dn, contextlib.redirect_stdout(dn), warnings.catch_warnings():
+        warnings.simplefilter("ignore")                 # complex -> float64 in Sxxsum[:] = ...
+        for c, (n, N, iw, fs) in enumerate(cases):
+            x = rs.standard_normal(n) * np.sin(np.linspace(0.0, 7.0, n))
+            f, Sxx, M = ref["fct_welch"](x, fs, N, iw)
+            out["welch%d_cfg" % c] = np.array([n, N, iw, fs])
+            out["welch%d_x" % c] = x
+            out["welch%d_f" % c] = f
+            out["welch%d_Sxx" % c] = Sxx
+            out["welch%d_M" % c] = np.array(M)
+        T = rs.standard_normal((9, 4)) * np.array([3.0, 1.0, 1e-3, 1e5])
+        tmp = tempfile.mkdtemp()
+        try:
+            ref["write_temporal_modes"](3, 9, 0.0731, T, tmp + "/")
+            names = sorted(os.listdir(tmp))
+            out["tmodes_T"] = T
+            out["tmodes_names"] = np.array(names)
+            out["tmodes_text"] = np.array([open(os.path.join(tmp, n)).read() for n in names])
+        finally:
+            shutil.rmtree(tmp)
+    return out
+
+
 def main():
     only = set(sys.argv[1:])
     ref = load_reference()
     if only:
+        if "unit_verbose" in only:
+            np.savez_compressed(os.path.join(HERE, "unit_verbose.npz"), **unit_verbose(ref))
         if "unit_adapt2d" in only:
             np.savez_compressed(os.path.join(HERE, "unit_adapt2d.npz"), **unit_adapt2d(ref))
         if "unit_read_prf" in only:
@@ -419,6 +458,7 @@ def main():
     np.savez_compressed(os.path.join(HERE, "unit_adapt2d.npz"), **unit_adapt2d(ref))
     np.savez_compressed(os.path.join(HERE, "unit_read_prf.npz"), **unit_read_prf(ref))
     np.savez_compressed(os.path.join(HERE, "readprf_case.npz"), **prf_case(ref))
+    np.savez_compressed(os.path.join(HERE, "unit_verbose.npz"), **unit_verbose(ref))
     for name, kw in CASES.items():
         _write_case(ref, name, kw)
 

@@ -144,3 +144,30 @@ def test_prf_row_geometry_doc_example():
     pts = PODFS.cell_centres(10, 11, 0.1, (1.0, 0.0, 0.0), 0.0, (0.0, 0.0, 0.0))
     row = ",".join(fmt(v) for v in pts[0])
     assert row == "0.000000000000,-0.500000000000,0.550000011921"
+
+
+def test_verbose_outputs_match_reference(golden_dir, tmp_path):
+    """fct_welch (nsigproclib_no_mpi.py:10-68, every window, odd and even
+    block sizes) and write_temporal_modes (PODFS.py:1468-1482) against the reference's own
+    functions run by tests/golden/make_golden.py: identical arrays, identical file text."""
+    import warnings
+    import nsigproclib as sp
+    import PODFS
+    g = np.load(os.path.join(golden_dir, "unit_verbose.npz"))
+    ncase = 0
+    while "welch%d_cfg" % ncase in g.files:
+        n, N, iw, fs = g["welch%d_cfg" % ncase]
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            f, Sxx, M = sp.fct_welch(g["welch%d_x" % ncase], float(fs), int(N), int(iw))
+        assert M == int(g["welch%d_M" % ncase])
+        assert np.array_equal(f, g["welch%d_f" % ncase])
+        assert Sxx.dtype == g["welch%d_Sxx" % ncase].dtype
+        assert np.array_equal(Sxx, g["welch%d_Sxx" % ncase])
+        ncase += 1
+    assert ncase == 6
+    PODFS.write_temporal_modes(3, 9, 0.0731, g["tmodes_T"], str(tmp_path) + "/")
+    names = sorted(os.listdir(tmp_path))
+    assert names == [str(s) for s in g["tmodes_names"]]
+    for name, text in zip(names, g["tmodes_text"]):
+        assert open(os.path.join(tmp_path, name)).read() == str(text)
