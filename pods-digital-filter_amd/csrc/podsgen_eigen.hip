@@ -405,7 +405,6 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
       double dd[2] = {0.0, 0.0};
 #pragma unroll
       for (int m = 0; m < S; ++m) {
-        if (m >= K && m < K + SG) continue;         // slab columns are updated in the symv
         dd[0] = __builtin_fma(p[m], x[m], dd[0]);   // w_{j-1} . v_j
         dd[1] = __builtin_fma(vp[m], x[m], dd[1]);  // v_{j-1} . v_j
       }
@@ -416,13 +415,13 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
     // The lane holding column j+1 also publishes column j+1 of A^{(j)} (stored value minus
     // the pending rank-2 update) for its rows, from the values the symv loop just read.
     // (j+1 always lies in slot K during range K.)
-    // Slab slots (L2-resident, SG > 0) get the rank-2 update of step j-1 here, in the same
-    // pass that reads them (one read + one write per column, straight-line code so all the
-    // loads issue up front), and enter the row sums as A^{(j)}; the dlatrd corrections
-    // above cover the other columns only.
-    // slab loads run SPF row groups ahead (the publish stores in between would otherwise pin
-    // each load behind the previous group's stores and serialise the L2 round trips)
-    constexpr int SPF = K == 0 ? 0 : 3;  // range 0 has no registers to spare
+    // Slab slots (L2-resident, SG > 0) are only read here, like the on-chip slots (A^{(j-1)}
+    // plus the dlatrd corrections above); their rank-2 update joins the others after the
+    // publish, where it overlaps the next column's hop.  (Updating them here mixed stores
+    // into the loads, and a pending store makes every load wait a full vmcnt drain: one L2
+    // round trip per row group on the critical path.)
+    // slab loads run SPF row groups ahead
+    constexpr int SPF = K == 0 ? 0 : 3;  // range 0: no registers to spare (depth 2 measured no faster)
     double slab[SG > 0 ? RL : 1][SG > 0 ? SG : 1];
 #pragma unroll
     for (int ii = 0; ii < (SG > 0 ? SPF * RH : 0); ++ii)
@@ -435,32 +434,17 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
         if (ii < RL)
 #pragma unroll
           for (int m = K; m < K + SG; ++m) slab[ii][m - K] = wm(m, I0 + ii, t);
-      double acc[RH], colv[RH], vr[RH], wr[RH];
-      bool live[RH];
+      double acc[RH], colv[RH];
 #pragma unroll
-      for (int q = 0; q < RH; ++q) {
-        const int i = I0 + h * RH + q;
-        const int r = g + G * i;
-        live[q] = r >= j + 1 && r < n;
-        acc[q] = 0.0;
-        if (SG > 0) {
-          vr[q] = live[q] ? uniform(rsv[i]) : 0.0;
-          wr[q] = live[q] ? uniform(rsw[i]) : 0.0;
-        }
-      }
+      for (int q = 0; q < RH; ++q) acc[q] = 0.0;
 #pragma unroll
       for (int m = K; m < S; ++m) {
-        const int c = t + TT * m;
 #pragma unroll
         for (int q = 0; q < RH; ++q) {
           const int ii = h * RH + q;
           double val;
           if (m < K + SG) {
-            const double old = slab[ii][m - K];
-            const bool upd = live[q] && c >= j + 1;
-            const double nv = __builtin_fma(-vr[q], p[m], __builtin_fma(-wr[q], vp[m], old));
-            if (upd) wm(m, I0 + ii, t) = nv;
-            val = upd ? nv : 0.0;
+            val = slab[ii][m - K];
           } else if (m < K + SG + SL) {
             val = Al[((m - K - SG) * RL + ii) * TT + t];
           } else {
@@ -474,8 +458,7 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
 #pragma unroll
         for (int q = 0; q < RH; ++q) {
           const int i = I0 + h * RH + q;
-          rcol[i] = SG > 0 ? colv[q]
-                           : __builtin_fma(-rsv[i], p[K], __builtin_fma(-rsw[i], vp[K], colv[q]));
+          rcol[i] = __builtin_fma(-rsv[i], p[K], __builtin_fma(-rsw[i], vp[K], colv[q]));
         }
       }
       const double sum = rows_wave_sum(acc);
@@ -527,11 +510,13 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
         wr[q] = live[q] ? uniform(rsw[i]) : 0.0;
       }
 #pragma unroll
-      for (int m = K + SG; m < S; ++m) {  // slab slots were updated in the symv pass
+      for (int m = K; m < S; ++m) {
 #pragma unroll
         for (int q = 0; q < RH; ++q) {
           const int ii = h * RH + q;
           if (m < K + SG) {
+            double& ref = wm(m, I0 + ii, t);
+            ref = __builtin_fma(-vr[q], p[m], __builtin_fma(-wr[q], vp[m], ref));
           } else if (m < K + SG + SL) {
             double& ref = Al[((m - K - SG) * RL + ii) * TT + t];
             ref = __builtin_fma(-vr[q], p[m], __builtin_fma(-wr[q], vp[m], ref));
@@ -1244,7 +1229,10 @@ int trd_plan(int n, int* R, int* G, int64_t* slab_doubles) {
 
 // One launch per column range (k_trd header).  Storage split per range {SG, SL}: 16 rows
 // x 8 slots = 128 doubles/lane at range 0 do not fit VGPRs + LDS next to the vectors, so
-// two slots stay in the (L2-resident) slab there; later ranges hold everything on chip.
+// one slot stays in the (L2-resident) slab there; later ranges hold everything on chip.
+// Range 1 (14 rows x 7 slots) keeps all of it in VGPRs + LDS even though the compiler then
+// spills ~100 VGPRs of loop-invariant state: 5.43 ms against 6.25 ms with a slab slot,
+// whose mixed load/store traffic serialises every row group on a full vmcnt drain.
 hipError_t launch_trd(const TrdArgs& a, int R, hipStream_t st) {
   using namespace eig;
   hipError_t e = hipSuccess;
