@@ -218,7 +218,7 @@ struct pods_ctx {
   RngLayout layout;
   RngBuffers rng;
   DevBuf R, T1, A, mean, lund, taps, rot, prog_mean, prog_dft, tbuf, mag, lam, cwork, items, spwork, prog_rank;
-  DevBuf e_wm, e_x, e_flags, e_det, e_v, e_t, e_part, e_w2, e_inv;  // pods_syev workspace
+  DevBuf e_wm, e_x, e_flags, e_det, e_v, e_t, e_part, e_w2, e_inv, e_cnt;  // pods_syev workspace
   int e_G = 0;
   int nitems = 0;
   int64_t items_key = -1;
@@ -325,7 +325,7 @@ int pods_destroy(pods_ctx* c) {
   for (DevBuf* b : {&c->R, &c->T1, &c->A, &c->mean, &c->lund, &c->taps, &c->rot, &c->prog_mean,
                     &c->prog_dft, &c->tbuf, &c->mag, &c->lam, &c->cwork, &c->items, &c->e_wm,
                     &c->e_x, &c->e_flags, &c->e_det, &c->e_v, &c->e_t, &c->e_part, &c->e_w2,
-                    &c->e_inv, &c->spwork, &c->prog_rank, &c->zero})
+                    &c->e_inv, &c->e_cnt, &c->spwork, &c->prog_rank, &c->zero})
     release(*b);
   c->rng.free_all();
   delete c;
@@ -720,11 +720,16 @@ int pods_syev(pods_ctx* c, const double* C, int n, int nvec, double* lam_desc, d
   double* E = det + n;
   double* tau = det + 2 * (int64_t)n;
   double* bounds = det + 3 * (int64_t)n;
+  // All n eigenvalues start from brackets given by Sturm counts at 64 Ki shared shifts
+  // (k_sturm_grid, 0.16 ms): k_bisect 2.09 -> 1.41 ms.  PODS_BISECT_PLAIN=1 starts every
+  // eigenvalue from the Gershgorin interval instead.
   // (Bisecting the nvec wanted eigenvalues first and the rest on a side stream was measured
   // slower: each eigenvalue's bisection is latency bound (13 sequential n-step Sturm
   // passes), so the top nvec alone cost as much as all n, and the side launch slowed the
   // back-transformation kernels it shared CUs with.)
-  PODS_HIP(pods::launch_tri_eigvals(D, E, n, bounds, lam_desc, c->stream));
+  PODS_HIP(ensure(c->e_cnt, pods::tri_grid_bytes()));
+  int* gcnt = std::getenv("PODS_BISECT_PLAIN") ? nullptr : c->e_cnt.as<int>();
+  PODS_HIP(pods::launch_tri_eigvals(D, E, n, bounds, lam_desc, gcnt, c->stream));
   if (nvec > 0) {
     const int nblk = std::max((n - 1 + 63) / 64, 1);
     PODS_HIP(ensure(c->e_inv, (size_t)nvec * n * sizeof(double)));

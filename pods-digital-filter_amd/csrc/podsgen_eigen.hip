@@ -649,6 +649,52 @@ __device__ __forceinline__ void sturm_counts(const double2* __restrict__ de, int
   }
 }
 
+// Shared shifts for the first bracket of every eigenvalue: NSH spread uniformly over the
+// Gershgorin interval and NSH log-spaced over [2^-56.5, 1] * tnorm, where a POD spectrum
+// keeps most of its eigenvalues.  One Sturm count per shift (k_sturm_grid) brackets all n
+// eigenvalues at once; k_bisect then refines each from the tighter of its two brackets.
+constexpr int NSH = 32768;
+__device__ __forceinline__ double grid_shift(int s, double gl, double gu) {
+  if (s < NSH) return gl + (gu - gl) * ((double)(s + 1) / (double)(NSH + 1));
+  const double tn = fmax(fabs(gl), fabs(gu));
+  return tn * exp2(-56.5 * (double)(2 * NSH - 1 - s) / (double)NSH);  // ascending in s
+}
+
+__global__ __launch_bounds__(256) void k_sturm_grid(const double* __restrict__ D,
+                                                    const double* __restrict__ E, int n,
+                                                    const double* __restrict__ bounds,
+                                                    int* __restrict__ cnt) {
+  extern __shared__ double2 de[];
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const double e = i > 0 ? E[i - 1] : 0.0;
+    de[i] = make_double2(D[i], e * e);
+  }
+  __syncthreads();
+  const int s = blockIdx.x * 256 + threadIdx.x;
+  if (s >= 2 * NSH) return;
+  const double sig[1] = {grid_shift(s, bounds[0], bounds[1])};
+  int c[1];
+  sturm_counts<1>(de, n, sig, bounds[2], c);
+  cnt[s] = c[0];
+}
+
+// [lo, hi) from one shift family: the first shift with count >= k+1 and the one before it
+// (a binary search on the counts; both ends are tested, so count(lo) <= k < count(hi) holds
+// even where rounding makes the counts non-monotone).
+__device__ __forceinline__ void grid_bracket(const int* __restrict__ cnt, int base, int k, double gl,
+                                             double gu, double& lo, double& hi) {
+  int a = 0, b = NSH;
+  while (a < b) {
+    const int mid = (a + b) >> 1;
+    if (cnt[base + mid] >= k + 1)
+      b = mid;
+    else
+      a = mid + 1;
+  }
+  hi = a < NSH ? grid_shift(base + a, gl, gu) : DBL_MAX;
+  lo = a > 0 ? grid_shift(base + a - 1, gl, gu) : -DBL_MAX;
+}
+
 constexpr int BL = 16;  // lanes per eigenvalue
 constexpr int NCH = 1;  // shifts per lane: 16 shifts per step split the bracket into 17
 
@@ -658,7 +704,8 @@ constexpr int NCH = 1;  // shifts per lane: 16 shifts per step split the bracket
 __global__ __launch_bounds__(256) void k_bisect(const double* __restrict__ D,
                                                 const double* __restrict__ E, int n,
                                                 const double* __restrict__ bounds,
-                                                double* __restrict__ lam_desc, int k0, int k1) {
+                                                double* __restrict__ lam_desc, int k0, int k1,
+                                                const int* __restrict__ gcnt) {
   extern __shared__ double2 de[];
   const int t = threadIdx.x, lane = t & 63;
   for (int i = t; i < n; i += 256) {
@@ -671,6 +718,17 @@ __global__ __launch_bounds__(256) void k_bisect(const double* __restrict__ D,
   const int k = k0 + blockIdx.x * (256 / BL) + t / BL;  // ascending index, [k0, k1) this launch
   const bool active = k < k1;
   double lo = gl, hi = gu;
+  if (gcnt && active) {
+    double lu, hu, ll, hl;
+    grid_bracket(gcnt, 0, k, gl, gu, lu, hu);
+    grid_bracket(gcnt, NSH, k, gl, gu, ll, hl);
+    lo = fmax(gl, lu);
+    hi = fmin(gu, hu);
+    if (fmax(lo, ll) < fmin(hi, hl)) {
+      lo = fmax(lo, ll);
+      hi = fmin(hi, hl);
+    }
+  }
   for (int it = 0; it < 128; ++it) {
     const bool conv = !active || (hi - lo) <= fmax(atol, 2.0 * DBL_EPSILON * fmax(fabs(lo), fabs(hi)));
     if (__all(conv)) break;
@@ -1276,23 +1334,34 @@ hipError_t launch_tri_bounds(const double* D, const double* E, int n, double* bo
 // Eigenvalues with ascending indices [k0, k1) (written to lam_desc[n-1-k]); bounds from
 // launch_tri_bounds.
 hipError_t launch_tri_bisect(const double* D, const double* E, int n, const double* bounds,
-                             double* lam_desc, int k0, int k1, hipStream_t st) {
+                             double* lam_desc, int k0, int k1, int* grid_cnt, hipStream_t st) {
   if (k1 <= k0) return hipSuccess;
   const size_t lds = (size_t)n * sizeof(double2);
+  if (grid_cnt) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&eig::k_sturm_grid),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(eig::k_sturm_grid, dim3(2 * eig::NSH / 256), dim3(256), lds, st, D, E, n, bounds,
+                       grid_cnt);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&eig::k_bisect),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   const int per = 256 / eig::BL;
   hipLaunchKernelGGL(eig::k_bisect, dim3((k1 - k0 + per - 1) / per), dim3(256), lds, st, D, E, n,
-                     bounds, lam_desc, k0, k1);
+                     bounds, lam_desc, k0, k1, grid_cnt);
   return hipGetLastError();
 }
 
+size_t tri_grid_bytes() { return (size_t)2 * eig::NSH * sizeof(int); }
+
 hipError_t launch_tri_eigvals(const double* D, const double* E, int n, double* bounds,
-                              double* lam_desc, hipStream_t st) {
+                              double* lam_desc, int* grid_cnt, hipStream_t st) {
   hipError_t e = launch_tri_bounds(D, E, n, bounds, st);
   if (e != hipSuccess) return e;
-  return launch_tri_bisect(D, E, n, bounds, lam_desc, 0, n, st);
+  return launch_tri_bisect(D, E, n, bounds, lam_desc, 0, n, grid_cnt, st);
 }
 
 hipError_t launch_tri_eigvecs(const double* D, const double* E, int n, const double* lam_desc,

@@ -69,12 +69,14 @@ struct TrdArgs {
 int trd_plan(int n, int* R, int* G, int64_t* slab_doubles);
 hipError_t launch_trd(const TrdArgs& a, int R, hipStream_t st);
 // bounds: 4 doubles {gl, gu, pivmin, atol}; lam_desc: n eigenvalues of T, descending
+// grid_cnt (tri_grid_bytes(), may be null): counts at shared shifts for the first brackets
 hipError_t launch_tri_eigvals(const double* D, const double* E, int n, double* bounds,
-                              double* lam_desc, hipStream_t st);
+                              double* lam_desc, int* grid_cnt, hipStream_t st);
+size_t tri_grid_bytes();
 // the same in two parts: Gershgorin bounds, then the eigenvalues with ascending index [k0, k1)
 hipError_t launch_tri_bounds(const double* D, const double* E, int n, double* bounds, hipStream_t st);
 hipError_t launch_tri_bisect(const double* D, const double* E, int n, const double* bounds,
-                             double* lam_desc, int k0, int k1, hipStream_t st);
+                             double* lam_desc, int k0, int k1, int* grid_cnt, hipStream_t st);
 // Z: n x nvec row-major eigenvectors of T for lam_desc[0..nvec); X: nvec x n scratch
 hipError_t launch_tri_eigvecs(const double* D, const double* E, int n, const double* lam_desc,
                               const double* bounds, int nvec, double* X, double* Z, hipStream_t st);
