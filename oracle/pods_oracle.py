@@ -219,6 +219,28 @@ def adapt2d_point_coeffs(mean_profile, inner_d, uin, uuin, vvin, wwin, uwin, jma
     return tuple(co), um
 
 
+def read_profile(path, kma):
+    """read_profile (digitalfilters.py:487-522): columns y, U, uu, vv, ww, uv; the half-channel
+    rows are mirrored about y = 1 (uv changes sign), y normalised to [0, 1], each column
+    interpolated to kma points with an interpolating cubic spline, both walls set to zero."""
+    from scipy import interpolate
+    d = np.genfromtxt(path, names=True, autostrip=True, comments="#")
+    n = d.shape[0]
+    mirrored = d[0:n - 2][::-1]
+    d = np.concatenate([d, mirrored])
+    d["y"][n:] = (-(d["y"][n:] - 1.0) + 1)
+    d["uv"][n:] = -d["uv"][n:]
+    z = d["y"]
+    z = (z - np.min(z)) / (np.max(z) - np.min(z))
+    zi = np.linspace(np.min(z), np.max(z), kma)
+    out = []
+    for name in ("U", "uu", "vv", "ww", "uv"):
+        v = interpolate.splev(zi, interpolate.splrep(z, d[name], s=0), der=0)
+        v[0] = v[-1] = 0.
+        out.append(v)
+    return tuple(out)
+
+
 def rotation_matrix(nx, ny, nz):
     """prof_rotation_matrix, digitalfilters.py:1064-1116 (R = Ra(azimuth) . Rp(polar))."""
     n = np.sqrt(nx ** 2 + ny ** 2 + nz ** 2)
@@ -434,6 +456,7 @@ class DFConfig:
     mean_profile: str = "hyperbolic-tangent"   # -p (:1146); the 2-D ones go through adapt2d
     inner_d: float = 0.5                       # --ring (:1275)
     ln_prf: Optional[float] = None             # lnx from read_prf (:1301-1305)
+    profile1d: Optional[dict] = None           # U,uu,vv,ww,uw from read_profile (:1306-1307)
     # derived
     nfx: int = 0
     nfy: int = 0
@@ -455,7 +478,10 @@ class DFConfig:
         nrm = np.sqrt(n1[0] ** 2 + n1[1] ** 2 + n1[2] ** 2)
         self.n_unit = (n1[0] / nrm, n1[1] / nrm, n1[2] / nrm)
         V = W = 0
-        if self.prf is None:
+        if self.prf is None and self.profile1d is not None:
+            self.profile = {k: np.array(self.profile1d[k], dtype=np.float64) for k in ("U", "uu", "vv", "ww", "uw")}
+            U = self.profile["U"]
+        elif self.prf is None:
             U, uu, vv, ww, uw = build_profile(self.mean_profile, "top-hat",
                                               self.bulk_velocity, self.u_dash, self.kma)
             self.profile = dict(U=U, uu=uu, vv=vv, ww=ww, uw=uw)
@@ -491,7 +517,8 @@ class DFConfig:
 
     @property
     def rotated(self):
-        return self.prf is None
+        """main() rotates only when no profile file was given (profilefile == 'none', :1476)."""
+        return self.prf is None and self.profile1d is None
 
 
 def stream_plane_offset(cfg, c, p):
@@ -547,11 +574,9 @@ def lund_point_coeffs(cfg):
 
 def generate(cfg, loops=False, steps=None, stream=None):
     """Snapshot matrix A (3P, ns) before mean subtraction -- main() :1403-1477."""
-    J, K, P = cfg.jma, cfg.kma, cfg.P
+    P = cfg.P
     NX = 2 * cfg.nfx + 1
-    bx = calccoeff(cfg.nfx, cfg.lnx)
-    by = calccoeff(cfg.nfy, cfg.lny)
-    bz = calccoeff(cfg.nfz, cfg.lnz)
+    taps = _taps(cfg)
     ns = cfg.ns if steps is None else steps
     if stream is None:
         rs = np.random.RandomState(cfg.seed)
@@ -567,43 +592,109 @@ def generate(cfg, loops=False, steps=None, stream=None):
     Jp, Kp = cfg.plane_shape
     xs = [draw((NX, Jp, Kp)) for _ in range(3)]
     A = np.zeros((3 * P, ns), dtype=np.float64)
-    pr = cfg.profile
-    coeffs = None
-    R = rotation_matrix(*cfg.n_unit) if cfg.rotated else None
+    cache = {}
     for i in range(ns):
-        if loops:
-            ys = [filter_block_scipy(x, bx, by, bz) for x in xs]
-        else:
-            ys = [filter_block(x, bx, by, bz) for x in xs]
-        if cfg.prf is None and cfg.mean_profile in PROFILES_2D:   # main() :1447-1449
-            if coeffs is None:
-                coeffs = adapt2d_point_coeffs(cfg.mean_profile, cfg.inner_d, pr["U"], pr["uu"], pr["vv"],
-                                              pr["ww"], pr["uw"], J, K)
-            u, v, w = apply_lund(ys[0], ys[1], ys[2], coeffs[0], coeffs[1])
-        elif cfg.prf is None:
-            if loops:
-                adapt1d_loops(ys[0], ys[1], ys[2], pr["U"], pr["uu"], pr["vv"], pr["ww"], pr["uw"], J, K)
-                u, v, w = ys
-            else:
-                if coeffs is None:
-                    coeffs = [np.broadcast_to(c, (K,)) for c in
-                              lund1d_coeffs(pr["uu"], pr["vv"], pr["ww"], pr["uw"])]
-                u, v, w = apply_lund(ys[0], ys[1], ys[2], coeffs, pr["U"])
-        else:
-            if coeffs is None:
-                coeffs = lundprf_coeffs(pr["uu"], pr["vv"], pr["ww"], pr["uv"], pr["uw"], pr["vw"])
-            u, v, w = apply_lund(ys[0], ys[1], ys[2], coeffs, pr["U"], pr["V"], pr["W"])
+        col = _step_column(cfg, xs, taps, loops, cache)
         if i + 1 < ns:  # the draws after the final filter never reach A
             xs = [np.roll(x, -1, axis=0) for x in xs]
             for x in xs:
                 x[NX - 1] = draw((Jp, Kp))
-        A[0:P, i] = u.reshape(P)
-        A[P:2 * P, i] = v.reshape(P)
-        A[2 * P:3 * P, i] = w.reshape(P)
-        if R is not None:
-            if loops or not np.array_equal(R, np.eye(3)):
-                A[:, i] = rotate_velocity(A[:, i], R)
+        A[:, i] = col
     return A
+
+
+def _taps(cfg):
+    return calccoeff(cfg.nfx, cfg.lnx), calccoeff(cfg.nfy, cfg.lny), calccoeff(cfg.nfz, cfg.lnz)
+
+
+def _step_column(cfg, xs, taps, loops, cache):
+    """One pass of the step loop body (main() :1440-1477): filter the three components'
+    plane windows, Lund transform (adapt1d / adapt2d / adapt2prf), snapshot column, rotation."""
+    J, K, P = cfg.jma, cfg.kma, cfg.P
+    bx, by, bz = taps
+    pr = cfg.profile
+    if loops:
+        ys = [filter_block_scipy(x, bx, by, bz) for x in xs]
+    else:
+        ys = [filter_block(x, bx, by, bz) for x in xs]
+    if cfg.prf is None and cfg.mean_profile in PROFILES_2D:   # main() :1447-1449
+        if "c" not in cache:
+            cache["c"] = adapt2d_point_coeffs(cfg.mean_profile, cfg.inner_d, pr["U"], pr["uu"], pr["vv"],
+                                              pr["ww"], pr["uw"], J, K)
+        u, v, w = apply_lund(ys[0], ys[1], ys[2], cache["c"][0], cache["c"][1])
+    elif cfg.prf is None:
+        if loops:
+            adapt1d_loops(ys[0], ys[1], ys[2], pr["U"], pr["uu"], pr["vv"], pr["ww"], pr["uw"], J, K)
+            u, v, w = ys
+        else:
+            if "c" not in cache:
+                cache["c"] = [np.broadcast_to(c, (K,)) for c in
+                              lund1d_coeffs(pr["uu"], pr["vv"], pr["ww"], pr["uw"])]
+            u, v, w = apply_lund(ys[0], ys[1], ys[2], cache["c"], pr["U"])
+    else:
+        if "c" not in cache:
+            cache["c"] = lundprf_coeffs(pr["uu"], pr["vv"], pr["ww"], pr["uv"], pr["uw"], pr["vw"])
+        u, v, w = apply_lund(ys[0], ys[1], ys[2], cache["c"], pr["U"], pr["V"], pr["W"])
+    col = np.empty(3 * P)
+    col[0:P] = u.reshape(P)
+    col[P:2 * P] = v.reshape(P)
+    col[2 * P:3 * P] = w.reshape(P)
+    if cfg.rotated:
+        if "R" not in cache:
+            cache["R"] = rotation_matrix(*cfg.n_unit)
+        R = cache["R"]
+        if loops or not np.array_equal(R, np.eye(3)):
+            col = rotate_velocity(col, R)
+    return col
+
+
+def generate_steps(cfg, steps, chunk=1 << 24):
+    """Columns A[:, i] for the listed steps only, at any size: the planes step i filters
+    (planes i..i+2nfx of each component, stream_plane_offset) are cut out of ONE sequential
+    pass over the reference's draw stream (drawn in chunks and discarded), so late steps of a
+    4096-step run cost one pass over ~0.9 G doubles instead of the whole step loop.
+    Returns {step: column (3P,)}, each equal to generate(cfg)[:, step]."""
+    NX = 2 * cfg.nfx + 1
+    S = cfg.S
+    Jp, Kp = cfg.plane_shape
+    want = {}
+    for i in steps:
+        for c in range(3):
+            for p in range(i, i + NX):
+                want[stream_plane_offset(cfg, c, p)] = None
+    starts = sorted(want)
+    rs = np.random.RandomState(cfg.seed)
+    pos = 0
+    k = 0
+    buf = np.empty(0)
+    buf0 = 0
+    while k < len(starts):
+        need_end = starts[k] + S
+        if buf0 + len(buf) < need_end:  # extend the window: keep the tail from starts[k]
+            keep = buf[max(starts[k] - buf0, 0):] if starts[k] < buf0 + len(buf) else np.empty(0)
+            if starts[k] >= buf0 + len(buf):  # skip ahead (draw and discard)
+                while pos < starts[k]:
+                    n = min(chunk, starts[k] - pos)
+                    rs.uniform(low=-SQRT3, high=SQRT3, size=n)
+                    pos += n
+                keep_start = pos
+            else:
+                keep_start = max(starts[k], buf0)
+            n = max(chunk, need_end - pos)
+            new = rs.uniform(low=-SQRT3, high=SQRT3, size=n)
+            buf = np.concatenate([keep, new])
+            buf0 = keep_start
+            pos += n
+        o = starts[k] - buf0
+        want[starts[k]] = buf[o:o + S].reshape(Jp, Kp).copy()
+        k += 1
+    taps = _taps(cfg)
+    out = {}
+    cache = {}
+    for i in steps:
+        xs = [np.stack([want[stream_plane_offset(cfg, c, p)] for p in range(i, i + NX)]) for c in range(3)]
+        out[i] = _step_column(cfg, xs, taps, False, cache)
+    return out
 
 
 def mean_and_center(A):
@@ -779,7 +870,7 @@ def eigenvalues_text(num_valid, ns, energy):
     total = cum[num_valid - 1]
     out = ["#\n",
            "# mode, energy, cumulative, percenterage energy, percentage cumulative, condition number (absolute value if negative)\n",
-           "#           Note: cummulative energies are set to zero after first negative energy",
+           "#\t\tNote: cummulative energies are set to zero after first negative energy",
            "#\n"]
     for i in range(num_valid):
         out.append("%4.1d %18.10e %18.10e %18.10e %18.10e %18.10e\n" % (

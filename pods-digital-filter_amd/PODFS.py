@@ -192,7 +192,7 @@ def write_eigenvalues(num_valid_modes, num_snapshots, energy, filename):
     with open(filename, "w") as f:
         f.write("#\n")
         f.write("# mode, energy, cumulative, percenterage energy, percentage cumulative, condition number (absolute value if negative)\n")
-        f.write("#           Note: cummulative energies are set to zero after first negative energy")
+        f.write("#\t\tNote: cummulative energies are set to zero after first negative energy")
         f.write("#\n")
         for i in range(num_valid_modes):
             f.write("%4.1d %18.10e %18.10e %18.10e %18.10e %18.10e\n" % (
@@ -240,7 +240,10 @@ def POD(A, num_snapshots, num_points, num_components, correct_for_cell_volumes, 
         os.makedirs(restart_dir, exist_ok=True)
         write_eigenvalues(res.num_valid, num_snapshots, res.energy, restart_dir + "POD.eigenvalues.dat")
     T = res.T.cpu().numpy() if res.T is not None else None
-    if getattr(i_d, "verbose", False) and T is not None and restart_dir:
+    rank0 = dist is None or not dist.is_initialized() or dist.get_rank() == 0
+    # verbose temporal modes (:1352-1356): rank 0 holds the full (ns, ns) T; the others only
+    # the broadcast T[:, :nm]
+    if getattr(i_d, "verbose", False) and T is not None and restart_dir and rank0:
         write_temporal_modes(res.num_valid, num_snapshots, dt, T, restart_dir)
     i_d.temporal_modes = T
     i_d.spatial_modes = res.phi.cpu().numpy()
@@ -351,8 +354,10 @@ def pod2prf(i_d):
     if i_d.hdf5:
         i_d.mean[:, 0:3] = points
         i_d.mean[:, 3:] = u
-    t_o = getattr(i_d, "t_o", (0, 0, 0))
-    rhs = (0 + t_o[0]) * n[0] + (0 + t_o[1]) * n[1] + (0 + t_o[2]) * n[2]
+    # the reference resets the translation before writing (PODFS.py:1669), so the plane
+    # rhs of PODFS_mean.prf is (0+0)*n1 + (0+0)*n2 + (0+0)*n3 (:1717) whatever --ox/--oy/--oz
+    i_d.t_o = np.array([0, 0, 0])
+    rhs = (0 + i_d.t_o[0]) * n[0] + (0 + i_d.t_o[1]) * n[1] + (0 + i_d.t_o[2]) * n[2]
     with open(rdir + "PODFS_mean.prf", "w") as f:
         f.write(_prf_header("PODFS_mean", n, rhs))
         f.write(_prf_rows(points, u))

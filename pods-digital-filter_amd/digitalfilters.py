@@ -347,18 +347,23 @@ def main(argv=None):
     gen = _E.Generator(s, device=local, rank=rank, world=world)
     i_d._pods_ctx = gen.ctx
     snap = gen.generate()  # main() step loop :1403-1477 as one device pass
-    if options.verbose and world == 1:
+    if options.verbose:  # per-step snapshot planes (:1479-1481), written by rank 0
         A = snap.to_host()
-        for i in range(s.ns):
-            i_d.time = i * s.dt_eff
-            save_plane(A[:, i], i_d)
+        if world > 1:
+            A = gather_row_slabs(dist, s, A)
+        if rank == 0:
+            for i in range(s.ns):
+                i_d.time = i * s.dt_eff
+                save_plane(A[:, i], i_d)
+        del A
     nmw = s.nm if options.verbose else 0
     pod_res = pod.POD(snap, s.ns, s.P, 3, "false", [], "PODFS/", "false", 1.0e-15, s.nm, nmw, "false",
                       "false", i_d.grid, None, s.dt_eff, "velocity", 1, s.ns, 1, 1, i_d,
                       dist=dist if world > 1 else None)
     mean_local = pod_res.mean.cpu().numpy()
     if world > 1:
-        mean_field, spatial = _gather_slabs(dist, s, gen, mean_local, i_d.spatial_modes)
+        both = gather_row_slabs(dist, s, np.concatenate([mean_local[:, None], i_d.spatial_modes], axis=1))
+        mean_field, spatial = (both[:, 0].copy(), both[:, 1:].copy()) if rank == 0 else (None, None)
     else:
         mean_field, spatial = mean_local, i_d.spatial_modes
     i_d.mean_field = mean_field
@@ -373,23 +378,39 @@ def main(argv=None):
     return i_d
 
 
-def _gather_slabs(dist, s, gen, mean_local, phi_local):
-    """Reassemble [u(P); v(P); w(P)] rows from the row slabs of every rank (rank 0)."""
+def gather_row_slabs(dist, s, local):
+    """Reassemble rows [u(P); v(P); w(P)] of a per-rank array from the row slabs of every rank
+    onto rank 0 (one tensor gather; other ranks get None).
+
+    local: (3*(j1-j0)*kma, m) rows of this rank's slab (host).  Slabs are sized by
+    host.row_slab, so every rank knows every slab's row count; they are zero-padded to the
+    largest for the gather.  nccl gathers device tensors, gloo host tensors."""
     import torch
-    world = dist.get_world_size()
-    K, nm = s.kma, phi_local.shape[1]
-    parts = [None] * world
-    dist.all_gather_object(parts, (gen.j0, gen.j1, mean_local, phi_local))
-    P = s.P
-    mean = np.zeros(3 * P)
-    phi = np.zeros((3 * P, nm))
-    for j0, j1, m, f in parts:
+    world, rank = dist.get_world_size(), dist.get_rank()
+    K, P = s.kma, s.P
+    local = np.asarray(local, dtype=np.float64)
+    squeeze = local.ndim == 1
+    if squeeze:
+        local = local[:, None]
+    m = local.shape[1]
+    slabs = [_H.row_slab(s.jma, r, world) for r in range(world)]
+    rows = [3 * (j1 - j0) * K for j0, j1 in slabs]
+    if local.shape[0] != rows[rank]:
+        raise ValueError("rank %d holds %d rows, its slab has %d" % (rank, local.shape[0], rows[rank]))
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    buf = torch.zeros((max(rows), m), dtype=torch.float64, device=dev)
+    buf[:rows[rank]] = torch.from_numpy(local).to(dev)
+    parts = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, parts, dst=0)
+    if rank != 0:
+        return None
+    out = np.zeros((3 * P, m))
+    for (j0, j1), n, t in zip(slabs, rows, parts):
+        f = t[:n].cpu().numpy()
         pl = (j1 - j0) * K
         for c in range(3):
-            mean[c * P + j0 * K:c * P + j1 * K] = m[c * pl:(c + 1) * pl]
-            phi[c * P + j0 * K:c * P + j1 * K] = f[c * pl:(c + 1) * pl]
-    del torch
-    return mean, phi
+            out[c * P + j0 * K:c * P + j1 * K] = f[c * pl:(c + 1) * pl]
+    return out[:, 0] if squeeze else out
 
 
 if __name__ == "__main__":

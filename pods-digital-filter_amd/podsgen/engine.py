@@ -164,6 +164,35 @@ def _dist_info(dist):
     return dist, dist.get_rank(), dist.get_world_size()
 
 
+_TRIL = {}
+
+
+def _tril_index(n, device):
+    """Linear indices of the lower triangle (with the diagonal) of an n x n row-major matrix,
+    and of the mirrored upper-triangle positions, cached per (n, device)."""
+    key = (n, str(device))
+    if key not in _TRIL:
+        r, c = torch.tril_indices(n, n, device=device)
+        _TRIL[key] = (r * n + c, c * n + r)
+    return _TRIL[key]
+
+
+def allreduce_correlation(dist, C, ns, divide):
+    """Sum the ranks' partial correlations C_g = A_g^T A_g (row slabs) and divide by ns
+    (PODFS.py:1455, np.dot(A.T, A)/ns): ONE all_reduce of the packed lower triangle
+    (ns(ns+1)/2 doubles, half of C) over RCCL/xGMI, then divide(packed, ns) and unpack into
+    both triangles, so C stays exactly symmetric.  divide is the device division
+    (pods_divide_inplace: x / ns, IEEE-rounded like numpy's)."""
+    lo, up = _tril_index(ns, C.device)
+    flat = C.view(-1)
+    packed = flat.index_select(0, lo)
+    dist.all_reduce(packed)
+    divide(packed, ns)
+    flat[lo] = packed
+    flat[up] = packed
+    return C
+
+
 SYEV_MAX_N = 4096   # pods_syev's on-chip limit (trd_plan)
 SYEV_MAX_VEC = 64
 
@@ -237,8 +266,9 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
         check(lib.pods_corr(ctx.h, ptr(C), 1 if world == 1 else 0), "pods_corr")
     if world > 1:
         with tm("allreduce"):
-            dist.all_reduce(C)
-            check(lib.pods_divide_inplace(ctx.h, ptr(C), ns * ns, float(ns)), "pods_divide_inplace")
+            def divide(x, d):
+                check(lib.pods_divide_inplace(ctx.h, ptr(x), x.numel(), float(d)), "pods_divide_inplace")
+            allreduce_correlation(dist, C, ns, divide)
     meta = torch.zeros(4, dtype=torch.int64, device=dev)
     lam_desc_t = torch.empty(ns, dtype=torch.float64, device=dev)
     T = None

@@ -13,7 +13,8 @@ The reference (sidbannet/PODS-digital-filter) is Python 2 and cannot be imported
 this interpreter (mixed tabs, print statements).  We therefore
 
   1. read digitalfilters.py / PODFS.py as text and apply Python 2's tab rule
-     (expandtabs(8));
+     (tabs -> next multiple of 8) to the leading indentation only, so tabs inside
+     string literals survive (PODFS.py:1421 writes '#\\t\\tNote');
   2. run lib2to3 over the module text (print/except/zip/... fixers);
   3. parse the result with `ast` and pull out ONLY the pure numpy/scipy functions on
      the hot path -- no module-level imports of vtk/h5py/matplotlib are executed, and
@@ -46,9 +47,11 @@ are replayed below line by line with the same numpy calls, each citing its line.
 Run:  python tests/golden/make_golden.py      (writes tests/golden/*.npz, *.dat)
 """
 import ast
+import contextlib
 import io
 import math
 import os
+import re
 import shutil
 import sys
 import tempfile
@@ -76,7 +79,7 @@ SEMANTIC_PATCHES = {
 }
 
 DF_FUNCS = ["calccoeff", "filter3DSciPy1D", "adapt1d", "adapt2prf", "adapt2d", "build_profile",
-            "prof_rotation_matrix", "rotate_velocity", "read_prf"]
+            "prof_rotation_matrix", "rotate_velocity", "read_prf", "read_profile"]
 # read_prf (digitalfilters.py:524-1035): Python 2 `3/2 == 1` (:758, :767, :779, :788), and its
 # nplotlib contour plots (:851-872, :1011-1022; VTK/matplotlib, side effects only) dropped
 # line by line (regex below) -- nothing they draw feeds the returned profile.
@@ -84,16 +87,58 @@ SEMANTIC_PATCHES["read_prf"] = [("(3/2)", "(3//2)")]
 DROP_LINES = {"read_prf": r"^(\s*)plt\.(contourf|close)\(.*$"}
 PROFILES_2D = ("double-hyperbolic-tangent", "circular-hyperbolic-tangent", "ring-hyperbolic-tangent")
 POD_FUNCS = ["write_eigenvalues", "sort_eigenvalues", "calculate_correlation_matrix",
-             "fourier_coefficients", "write_temporal_modes"]
+             "fourier_coefficients", "write_temporal_modes", "save_plane"]
+# save_plane (PODFS.py:854-887): its VTK cell-centre lookup (:856-861) is the only VTK use;
+# the points are handed in instead (VTK geometry -> given/analytic points).
+SEMANTIC_PATCHES["save_plane"] = [
+    ("cc = vtk.vtkCellCenters()", "pass"),
+    ("cc.SetInputData(i_d.grid)", "pass"),
+    ("cc.VertexCellsOn()", "pass"),
+    ("cc.Update()", "pass"),
+    ("points = VN.vtk_to_numpy(cc.GetOutput().GetPoints().GetData())", "points = i_d.grid_points"),
+    ("npt = cc.GetOutput().GetNumberOfPoints()", "npt = points.shape[0]"),
+]
 SIG_FUNCS = ["fct_welch"]
+# nsigproclib_no_mpi.str (:880-882, '%0.12f') -- kept in its own namespace `sp` (PODFS.py
+# imports the module as sp), so the builtin str the writers also call is not shadowed.
+SP_FUNCS = ["str"]
 # Python 2 integer division in the frequency axis (nsigproclib_no_mpi.py:53): -N/2 == (-N)//2
 SEMANTIC_PATCHES["fct_welch"] = [("np.linspace(-N/2,N/2-1,N)", "np.linspace(-N//2,N//2-1,N)")]
+
+
+def _expand_indentation(text):
+    """Python 2's tab rule (tabs to the next multiple of 8) applied to the leading
+    indentation of each logical line only.  Tabs inside string literals (e.g. the
+    '#\\t\\tNote' header of PODFS.py:1421) and inside triple-quoted blocks are kept."""
+    out = []
+    in_triple = None
+    for line in text.splitlines(keepends=True):
+        if in_triple is None:
+            m = re.match(r"[ \t]*", line)
+            line = m.group(0).expandtabs(8) + line[m.end():]
+        # track triple-quoted blocks opened/closed on this line (the reference's docstrings)
+        pos = 0
+        while True:
+            if in_triple is None:
+                hits = [(line.find(q, pos), q) for q in ('"""', "'''")]
+                hits = [h for h in hits if h[0] >= 0]
+                if not hits:
+                    break
+                at, q = min(hits)
+                in_triple, pos = q, at + 3
+            else:
+                at = line.find(in_triple, pos)
+                if at < 0:
+                    break
+                in_triple, pos = None, at + 3
+        out.append(line)
+    return "".join(out)
 
 
 def _translate(path):
     from lib2to3 import refactor
     with open(path, "r") as f:
-        src = f.read().expandtabs(8)
+        src = _expand_indentation(f.read())
     if not src.endswith("\n"):
         src += "\n"
     fixers = refactor.get_fixers_from_package("lib2to3.fixes")
@@ -119,6 +164,11 @@ def load_reference():
     from scipy import interpolate
     ns = {"np": np, "scSig": scSig, "math": math, "Pi": np.pi, "linalg": np.linalg,
           "interpolate": interpolate, "sys": sys}
+    sp_ns = {"np": np}
+    ns["sp"] = type("sp", (), {})
+    for name, text in _extract(_translate(os.path.join(REF, "nsigproclib_no_mpi.py")), SP_FUNCS).items():
+        exec(compile(text, "<reference:sp.%s>" % name, "exec"), sp_ns)
+        setattr(ns["sp"], name, staticmethod(sp_ns[name]))
     for path, names in ((os.path.join(REF, "digitalfilters.py"), DF_FUNCS),
                         (os.path.join(REF, "PODFS.py"), POD_FUNCS),
                         (os.path.join(REF, "nsigproclib_no_mpi.py"), SIG_FUNCS)):
@@ -142,7 +192,8 @@ class Obj(object):
 def run_reference_pipeline(ref, *, jma, kma, ns, seed, lengthscale=3.0, fwidth=2.0, dt=0.0,
                            res=0.1, bulk_velocity=1.0, u_dash=0.02, nm=20, et=0.9,
                            normal=(1.0, 0.0, 0.0), prf=None, workdir=None,
-                           mean_profile="hyperbolic-tangent", inner_d=0.5, ln_prf=None):
+                           mean_profile="hyperbolic-tangent", inner_d=0.5, ln_prf=None,
+                           profile_text=None):
     """Replay digitalfilters.py main() (:1244-1510) + PODFS.POD (:1294-1393) with the
     reference's own functions.  prf=None -> built profile (adapt1d, or adapt2d for the 2-D
     mean profiles, + rotation); prf=dict(U,V,W,uu,vv,ww,uv,uw,vw) of (jma,kma) arrays ->
@@ -159,7 +210,16 @@ def run_reference_pipeline(ref, *, jma, kma, ns, seed, lengthscale=3.0, fwidth=2
     ny = n1[1] / np.sqrt(n1[0]**2 + n1[1]**2 + n1[2]**2)
     nz = n1[2] / np.sqrt(n1[0]**2 + n1[1]**2 + n1[2]**2)
     V = W = 0
-    if prf is None:
+    if profile_text is not None:                          # :1306-1307 (-P profile.dat)
+        pdir = tempfile.mkdtemp(prefix="pods_profile_")
+        try:
+            with open(os.path.join(pdir, "profile.dat"), "w") as f:
+                f.write(profile_text)
+            with contextlib.redirect_stdout(io.StringIO()):
+                U, uu, vv, ww, uw = ref["read_profile"](os.path.join(pdir, "profile.dat"), kma)
+        finally:
+            shutil.rmtree(pdir)
+    elif prf is None:
         U, uu, vv, ww, uw = ref["build_profile"](mean_profile, "top-hat",
                                                  bulk_velocity, u_dash, kma)      # :1305
     else:
@@ -206,7 +266,7 @@ def run_reference_pipeline(ref, *, jma, kma, ns, seed, lengthscale=3.0, fwidth=2
         A[0:jma*kma, i] = yu.reshape(jma*kma)             # :1471-1473
         A[jma*kma:2*jma*kma, i] = yv.reshape(jma*kma)
         A[2*jma*kma:3*jma*kma, i] = yw.reshape(jma*kma)
-        if prf is None:                                   # :1476-1477
+        if prf is None and profile_text is None:          # :1476-1477 (profilefile == 'none')
             A[:, i] = ref["rotate_velocity"](A[:, i], nx, ny, nz)
     out["A_raw"] = A.copy()
     out["filtered_first_steps"] = np.stack(filt)
@@ -306,7 +366,14 @@ CASES = {
     "circ_11x10x6": dict(jma=11, kma=10, ns=6, seed=22, mean_profile="circular-hyperbolic-tangent",
                          normal=(1.0, 0.5, -0.25)),
     "ring_12x13x6": dict(jma=12, kma=13, ns=6, seed=23, mean_profile="ring-hyperbolic-tangent", inner_d=0.3),
+    # -P profile.dat: read_profile (:487-522) -> adapt1d, no rotation (:1476), clamps (:1344-1350)
+    "prof1d_14x16x8": dict(jma=14, kma=16, ns=8, seed=41, normal=(1.0, 0.3, 0.0), profile_text="synthetic"),
+    # mid-size: three 256-row SYRK blocks with split K, the split snapshot axis of the
+    # spatial-mode pass (ks = 4), DFT/ranking at ns = 520.  Stored reduced (no A_raw / full C).
+    "mid_40x40x520": dict(jma=40, kma=40, ns=520, seed=97, reduced=True),
 }
+MID_STEPS = [0, 1, 255, 256, 518, 519]          # A_raw columns kept for the reduced case
+MID_C_ROWS = [0, 1, 255, 256, 257, 300, 511, 512, 519]
 
 
 def write_synthetic_prf(path, seed=5):
@@ -393,6 +460,77 @@ def unit_adapt2d(ref):
     return out
 
 
+def synthetic_profile_text(npts=15):
+    """A 1-D channel profile file for read_profile (digitalfilters.py:487-522): columns
+    y U uu vv ww uv over the lower half channel y in [0, 1] (mirrored by the reader).  The
+    wall-normal stresses are steep at the wall so the spline overshoots below zero and
+    main()'s clamps (:1344-1350) are exercised."""
+    y = np.linspace(0.0, 1.0, npts)
+    U = np.tanh(6.0 * y) * (1.0 + 0.1 * y)
+    uu = 4e-3 * np.exp(-4.0 * y) * np.tanh(30.0 * y) ** 2
+    vv = 1e-3 * (1.0 - np.exp(-8.0 * y)) * (1.2 - y)
+    ww = 2e-3 * np.tanh(12.0 * y) * (1.1 - 0.5 * y)
+    uv = -1.5e-3 * np.tanh(9.0 * y) * (1.0 - y)
+    lines = ["# y U uu vv ww uv"]
+    for r in zip(y, U, uu, vv, ww, uv):
+        lines.append(" ".join("%.10e" % v for v in r))
+    return "\n".join(lines) + "\n"
+
+
+def unit_read_profile(ref):
+    """read_profile (digitalfilters.py:487-522) on the synthetic file at a few kma."""
+    out = {"text": np.array(synthetic_profile_text())}
+    d = tempfile.mkdtemp(prefix="pods_profile_")
+    try:
+        path = os.path.join(d, "profile.dat")
+        with open(path, "w") as f:
+            f.write(str(out["text"]))
+        for kma in (17, 32, 64):
+            with contextlib.redirect_stdout(io.StringIO()):
+                res = ref["read_profile"](path, kma)
+            out["k%d" % kma] = np.stack(res)
+    finally:
+        shutil.rmtree(d)
+    return out
+
+
+def unit_save_plane(ref):
+    """save_plane (PODFS.py:854-887), the verbose per-step snapshot .prf: file name from
+    i_d.time ('%.5E'), header with the plane normal and rhs, rows '%0.12f'."""
+    rs = np.random.RandomState(17)
+    out = {}
+    cases = [((1.0, 0.0, 0.0), (0.0, 0.0, 0.0), 0.0), ((1.0, 0.0, 0.0), (0.5, 0.0, 0.0), 0.0731),
+             ((0.6, -0.48, 0.64), (0.25, -1.5, 2.0), 12.5)]
+    for c, (n, t_o, tm) in enumerate(cases):
+        npt = 7 + 3 * c
+        pts = rs.standard_normal((npt, 3)).astype(np.float32).astype(np.float64)
+        u = rs.standard_normal(3 * npt) * 10.0 ** rs.randint(-3, 2, 3 * npt)
+        i_d = Obj()
+        i_d.grid_points = pts
+        i_d.n = [np.float64(v) for v in n]
+        i_d.t_o = [float(v) for v in t_o]
+        i_d.time = tm
+        d = tempfile.mkdtemp(prefix="pods_plane_")
+        cwd = os.getcwd()
+        try:
+            os.chdir(d)
+            os.makedirs("PODFS")
+            ref["save_plane"](u, i_d)
+            names = os.listdir("PODFS")
+            assert len(names) == 1
+            out["plane%d_name" % c] = np.array(names[0])
+            out["plane%d_text" % c] = np.array(open(os.path.join("PODFS", names[0])).read())
+        finally:
+            os.chdir(cwd)
+            shutil.rmtree(d)
+        out["plane%d_points" % c] = pts
+        out["plane%d_u" % c] = u
+        out["plane%d_n" % c] = np.array(n)
+        out["plane%d_t_o" % c] = np.array(t_o)
+        out["plane%d_time" % c] = np.array(tm)
+    return out
+
+
 def unit_verbose(ref):
     """The verbose outputs: fct_welch on temporal-mode-like signals for
     each window and odd/even block sizes, and write_temporal_modes' text for a small T."""
@@ -428,6 +566,10 @@ def main():
     only = set(sys.argv[1:])
     ref = load_reference()
     if only:
+        if "unit_read_profile" in only:
+            np.savez_compressed(os.path.join(HERE, "unit_read_profile.npz"), **unit_read_profile(ref))
+        if "unit_save_plane" in only:
+            np.savez_compressed(os.path.join(HERE, "unit_save_plane.npz"), **unit_save_plane(ref))
         if "unit_verbose" in only:
             np.savez_compressed(os.path.join(HERE, "unit_verbose.npz"), **unit_verbose(ref))
         if "unit_adapt2d" in only:
@@ -459,18 +601,33 @@ def main():
     np.savez_compressed(os.path.join(HERE, "unit_read_prf.npz"), **unit_read_prf(ref))
     np.savez_compressed(os.path.join(HERE, "readprf_case.npz"), **prf_case(ref))
     np.savez_compressed(os.path.join(HERE, "unit_verbose.npz"), **unit_verbose(ref))
+    np.savez_compressed(os.path.join(HERE, "unit_read_profile.npz"), **unit_read_profile(ref))
+    np.savez_compressed(os.path.join(HERE, "unit_save_plane.npz"), **unit_save_plane(ref))
     for name, kw in CASES.items():
         _write_case(ref, name, kw)
 
 
 def _write_case(ref, name, kw):
     kw = dict(kw)
+    reduced = kw.pop("reduced", False)
     if kw.get("prf") == "synthetic":
         kw["prf"] = synthetic_prf(kw["jma"], kw["kma"], kw["seed"])
         extra = {"prf_" + k: v for k, v in kw["prf"].items()}
     else:
         extra = {}
+    if kw.get("profile_text") == "synthetic":
+        kw["profile_text"] = synthetic_profile_text()
     res = run_reference_pipeline(ref, **kw)
+    if reduced:  # keep the fixture small: sampled columns/rows plus checksums
+        A, C = res.pop("A_raw"), res.pop("C")
+        res.pop("filtered_first_steps")
+        res["A_steps"] = np.array(MID_STEPS)
+        res["A_cols"] = A[:, MID_STEPS].T.copy()
+        res["C_rows_idx"] = np.array(MID_C_ROWS)
+        res["C_rows"] = C[MID_C_ROWS].copy()
+        res["C_diag"] = np.diag(C).copy()
+        res["C_max"] = np.array(np.max(np.abs(C)))
+        res["C_colsum"] = C.sum(axis=0)
     meta = {k: np.array(v) for k, v in kw.items() if k != "prf"}
     res.update({"cfg_" + k: v for k, v in meta.items()})
     res.update(extra)

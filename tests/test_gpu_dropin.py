@@ -166,9 +166,75 @@ def test_sharded_pipeline_two_ranks_one_device():
         for comp in range(3):
             rows = slice(comp * P + d["j0"] * K, comp * P + d["j1"] * K)
             assert np.array_equal(d["mean"][comp * pl:(comp + 1) * pl], mean[rows])
-            for m in range(pod.nm):
+    # signed modes: ONE sign per mode for the whole field (the eigenvector's), taken from
+    # rank 0's slab; every slab must then agree with that sign -- a per-slab sign error fails
+    for m in range(pod.nm):
+        d0 = out[0]
+        pl0 = (d0["j1"] - d0["j0"]) * K
+        rows0 = slice(d0["j0"] * K, d0["j1"] * K)
+        sg = np.sign(np.dot(d0["phi"][:pl0, m], phi[rows0, m]))
+        assert sg != 0
+        for r in range(2):
+            d = out[r]
+            pl = (d["j1"] - d["j0"]) * K
+            for comp in range(3):
+                rows = slice(comp * P + d["j0"] * K, comp * P + d["j1"] * K)
                 a = d["phi"][comp * pl:(comp + 1) * pl, m]
-                b = phi[rows, m]
-                sg = np.sign(np.dot(phi[:, m], phi[:, m]))  # same sign convention on both runs?
-                assert np.max(np.abs(np.abs(a) - np.abs(b))) <= 1e-10 * np.max(np.abs(phi[:, m])) * sg
-    assert np.max(np.abs(np.abs(out[0]["c"]) - np.abs(fo.c))) <= 1e-6 * np.max(np.abs(fo.c))
+                assert np.max(np.abs(sg * a - phi[rows, m])) <= 1e-10 * np.max(np.abs(phi[:, m])), (r, comp, m)
+        c_sg = sg
+        assert np.max(np.abs(c_sg * out[0]["c"][:, m] - fo.c[:, m])) <= 1e-6 * np.max(np.abs(fo.c[:, m]))
+
+
+def _verbose_worker(rank, world, port, wdir, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK="0")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.chdir(wdir)
+    import digitalfilters as df
+    i_d = df.main(["-n", "6", "--seed", "19", "-j", "9", "-k", "8", "-v"])
+    out[rank] = dict(nm=i_d.nm, mean=None if rank else i_d.mean_field)
+    dist.destroy_process_group()
+
+
+def test_verbose_cli_two_ranks_one_device(tmp_path):
+    """digitalfilters.py -v under 2 ranks (gloo, one GPU): the per-step snapshot planes are
+    gathered to rank 0 and written there byte-identical to the single-rank run (A is
+    bit-exact), the temporal-mode files come from rank 0's full T only (no IndexError on the
+    ranks holding T[:, :nm]), and the PODFS outputs match the single-rank run."""
+    import multiprocessing as mp
+    single, multi = tmp_path / "single", tmp_path / "multi"
+    single.mkdir()
+    multi.mkdir()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_verbose_worker, args=(0, 1, 29700 + os.getpid() % 500, str(single), out))
+    p.start()
+    p.join(300)
+    assert p.exitcode == 0
+    ref = dict(out[0])
+    port = 29200 + os.getpid() % 500
+    procs = [ctx.Process(target=_verbose_worker, args=(r, 2, port, str(multi), out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+        assert p.exitcode == 0
+    assert out[0]["nm"] == ref["nm"] and out[1]["nm"] == ref["nm"]
+    assert np.array_equal(out[0]["mean"], ref["mean"])
+    names = sorted(os.listdir(single / "PODFS"))
+    assert sorted(os.listdir(multi / "PODFS")) == names
+    planes = [n for n in names if n.endswith(".prf") and not n.startswith("PODFS_")]
+    assert len(planes) == 6
+    for n in planes:
+        assert (single / "PODFS" / n).read_text() == (multi / "PODFS" / n).read_text(), n
+    tmodes = [n for n in names if n.startswith("POD.temporal_mode_")]
+    assert len(tmodes) >= ref["nm"]
+    for n in tmodes:
+        a = np.loadtxt(single / "PODFS" / n)
+        b = np.loadtxt(multi / "PODFS" / n)
+        assert np.array_equal(a[:, 0], b[:, 0])
+        sg = np.sign(np.dot(a[:, 1], b[:, 1]))
+        assert np.max(np.abs(a[:, 1] - sg * b[:, 1])) <= 1e-9 * np.max(np.abs(a[:, 1])), n
+    assert (single / "PODFS" / "PODFS_mean.prf").read_text() == (multi / "PODFS" / "PODFS_mean.prf").read_text()

@@ -140,6 +140,53 @@ def test_eigenvalue_file_writer(golden_dir, tmp_path):
     assert open(fn).read() == str(g["eigenvalues_dat"])
 
 
+def test_read_profile_dropin_matches_reference(golden_dir, tmp_path):
+    """digitalfilters.read_profile (drop-in) == the reference's read_profile (:487-522)."""
+    import digitalfilters as df
+    g = np.load(os.path.join(golden_dir, "unit_read_profile.npz"))
+    path = tmp_path / "profile.dat"
+    path.write_text(str(g["text"]))
+    for kma in (17, 32, 64):
+        assert np.array_equal(np.stack(df.read_profile(str(path), kma)), g["k%d" % kma]), kma
+
+
+def test_profile_file_setup_matches_oracle(golden_dir, tmp_path):
+    """-i profile.dat: the drop-in CLI setup reads the profile, clamps the stresses and skips
+    the rotation (:1306-1307, :1344-1350, :1476) exactly as the pinned oracle config does."""
+    import digitalfilters as df
+    from test_oracle_golden import cfg_from
+    g = np.load(os.path.join(golden_dir, "prof1d_14x16x8.npz"))
+    path = tmp_path / "profile.dat"
+    path.write_text(str(g["cfg_profile_text"]))
+    opts = df.make_parser().parse_args(["-j", "14", "-k", "16", "-n", "8", "--seed", "41", "-i", str(path),
+                                        "--nx", "1.0", "--ny", "0.3"])[0]
+    s = df.setup_from_options(opts)
+    cfg = cfg_from(g)
+    assert not s.rotated and not cfg.rotated
+    assert s.dt_eff == cfg.dt_eff == float(g["dt"])
+    for key in ("U", "uu", "vv", "ww", "uw"):
+        assert np.array_equal(s.profile[key], cfg.profile[key]), key
+
+
+def test_save_plane_matches_reference(golden_dir, tmp_path, monkeypatch):
+    """save_plane (verbose per-step snapshot .prf, PODFS.py:854-887): file name and text equal
+    to the reference's for three planes (default normal, a translation, a tilted plane)."""
+    import types
+    import digitalfilters as df
+    g = np.load(os.path.join(golden_dir, "unit_save_plane.npz"))
+    monkeypatch.chdir(tmp_path)
+    for c in range(3):
+        i_d = types.SimpleNamespace()
+        i_d.grid = types.SimpleNamespace(points=g["plane%d_points" % c])
+        i_d.n = [np.float64(v) for v in g["plane%d_n" % c]]
+        i_d.t_o = [float(v) for v in g["plane%d_t_o" % c]]
+        i_d.time = float(g["plane%d_time" % c])
+        df.save_plane(g["plane%d_u" % c], i_d)
+        name = str(g["plane%d_name" % c])
+        assert os.path.exists(os.path.join("PODFS", name)), name
+        assert open(os.path.join("PODFS", name)).read() == str(g["plane%d_text" % c])
+
+
 def test_sort_eigenvalues_semantics():
     import PODFS
     energy = np.array([1.0, 3.0, np.nan, 3.0, -2.0])
@@ -202,41 +249,58 @@ def test_hdf5_layout(tmp_path):
 
 
 def _gloo_worker(rank, world, port, A, out):
+    """One rank of the product's multi-GPU host path on gloo/CPU tensors:
+    engine.allreduce_correlation (packed lower-triangle all-reduce, divide, mirror) and
+    digitalfilters.gather_row_slabs (row slabs -> rank 0), on the rows host.row_slab gives it."""
     import torch
     import torch.distributed as dist
     import podsgen
+    import digitalfilters as df
+    from podsgen import engine as E
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    J, K, ns = 12, 5, 9
+    J, K, ns = 13, 5, 9
     j0, j1 = podsgen.row_slab(J, rank, world)
     P = J * K
     rows = np.concatenate([np.arange(c * P + j0 * K, c * P + j1 * K) for c in range(3)])
     Al = A[rows]
-    Ac = Al - np.mean(Al, 1)[:, None]
-    Cp = torch.from_numpy(np.dot(Ac.T, Ac))
-    dist.all_reduce(Cp)
-    out[rank] = (Cp.numpy() / ns).tobytes()
+    mean = np.mean(Al, 1)
+    Ac = Al - mean[:, None]
+    C = torch.from_numpy(np.dot(Ac.T, Ac))
+    E.allreduce_correlation(dist, C, ns, lambda x, d: x.copy_(torch.from_numpy(x.numpy() / d)))
+    s = podsgen.DFSetup(jma=J, kma=K, ns=ns, seed=1)
+    full = df.gather_row_slabs(dist, s, np.concatenate([mean[:, None], Ac], axis=1))
+    out[rank] = (C.numpy().tobytes(), None if full is None else full.tobytes())
     dist.destroy_process_group()
 
 
-def test_gloo_world2_correlation_decomposition():
-    """The multi-GPU decomposition (row slabs, partial A^T A, one all-reduce sum, divide)
-    reproduces the single-device correlation (oracle arithmetic, gloo transport)."""
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_multirank_correlation_and_gather(world):
+    """The multi-GPU decomposition through the product's host code (gloo transport, world 2
+    and 3 with unequal slabs): partial A_g^T A_g, the packed lower-triangle all-reduce, the
+    divide by ns, the mirror (C exactly symmetric), and the slab gather to rank 0."""
     import multiprocessing as mp
     rng = np.random.default_rng(0)
-    A = rng.standard_normal((3 * 12 * 5, 9)) + 1.0
+    J, K, ns = 13, 5, 9
+    A = rng.standard_normal((3 * J * K, ns)) + 1.0
     mgr = mp.Manager()
     out = mgr.dict()
-    port = 29500 + os.getpid() % 1000
+    port = 29500 + (os.getpid() + 17 * world) % 1000
     ctx = mp.get_context("spawn")
-    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, A, out)) for r in range(2)]
+    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, A, out)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(120)
         assert p.exitcode == 0
-    Ac = A - np.mean(A, 1)[:, None]
-    ref = np.dot(Ac.T, Ac) / 9
-    for r in range(2):
-        C = np.frombuffer(out[r]).reshape(9, 9)
+    mean = np.mean(A, 1)
+    Ac = A - mean[:, None]
+    ref = np.dot(Ac.T, Ac) / ns
+    for r in range(world):
+        C = np.frombuffer(out[r][0]).reshape(ns, ns)
+        assert np.array_equal(C, C.T)
         assert np.max(np.abs(C - ref)) <= 1e-13 * np.max(np.abs(ref))
+        assert (out[r][1] is None) == (r != 0)
+    full = np.frombuffer(out[0][1]).reshape(3 * J * K, ns + 1)
+    assert np.array_equal(full[:, 0], mean)
+    assert np.array_equal(full[:, 1:], Ac)

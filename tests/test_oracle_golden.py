@@ -8,7 +8,7 @@ import pytest
 from oracle import pods_oracle as O
 
 CASES = ["c1_32x32x64", "cli_10x11x5", "odd_12x9x17_aniso", "prf_8x12x9", "rot_6x7x6",
-         "dtanh_9x12x7", "circ_11x10x6", "ring_12x13x6", "readprf_case"]
+         "dtanh_9x12x7", "circ_11x10x6", "ring_12x13x6", "readprf_case", "prof1d_14x16x8"]
 UNIT_2D = ["dtanh", "circ", "circ_odd", "ring", "ring_thin"]
 
 
@@ -30,7 +30,57 @@ def cfg_from(g):
         kw["inner_d"] = float(g["cfg_inner_d"])
     if "cfg_ln_prf" in g.files:
         kw["ln_prf"] = float(g["cfg_ln_prf"])
+    if "cfg_profile_text" in g.files:
+        kw["profile1d"] = profile1d_from_text(str(g["cfg_profile_text"]), kw["kma"])
     return O.DFConfig(**kw)
+
+
+def profile1d_from_text(text, kma):
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "profile.dat")
+        with open(path, "w") as f:
+            f.write(text)
+        U, uu, vv, ww, uw = O.read_profile(path, kma)
+    return dict(U=U, uu=uu, vv=vv, ww=ww, uw=uw)
+
+
+def test_read_profile_matches_reference(golden_dir, tmp_path):
+    """read_profile (digitalfilters.py:487-522) restated == the reference's own output."""
+    g = np.load(os.path.join(golden_dir, "unit_read_profile.npz"))
+    path = tmp_path / "profile.dat"
+    path.write_text(str(g["text"]))
+    for kma in (17, 32, 64):
+        assert np.array_equal(np.stack(O.read_profile(str(path), kma)), g["k%d" % kma]), kma
+
+
+def test_mid_case_reduced(golden_dir):
+    """40 x 40 x 520 (three 256-row SYRK blocks, split K, spatial split ks=4 on the GPU side):
+    the oracle against the reference's sampled columns, C rows, eigenvalues, modes and FC."""
+    g = load(golden_dir, "mid_40x40x520")
+    cfg = cfg_from(g)
+    A = O.generate(cfg)
+    for k, i in enumerate(g["A_steps"]):
+        assert np.array_equal(A[:, i], g["A_cols"][k]), i
+    mean, Ac = O.mean_and_center(A)
+    assert np.array_equal(mean, g["mean_field"])
+    res = O.pod(Ac, cfg.ns, cfg.nm)
+    C = res["C"]
+    assert np.array_equal(C[g["C_rows_idx"]], g["C_rows"])
+    assert np.array_equal(np.diag(C), g["C_diag"])
+    assert np.array_equal(C.sum(axis=0), g["C_colsum"])
+    lam = g["energy"].real
+    assert np.max(np.abs(res["energy"] - lam)) <= 1e-12 * lam[0]
+    assert res["num_valid"] == int(g["num_valid_modes"]) and res["nm"] == int(g["nm"])
+    nm = res["nm"]
+    T, Tg = res["T"][:, :nm], g["temporal_modes"].real
+    Phi, Pg = res["spatial"], g["spatial_modes"]
+    for j in range(nm):
+        sg = np.sign(np.dot(T[:, j], Tg[:, j]))
+        assert np.max(np.abs(sg * T[:, j] - Tg[:, j])) <= 1e-10 * np.max(np.abs(Tg[:, j])), j
+        assert np.max(np.abs(sg * Phi[:, j] - Pg[:, j])) <= 1e-10 * np.max(np.abs(Pg[:, j])), j
+    fo = O.fourier(res["T"], cfg.ns, cfg.dt_eff, nm, cfg.et)
+    assert np.array_equal(fo["c_count"], g["N_FC"])
 
 
 def unit_2d(golden_dir, tag):
