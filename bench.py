@@ -40,7 +40,45 @@ CONFIGS = {
     "c1": (32, 32, 64, "32x32 inlet x 64 snapshots (BASELINE config 1)"),
     "c3": (256, 256, 4096, "256x256 inlet x 4096 snapshots, digital filter + full PODFS (BASELINE config 3)"),
     "c4": (512, 512, 8192, "512x512 inlet x 8192 snapshots (BASELINE config 4)"),
+    # BASELINE config 5: 1024^2 inlet, anisotropic length scales (-t: lnx = 2 ln -> nfx = 12,
+    # nfy = nfz = 6) and an inhomogeneous Reynolds-stress field through adapt2prf.  The full
+    # 16384-snapshot job needs ~165 GB per GPU on 8 GPUs (A 412 GB in all); c5s is the same
+    # workload at 1024 snapshots, which fits one GPU (readiness check, not a BASELINE line).
+    "c5": (1024, 1024, 16384, "1024x1024 inlet x 16384 snapshots, anisotropic filter + inhomogeneous R "
+                              "(BASELINE config 5)"),
+    "c5s": (1024, 1024, 1024, "1024x1024 inlet x 1024 snapshots, anisotropic filter + inhomogeneous R "
+                              "(config 5 workload at reduced ns, one GPU)"),
 }
+
+
+def c5_profile(J, K):
+    """a deterministic inhomogeneous SPD stress field on a tanh jet,
+    uu = vv = ww = (0.02 U)^2 scaled, uv/uw/vw = rho sqrt(..) with a smooth rho in (-0.4, 0.4),
+    fed through adapt2prf (digitalfilters.py:180-231) like a read_prf profile."""
+    y = np.linspace(-0.5, 0.5, J)[:, None]
+    z = np.linspace(-0.5, 0.5, K)[None, :]
+    U = 0.5 * (1.0 + np.tanh(10.0 * (0.5 - np.sqrt(y ** 2 + z ** 2)))) + 0.05
+    V = 0.01 * np.sin(3.0 * y) * np.ones_like(z)
+    W = 0.01 * np.cos(2.0 * z) * np.ones_like(y)
+    s = (0.02 * U) ** 2
+    rho = 0.4 * np.sin(2.0 * y + 3.0 * z) * np.ones_like(U)
+    uu, vv, ww = s.copy(), 1.1 * s, 0.9 * s
+    uv = rho * np.sqrt(uu * vv)
+    uw = -0.5 * rho * np.sqrt(uu * ww)
+    vw = 0.3 * rho * np.sqrt(vv * ww)
+    return dict(U=U, V=V, W=W, uu=uu, vv=vv, ww=ww, uv=uv, uw=uw, vw=vw)
+
+
+def make_setup(podsgen, config, seed):
+    J, K, ns, _ = CONFIGS[config]
+    if config in ("c5", "c5s"):
+        prf = c5_profile(J, K)
+        U = prf["U"]
+        flag = np.where(U ** 2 + prf["V"] ** 2 + prf["W"] ** 2 != 0)
+        dt1 = 0.1 / np.mean(U[flag])   # main() :1306-1309 with res = 0.1
+        # -t dt1/2 doubles the x length scale (:1310-1317): lnx = 6, nfx = 12
+        return podsgen.DFSetup(jma=J, kma=K, ns=ns, seed=seed, dt=dt1 / 2.0, prf=prf)
+    return podsgen.DFSetup(jma=J, kma=K, ns=ns, seed=seed)
 FP64_MFMA_PEAK_TFLOPS = 78.6  # MI355X dense FP64 matrix (spec); measured 70-76 by tools/mfma_bench.hip
 
 
@@ -59,12 +97,13 @@ def parse():
 def cpu_baseline(J, K, ns, nm=20, budget=20.0):
     """Time the oracle (test infrastructure, CPU) on a bounded sample and extrapolate."""
     from oracle import pods_oracle as O  # only the cpu_baseline leg imports the oracle
-    # threads actually used: the Python loops run on one, numpy's BLAS (SYRK, dgeev) on its pool
-    cores = 1
+    # threads actually used: the reference's Python loops (generation, reconstruction: ~95 % of
+    # the extrapolated time) run on ONE core; numpy's BLAS (SYRK, dgeev) uses its pool
+    blas_threads = 1
     try:
         from threadpoolctl import threadpool_info
-        cores = max([1] + [int(i.get("num_threads", 1)) for i in threadpool_info()
-                           if i.get("user_api") == "blas"])
+        blas_threads = max([1] + [int(i.get("num_threads", 1)) for i in threadpool_info()
+                                  if i.get("user_api") == "blas"])
     except Exception:
         pass
     t_all = time.perf_counter()
@@ -127,7 +166,11 @@ def cpu_baseline(J, K, ns, nm=20, budget=20.0):
               "DFT %d of %d frequencies, reconstruction loop %d iterations; extrapolated to the full job; "
               "sampled in %.1f s" % (np.__version__, m2, ns, J, K, ns_s, ns, n_e, nk, ns, reps,
                                      time.perf_counter() - t_all))
-    return {"value": J * K * ns / total / 1e6, "unit": "Mpoints/s", "cores": cores, "kind": "port",
+    blas_s = est["corr"] + est["eig"] + est["spatial"]
+    return {"value": J * K * ns / total / 1e6, "unit": "Mpoints/s", "cores": 1, "kind": "port",
+            "blas_threads": blas_threads,
+            "threads_note": "Python loops on 1 core (%.0f of %.0f s); SYRK/dgeev/Phi on %d BLAS threads (%.0f s)"
+                            % (total - blas_s, total, blas_threads, blas_s),
             "sample": sample, "extrapolated_seconds": round(total, 2),
             "stages_s": {k: round(v, 3) for k, v in est.items()}}
 
@@ -162,7 +205,7 @@ def main():
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     J, K, ns, desc = CONFIGS[args.config]
-    setup = podsgen.DFSetup(jma=J, kma=K, ns=ns, seed=args.seed)
+    setup = make_setup(podsgen, args.config, args.seed)
     gen = E.Generator(setup, device=local, rank=rank, world=world)
     d = dist if world > 1 else None
 
@@ -215,7 +258,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (seeded MT19937 random field, built tanh/top-hat profile)",
+            "data": ("synthetic (seeded MT19937 random field, inhomogeneous SPD stress field via adapt2prf, "
+                     "anisotropic x filter)" if args.config in ("c5", "c5s") else
+                     "synthetic (seeded MT19937 random field, built tanh/top-hat profile)"),
             "config": {"workload": desc, "jma": J, "kma": K, "ns": ns, "nm": setup.nm,
                        "nf": [setup.nfx, setup.nfy, setup.nfz], "parallelism": "row-slab dp%d" % world},
             "roofline": {"kernel": "pods_corr (k_syrk_glds + k_syrk_reduce), rank 0",
@@ -228,7 +273,7 @@ def main():
             "results": {"nm": int(pod.nm), "num_valid": int(pod.num_valid),
                         "N_FC": [int(x) for x in fo.c_count] if fo is not None else None},
         }
-        if world == 1 and not args.no_cpu:
+        if world == 1 and not args.no_cpu and args.config in ("c1", "c3"):
             out["cpu_baseline"] = cpu_baseline(J, K, ns, setup.nm, args.cpu_budget)
         print(json.dumps(out), flush=True)
     if world > 1:

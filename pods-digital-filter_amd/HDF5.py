@@ -10,7 +10,7 @@ Layout (CFDCodeIntegration.rst:59-74):
 Python 3 port of the same h5py calls (np.string_ -> np.bytes_, removed in numpy 2).
 This interpreter may not have h5py (the build image does not); then the identical h5py
 program runs in a Python that does (PODS_H5PY_PYTHON, or /opt/conda/bin/python3*),
-fed through a temporary .npz.  Without any h5py the call raises.
+fed per dataset through .npy files it memory-maps.  Without any h5py the call raises.
 """
 import glob
 import os
@@ -21,36 +21,47 @@ import tempfile
 import numpy as np
 
 _WRITER = r'''
+import os
 import sys
 import numpy as np
 import h5py
-d = np.load(sys.argv[1])
-f = h5py.File(sys.argv[2], "w")
-main = f.create_group("main")
-main.attrs["N_POD"] = int(d["nm"])
-main.attrs["period"] = float(d["period"])
-N_FC = main.create_dataset("N_FC", (int(d["nm"]),), dtype="i")
-N_FC[:] = d["N_FC"]
-n = int(np.sum(d["N_FC"]))
-FC = main.create_dataset("FC", (n * 3,), dtype=np.float64)
-FC[:] = d["FC"].reshape(n * 3, order="F")
-P = int(d["num_points"])
-data = main.create_dataset("mean", (P * 6,), dtype=np.float64)
-data[:] = d["mean"].reshape(P * 6, order="F")
-data.attrs["Np"] = P
-data.attrs["Nvar"] = 6
-data.attrs["Vars"] = np.bytes_("x,y,z,u,v,w,dummy")
-data.attrs["SF"] = [1., 1., 1., 1., 1., 1.]
-modes = main.create_group("modes")
-for i in range(int(d["nm"])):
-    counter = "%4.4i" % (i + 1)
-    data = modes.create_dataset("mode_" + counter, (P * 6,), dtype=np.float64)
-    data[:] = d["modes"][i, :, :].reshape(P * 6, order="F")
-    data.attrs["Np"] = P
-    data.attrs["Nvar"] = 6
-    data.attrs["Vars"] = np.bytes_("x,y,z,u,v,w,dummy")
-    data.attrs["SF"] = [1., 1., 1., 1., 1., 1.]
-f.close()
+
+
+def write(f, arrays, nm, period, num_points):
+    # HDF5.py:13-62, one dataset at a time (the modes are read one by one)
+    main = f.create_group("main")
+    main.attrs["N_POD"] = int(nm)
+    main.attrs["period"] = float(period)
+    N_FC = main.create_dataset("N_FC", (int(nm),), dtype="i")
+    N_FC[:] = arrays("N_FC")
+    n_fc = arrays("N_FC")
+    n = int(np.sum(n_fc))
+    FC = main.create_dataset("FC", (n * 3,), dtype=np.float64)
+    FC[:] = arrays("FC").reshape(n * 3, order="F")
+    P = int(num_points)
+
+    def put(grp, name, a):
+        data = grp.create_dataset(name, (P * 6,), dtype=np.float64)
+        data[:] = np.asarray(a).reshape(P * 6, order="F")
+        data.attrs["Np"] = P
+        data.attrs["Nvar"] = 6
+        data.attrs["Vars"] = np.bytes_("x,y,z,u,v,w,dummy")
+        data.attrs["SF"] = [1., 1., 1., 1., 1., 1.]
+    put(main, "mean", arrays("mean"))
+    modes = main.create_group("modes")
+    for i in range(int(nm)):
+        put(modes, "mode_" + "%4.4i" % (i + 1), arrays("mode", i))
+
+
+if __name__ == "__main__":
+    src, dst = sys.argv[1], sys.argv[2]
+    meta = np.load(os.path.join(src, "meta.npy"))
+
+    def arrays(name, i=None):
+        fn = name + ("_%04d" % i if i is not None else "") + ".npy"
+        return np.load(os.path.join(src, fn), mmap_mode="r")
+    with h5py.File(dst, "w") as f:
+        write(f, arrays, meta[0], meta[1], meta[2])
 '''
 
 
@@ -70,28 +81,42 @@ def _h5py_python():
 
 
 def write_HDF5(i_d, filename="PODFS/PODFS.hdf5"):
-    payload = dict(nm=np.array(i_d.nm), period=np.array(i_d.period), N_FC=np.asarray(i_d.N_FC),
-                   FC=np.asarray(i_d.FC, dtype=np.float64), num_points=np.array(i_d.num_points),
-                   mean=np.asarray(i_d.mean, dtype=np.float64), modes=np.asarray(i_d.modes, dtype=np.float64))
+    """HDF5.py:11-64.  With h5py in this interpreter the datasets are written directly, one
+    after the other; otherwise each array goes to its own .npy file and a Python with h5py
+    memory-maps them and writes dataset by dataset (the modes stream through one at a time,
+    nothing holds the whole payload twice -- config 5 writes 20 modes of 6 x 1 M doubles)."""
     d = os.path.dirname(filename)
     if d:
         os.makedirs(d, exist_ok=True)
+    nm, P = int(i_d.nm), int(i_d.num_points)
+    modes = np.asarray(i_d.modes, dtype=np.float64)
     try:
-        import h5py  # noqa: F401
-        have = True
+        import h5py
     except ImportError:
-        have = False
+        h5py = None
+    if h5py is not None:
+        ns_ = {}
+        exec(compile(_WRITER, "<HDF5 writer>", "exec"), ns_)
+        src = dict(N_FC=np.asarray(i_d.N_FC), FC=np.asarray(i_d.FC, dtype=np.float64),
+                   mean=np.asarray(i_d.mean, dtype=np.float64))
+        with h5py.File(filename, "w") as f:
+            ns_["write"](f, lambda name, i=None: modes[i] if name == "mode" else src[name], nm, i_d.period, P)
+        return filename
+    exe = _h5py_python()
+    if exe is None:
+        raise ImportError("HDF5 output needs h5py (none in this interpreter and no "
+                          "PODS_H5PY_PYTHON / conda python with h5py found)")
     with tempfile.TemporaryDirectory() as tmp:
-        npz = os.path.join(tmp, "podfs_payload.npz")
-        np.savez(npz, **payload)
-        if have:
-            exe = sys.executable
-        else:
-            exe = _h5py_python()
-            if exe is None:
-                raise ImportError("HDF5 output needs h5py (none in this interpreter and no "
-                                  "PODS_H5PY_PYTHON / conda python with h5py found)")
-        r = subprocess.run([exe, "-c", _WRITER, npz, filename], capture_output=True, text=True)
+        np.save(os.path.join(tmp, "meta.npy"), np.array([nm, float(i_d.period), P], dtype=np.float64))
+        np.save(os.path.join(tmp, "N_FC.npy"), np.asarray(i_d.N_FC))
+        np.save(os.path.join(tmp, "FC.npy"), np.asarray(i_d.FC, dtype=np.float64))
+        np.save(os.path.join(tmp, "mean.npy"), np.asarray(i_d.mean, dtype=np.float64))
+        for i in range(nm):
+            np.save(os.path.join(tmp, "mode_%04d.npy" % i), modes[i])
+        script = os.path.join(tmp, "writer.py")
+        with open(script, "w") as f:
+            f.write(_WRITER)
+        r = subprocess.run([exe, script, tmp, filename], capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("HDF5 writer failed: " + r.stderr[-2000:])
     return filename

@@ -1397,7 +1397,7 @@ hipError_t launch_filter_yz(int NY, const double* T1, const double* by, const do
 
 int filter_yz_max_K(int Kp) {
   (void)Kp;
-  return 512;  // 8-row tiles x 32 chunks of 16 outputs
+  return 1024;  // 8-row tiles x 64 chunks of 16 outputs on 512 threads (yz_tj)
 }
 
 hipError_t launch_mean(const double* AT, int64_t rowlen, int ns, const int* prog, int nprog,

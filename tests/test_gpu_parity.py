@@ -324,3 +324,28 @@ def test_mid_case_vs_reference(ctx, golden_dir):
     fo = E_.run_fourier(ctx, pod.T, pod.nm, s.ns, s.dt_eff, s.et)
     assert np.array_equal(fo.c_count, g["N_FC"]), (fo.c_count, g["N_FC"])
     assert np.array_equal(fo.FC[:, 0], g["FC"][:, 0])
+
+
+@pytest.mark.parametrize("J,K,ns,kw", [
+    (9, 1024, 3, {}),                                             # C5 width: 8-row tiles, 64 z chunks
+    (11, 600, 4, {"dt": 0.05}),                                   # K not a multiple of 16, nfx != nfy
+])
+def test_generate_wide_inlet_vs_oracle(ctx, J, K, ns, kw):
+    """kma up to 1024 (BASELINE config 5's 1024-point span): bit-exact against the oracle."""
+    s = podsgen.DFSetup(jma=J, kma=K, ns=ns, seed=77, **kw)
+    A = E.Generator(s, ctx=ctx).generate().to_host()
+    ref = O.generate(O.DFConfig(jma=J, kma=K, ns=ns, seed=77, **kw))
+    assert np.array_equal(A, ref)
+
+
+def test_generate_c5_style_prf_vs_oracle(ctx):
+    """The C5 workload (adapt2prf with a synthetic inhomogeneous stress field, anisotropic
+    x filter from -t) on a 12 x 640 inlet: bit-exact against the oracle."""
+    import bench
+    J, K, ns = 12, 640, 4
+    prf = bench.c5_profile(J, K)
+    s = podsgen.DFSetup(jma=J, kma=K, ns=ns, seed=5, dt=0.05, prf=prf)
+    assert s.nfx > s.nfy
+    A = E.Generator(s, ctx=ctx).generate().to_host()
+    ref = O.generate(O.DFConfig(jma=J, kma=K, ns=ns, seed=5, dt=0.05, prf=prf))
+    assert np.array_equal(A, ref)
