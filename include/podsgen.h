@@ -150,6 +150,20 @@ int pods_sytrd_trace(pods_ctx* ctx, const double* C_dev, int n, int wg, int64_t*
  * cross-workgroup wait timed out (results invalid).  Synchronises the stream. */
 int pods_syev_status(pods_ctx* ctx);
 
+/* Two-stage eigensolver for correlation matrices beyond pods_syev's on-chip limit (BASELINE
+ * configs 4/5, PODFS.py:1309-1310 at ns = 8192): dense -> band (bandwidth 32, fp64 MFMA
+ * blocked updates), band -> tridiagonal (bulge chasing), bisection, inverse iteration on the
+ * band matrix, back-transformation.  Same arguments and outputs as pods_syev; 3 <= n <=
+ * 8192, nvec <= 64.  Asynchronous on the bound stream; pods_syev2_status reports a hand-off
+ * timeout after the stream has drained. */
+int pods_syev2(pods_ctx* ctx, const double* C_dev, int n, int nvec, double* lambda_desc_dev,
+               double* vec_dev);
+int pods_syev2_status(pods_ctx* ctx);
+/* Diagnostics: copy `count` doubles of the last pods_syev2's workspace to the host:
+ * what = 0 the stage-1 band (n x 64, band[c*64 + d] = A[c+d][c]), 1 the same after stage 2,
+ * 2 the tridiagonal {D (n), E (n-1)}, 3 the reduced dense matrix (n x n). */
+int pods_syev2_inspect(pods_ctx* ctx, int n, int nvec, int what, double* out_host, int64_t count);
+
 /* Spatial modes Phi = ((A-m) T[:, :nm]) * (1/lambda) / ns (PODFS.py:1330-1333).
  * T_dev: ns x ldT row-major.  phi_dev: 3*P_local x nm row-major (reference layout). */
 int pods_spatial_modes(pods_ctx* ctx, const double* T_dev, int ldT, const double* lambda_host,

@@ -220,6 +220,9 @@ struct pods_ctx {
   DevBuf R, T1, A, mean, lund, taps, rot, prog_mean, prog_dft, tbuf, mag, lam, cwork, items, spwork, prog_rank;
   DevBuf e_wm, e_x, e_flags, e_det, e_v, e_t, e_part, e_w2, e_inv, e_cnt;  // pods_syev workspace
   int e_G = 0;
+  DevBuf e2_ws, e2_flags, e2_ipiv;  // pods_syev2 (two-stage) workspace
+  size_t e2_flag_words = 0;
+  uint32_t e2_epoch = 0;
   int nitems = 0;
   int64_t items_key = -1;
   int64_t lund_sj = 0;  // j-stride of the Lund table (0: constant along j)
@@ -325,7 +328,8 @@ int pods_destroy(pods_ctx* c) {
   for (DevBuf* b : {&c->R, &c->T1, &c->A, &c->mean, &c->lund, &c->taps, &c->rot, &c->prog_mean,
                     &c->prog_dft, &c->tbuf, &c->mag, &c->lam, &c->cwork, &c->items, &c->e_wm,
                     &c->e_x, &c->e_flags, &c->e_det, &c->e_v, &c->e_t, &c->e_part, &c->e_w2,
-                    &c->e_inv, &c->e_cnt, &c->spwork, &c->prog_rank, &c->zero})
+                    &c->e_inv, &c->e_cnt, &c->spwork, &c->prog_rank, &c->zero, &c->e2_ws, &c->e2_flags,
+                    &c->e2_ipiv})
     release(*b);
   c->rng.free_all();
   delete c;
@@ -743,6 +747,64 @@ int pods_syev(pods_ctx* c, const double* C, int n, int nvec, double* lam_desc, d
                                          c->e_flags.as<uint32_t>() + 1, vec,
                                          c->stream));
   }
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_syev2(pods_ctx* c, const double* C, int n, int nvec, double* lam_desc, double* vec) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!C || !lam_desc || n < 3 || nvec < 0 || nvec > std::min(n, 64) || (nvec > 0 && !vec))
+    return fail(PODS_ERR_ARG, "pods_syev2: bad arguments");
+  if (n > pods::syev2_max_n())
+    return fail(PODS_ERR_UNSUPPORTED, "pods_syev2: n > " + std::to_string(pods::syev2_max_n()));
+  PODS_HIP(hipSetDevice(c->device));
+  pods::SyevdPlan plan{};
+  const size_t wsd = pods::sy2sb_work_doubles(n, nvec, &plan);
+  PODS_HIP(ensure(c->e2_ws, wsd * sizeof(double)));
+  const size_t fw = 128 + (size_t)n;
+  if (c->e2_flag_words < fw) {
+    PODS_HIP(ensure(c->e2_flags, fw * sizeof(uint32_t)));
+    PODS_HIP(hipMemset(c->e2_flags.p, 0, fw * sizeof(uint32_t)));
+    c->e2_flag_words = fw;
+    c->e2_epoch = 0;
+  }
+  PODS_HIP(hipMemsetAsync(c->e2_flags.as<uint32_t>() + 64, 0, 64 * sizeof(uint32_t), c->stream));  // abort words
+  PODS_HIP(ensure(c->e2_ipiv, (size_t)std::max(nvec, 1) * n * sizeof(int)));
+  PODS_HIP(ensure(c->e_cnt, pods::tri_grid_bytes()));
+  ++c->e2_epoch;
+  PODS_HIP(pods::launch_syevd2(C, n, nvec, c->e2_ws.as<double>(), plan, c->e2_flags.as<uint32_t>(), c->e2_epoch,
+                               c->e2_ipiv.as<int>(), c->e_cnt.as<int>(), lam_desc, vec, c->stream));
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_syev2_inspect(pods_ctx* c, int n, int nvec, int what, double* out_host, int64_t count) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!c->e2_ws.p || !out_host || count < 0) return fail(PODS_ERR_ARG, "pods_syev2_inspect: bad arguments");
+  pods::SyevdPlan plan{};
+  pods::sy2sb_work_doubles(n, nvec, &plan);
+  const int64_t offs[10] = {plan.off_band0, plan.off_band, plan.off_de, plan.off_aw, plan.off_vx,
+                            plan.off_t, plan.off_tau, plan.off_y, plan.off_x, plan.off_w};
+  if (what < 0 || what > 9) return fail(PODS_ERR_ARG, "pods_syev2_inspect: what");
+  if ((size_t)(offs[what] + count) * sizeof(double) > c->e2_ws.bytes) return fail(PODS_ERR_ARG, "count");
+  PODS_HIP(hipMemcpyAsync(out_host, c->e2_ws.as<double>() + offs[what], (size_t)count * sizeof(double),
+                          hipMemcpyDeviceToHost, c->stream));
+  PODS_HIP(hipStreamSynchronize(c->stream));
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_syev2_status(pods_ctx* c) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!c->e2_flags.p) return PODS_OK;
+  uint32_t abort_word[2] = {0, 0};  // [0]: panel QR hand-offs, [1]: bulge chasing
+  PODS_HIP(hipMemcpyAsync(abort_word, c->e2_flags.as<uint32_t>() + 64, sizeof(abort_word), hipMemcpyDeviceToHost,
+                          c->stream));
+  PODS_HIP(hipStreamSynchronize(c->stream));
+  if (abort_word[0] || abort_word[1]) return fail(PODS_ERR_INTERNAL, "pods_syev2: hand-off wait timed out (aborted)");
   return PODS_OK;
   PODS_CATCH
 }

@@ -1376,6 +1376,12 @@ hipError_t launch_tri_eigvecs(const double* D, const double* E, int n, const dou
   return hipGetLastError();
 }
 
+hipError_t launch_orth(const double* lam_desc, const double* bounds, int n, int nvec, double* Z, int ldz,
+                       hipStream_t st) {
+  hipLaunchKernelGGL(eig::k_orth, dim3(1), dim3(256), 0, st, lam_desc, bounds, n, nvec, Z, ldz);
+  return hipGetLastError();
+}
+
 hipError_t launch_back_transform(const double* V, int64_t ldv, const double* tau, int n, int nvec,
                                  double* Tg, double* part, double* W2, uint32_t* abortw, double* Z,
                                  hipStream_t st) {

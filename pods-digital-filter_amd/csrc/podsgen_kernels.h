@@ -86,6 +86,24 @@ hipError_t launch_back_transform(const double* V, int64_t ldv, const double* tau
                                  double* Tg, double* part, double* W2, uint32_t* abortw, double* Z,
                                  hipStream_t st);
 void bt_plan(int n, int nvec, int* CR, int* G);
+// cluster modified Gram-Schmidt of the nvec eigenvector columns of Z (k_orth)
+hipError_t launch_orth(const double* lam_desc, const double* bounds, int n, int nvec, double* Z, int ldz,
+                       hipStream_t st);
+
+// ---- two-stage eigensolver for n > 4096 (podsgen_sy2sb.hip) ---------------------------
+struct SyevdPlan {
+  int B, np, KS, NZ, RP;
+  int64_t off_aw, off_vx, off_t, off_tau, off_y, off_x, off_w, off_zp, off_m, off_pub, off_band, off_band0,
+      off_de, off_inv, off_end;
+};
+int sy2sb_band();
+int syev2_max_n();  // the bisection keeps the tridiagonal in LDS
+// doubles of workspace for n, nvec (and the offsets inside it)
+size_t sy2sb_work_doubles(int n, int nvec, SyevdPlan* plan);
+// flags: 128 + n uint32 (zeroed once at allocation); ipiv: nvec * n ints; epoch: a counter
+// that grows by one per call (the panel hand-off tags); grid_cnt: tri_grid_bytes()
+hipError_t launch_syevd2(const double* C, int n, int nvec, double* ws, const SyevdPlan& p, uint32_t* flags,
+                         uint32_t epoch, int* ipiv, int* grid_cnt, double* lam_desc, double* vec, hipStream_t st);
 size_t bt_part_bytes(int n, int nvec);
 size_t bt_w2_bytes(int nvec);
 

@@ -1,0 +1,1018 @@
+// Two-stage symmetric eigensolver for correlation matrices too large for the on-chip
+// tridiagonalisation (pods_syev, n <= 4096): PODFS.py:1309-1310 at BASELINE configs 4/5
+// (ns = 8192, 16384), where rocSOLVER dsyevd takes 0.67 s / several s.
+//
+//   stage 1  dense -> band (lower bandwidth B): per panel of B columns
+//            k_pqr      Householder QR of the m x B panel below the band, rows spread over NW
+//                       co-resident workgroups with ONE cross-CU hop per column (partial Gram
+//                       rows + the pivot row are published, every workgroup forms the reflector
+//                       redundantly); writes the explicit V (m x B), tau and R, and
+//                       (one more hop: partial V^T V) T (dlarft 'F','C')
+//            k_ay       Y = A22 V on fp64 MFMA (split K)      \
+//            k_xt       X = Y T                                |  W = X - 1/2 V T^T V^T X
+//            k_z/k_zm   Z = V^T X, M = 1/2 T^T Z               |  (LAPACK dsytrd blocking)
+//            k_w        W = X - V M                           /
+//            k_upd      A22 -= V W^T + W V^T on fp64 MFMA, lower tiles mirrored (exactly
+//                       symmetric)
+//   stage 2  band -> tridiagonal by bulge chasing (k_sbtrd): sweep s annihilates column s
+//            below the subdiagonal with Householders of length <= B, chasing the bulge down;
+//            sweeps run concurrently on different workgroups, task (s, k) starting once
+//            sweep s-1 has finished its task k+2 (the last task whose elements it shares)
+//   eigenvalues  Sturm bisection of the tridiagonal (podsgen_eigen.hip)
+//   vectors  inverse iteration on the BAND matrix (k_band_invit: banded LU with partial
+//            pivoting of B - lambda I in an LDS window, two solves), cluster MGS (k_orth),
+//            then Y <- Q1 Y with the stage-1 panels (k_bt_z / k_bt_t / k_bt_u).
+// The algorithm's index bookkeeping is prototyped in tools/twostage_proto.py.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+
+#include "podsgen_kernels.h"
+
+namespace pods {
+namespace sb {
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double ld_c(const double* p) {
+  const unsigned long long u = __hip_atomic_load(
+      const_cast<unsigned long long*>(reinterpret_cast<const unsigned long long*>(p)), __ATOMIC_RELAXED,
+      __HIP_MEMORY_SCOPE_AGENT);
+  return __longlong_as_double((long long)u);
+}
+__device__ __forceinline__ void st_c(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_f(const uint32_t* p) {
+  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_f(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Pipelined coherent accesses (MI355X_MICROARCH.md "Valid forms": sc1 stores drained before
+// the flag, sc1 loads after the poll): raw buffer loads/stores with the sc1 policy bit, no
+// per-access wait (the agent-scope atomics above serialise: one round trip each).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const double* base, int64_t n) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), 0, (int)(n * 8), 0x00020000);
+}
+__device__ __forceinline__ double bld(__amdgpu_buffer_rsrc_t r, int idx) {
+  const auto q = __builtin_amdgcn_raw_buffer_load_b64(r, idx * 8, 0, (1u << 31) | 16u);
+  return __builtin_bit_cast(double, q);
+}
+__device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t r, int idx, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(
+      __builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0)), v), r, idx * 8, 0, 16u);
+}
+
+constexpr int SPIN_LIMIT = 1 << 22;
+
+// ---------------------------------------------------------------------------------------
+// k_pqr<B>: Householder QR of the panel P = A[r0:r0+m, c0:c0+B] (row-major A, ld lda).
+// Workgroup w holds panel rows [w*RP, min((w+1)*RP, m)) in LDS.  Column j: partial
+// s_k = sum_{r>j, local} P[r][j] P[r][k] (k >= j) and, from the owner of row j, P[j][k],
+// are published; after the hop every workgroup sums the partials in workgroup order
+// (identical bits everywhere), forms beta, tau, v = [1; P[j+1:, j] / (alpha - beta)] and
+// w_k = v^T P[:, k] = P[j][k] + s_k / (alpha - beta), and updates its rows.
+// Outputs: Vx (m x B explicit, unit diagonal, zeros above), tau (B), R into A's panel rows
+// [0, B) (zeros below the diagonal and in rows >= B).
+// ---------------------------------------------------------------------------------------
+template <int B>
+__global__ __launch_bounds__(256, 1) void k_pqr(double* __restrict__ A, int64_t lda, int r0, int c0, int m,
+                                               int RP, int NW, double* __restrict__ pub,
+                                               uint32_t* __restrict__ flags, uint32_t epoch,
+                                               uint32_t* __restrict__ abortw, double* __restrict__ Vx,
+                                               double* __restrict__ tau, double* __restrict__ gpart,
+                                               double* __restrict__ Tout) {
+  static_assert(B == 32, "k_pqr: one half-wave per panel row group (lane = column)");
+  constexpr int RG = 256 / B;   // 8 row groups (half-waves)
+  constexpr int NR = 256 / RG;  // rows per thread: RP <= 256
+  constexpr int LDP = B + 1;
+  __shared__ double red[RG][B];
+  __shared__ double S[B], rowj[B], taul[B];
+  __shared__ double gsum[64 * B];
+  __shared__ double G[B][LDP], Ts[B][LDP];
+  const int w = blockIdx.x, t = threadIdx.x;
+  const int kq = t % B, rg = t / B;
+  const int g0 = w * RP, g1 = min(g0 + RP, m);
+  const int nl = max(g1 - g0, 0);
+  const int src0 = (t & 63) & ~(B - 1);  // lane 0 of this half-wave
+  // P[i] = panel element (local row rg + RG*i, column kq), in registers
+  double P[NR];
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int r = rg + RG * i;
+    P[i] = r < nl ? A[(int64_t)(r0 + g0 + r) * lda + c0 + kq] : 0.0;
+  }
+  const int kc = min(m, B);
+  for (int j = 0; j < kc; ++j) {
+    // column j of my rows, from lane j of the half-wave
+    double pj[NR];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) pj[i] = __shfl(P[i], src0 + j);
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int gr = g0 + rg + RG * i;
+      if (gr > j && rg + RG * i < nl) acc = fma(pj[i], P[i], acc);
+    }
+    red[rg][kq] = kq >= j ? acc : 0.0;
+    // the pivot row's owner keeps row j for the publish
+    if (j >= g0 && j < g1 && rg == (j - g0) % RG) {
+      const int i = (j - g0) / RG;
+      double pr = 0.0;
+#pragma unroll
+      for (int q = 0; q < NR; ++q)
+        if (q == i) pr = P[q];
+      rowj[kq] = pr;
+    }
+    __syncthreads();
+    double* pb = pub + ((int64_t)(j & 1) * NW + w) * 2 * B;
+    const __amdgpu_buffer_rsrc_t rpub = rsrc(pub, (int64_t)2 * NW * 2 * B);
+    const int pbase = ((j & 1) * NW + w) * 2 * B;
+    if (t < B) {
+      double s = 0.0;
+#pragma unroll
+      for (int q = 0; q < RG; ++q) s += red[q][t];
+      bst(rpub, pbase + t, s);
+      if (j >= g0 && j < g1) bst(rpub, pbase + B + t, rowj[t]);
+    }
+    (void)pb;
+    drain();
+    __syncthreads();
+    const uint32_t want = epoch * 256u + (uint32_t)(j + 1);
+    if (t == 0) st_f(flags + w, want);
+    if (t < NW) {
+      int spin = 0;
+      while ((int)(ld_f(flags + t) - want) < 0) {
+        if (++spin > SPIN_LIMIT) {
+          st_f(abortw, 1u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+    {
+      const int qb = (j & 1) * NW * 2 * B;
+      for (int e = t; e < NW * B; e += 256) gsum[e] = bld(rpub, qb + (e / B) * 2 * B + (e % B));
+      if (t < B) rowj[t] = bld(rpub, qb + (j / RP) * 2 * B + B + t);
+    }
+    __syncthreads();
+    if (t < B) {
+      double s = 0.0;
+      for (int q = 0; q < NW; ++q) s += gsum[q * B + t];
+      S[t] = s;
+    }
+    __syncthreads();
+    // ---- reflector (dlarfg), redundantly in every thread -----------------------------
+    const double alpha = rowj[j], sigma = S[j];
+    double beta = alpha, tj = 0.0, scal = 0.0;
+    if (sigma != 0.0) {
+      beta = -copysign(sqrt(fma(alpha, alpha, sigma)), alpha);
+      tj = (beta - alpha) / beta;
+      scal = 1.0 / (alpha - beta);
+    }
+    if (t == 0) {
+      taul[j] = tj;
+      if (w == 0) tau[j] = tj;
+    }
+    const double wk = (kq > j) ? fma(scal, S[kq], rowj[kq]) : 0.0;
+    const double f = -tj * wk;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int gr = g0 + rg + RG * i;
+      if (gr < j) continue;
+      const double v = gr == j ? 1.0 : scal * pj[i];
+      if (kq > j) P[i] = fma(f, v, P[i]);
+      else if (kq == j) P[i] = gr == j ? beta : v;
+    }
+    __syncthreads();  // rowj / S are rewritten by the next column
+  }
+  // ---- outputs: explicit V and R; V (explicit) kept in registers for the Gram ----------
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int r = rg + RG * i;
+    const int gr = g0 + r;
+    if (r < nl) {
+      const double pv = P[i];
+      const double v = kq >= kc ? 0.0 : (gr > kq ? pv : (gr == kq ? 1.0 : 0.0));
+      Vx[(int64_t)gr * B + kq] = v;
+      A[(int64_t)(r0 + gr) * lda + c0 + kq] = (gr <= kq && gr < B) ? pv : 0.0;
+      P[i] = v;
+    } else {
+      P[i] = 0.0;
+    }
+  }
+  // ---- T (dlarft 'F','C'): G = V^T V (partials per workgroup) -> workgroup 0 -------------
+  // thread (b = kq, rg): sum over its rows of V[r][a] V[r][b] for every a (V[r][a] from lane a)
+  {
+    double gacc[B];
+#pragma unroll
+    for (int aa = 0; aa < B; ++aa) gacc[aa] = 0.0;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+#pragma unroll
+      for (int aa = 0; aa < B; ++aa) gacc[aa] = fma(__shfl(P[i], src0 + aa), P[i], gacc[aa]);
+    }
+    // reduce over the 8 row groups through LDS, one a-block at a time
+    const __amdgpu_buffer_rsrc_t rgp = rsrc(gpart, (int64_t)NW * B * B);
+    for (int a0 = 0; a0 < B; a0 += 8) {
+#pragma unroll
+      for (int aa = 0; aa < 8; ++aa) gsum[(rg * 8 + aa) * B + kq] = gacc[a0 + aa];
+      __syncthreads();
+      {
+        const int aa = t / B, b = t % B;  // 256 threads = 8 a's x 32 b's
+        double g = 0.0;
+#pragma unroll
+        for (int q = 0; q < RG; ++q) g += gsum[(q * 8 + aa) * B + b];
+        bst(rgp, w * B * B + (a0 + aa) * B + b, g);
+      }
+      __syncthreads();
+    }
+  }
+  drain();
+  __syncthreads();
+  const uint32_t wantg = epoch * 256u + 255u;
+  if (t == 0) st_f(flags + w, wantg);
+  if (w != 0) return;
+  if (t < NW) {
+    int spin = 0;
+    while ((int)(ld_f(flags + t) - wantg) < 0) {
+      if (++spin > SPIN_LIMIT) {
+        st_f(abortw, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  {
+    const __amdgpu_buffer_rsrc_t rgp = rsrc(gpart, (int64_t)NW * B * B);
+    for (int e = t; e < B * B; e += 256) {
+      double g = 0.0;
+      for (int q = 0; q < NW; ++q) g += bld(rgp, q * B * B + e);
+      G[e / B][e % B] = g;
+      Ts[e / B][e % B] = 0.0;
+    }
+  }
+  __syncthreads();
+  for (int i = 0; i < B; ++i) {
+    const double ti = i < kc ? taul[i] : 0.0;
+    double v = 0.0;
+    if (t < i) {
+      for (int q = t; q < i; ++q) v = fma(Ts[t][q], G[q][i], v);
+      v = -ti * v;
+    }
+    __syncthreads();
+    if (t < i) Ts[t][i] = v;
+    if (t == i) Ts[i][i] = ti;
+    __syncthreads();
+  }
+  for (int e = t; e < B * B; e += 256) Tout[e] = Ts[e / B][e % B];
+  if (t >= kc && t < B) tau[t] = 0.0;
+}
+
+// Y_s = A22[:, k-slice s] Vx[k-slice s, :] on v_mfma_f64_16x16x4 (A22 = A[r0:, r0:]).
+// Block: 64 rows x B cols, 4 waves x 16 rows; K staged through LDS 32 at a time.
+template <int B>
+__global__ __launch_bounds__(256) void k_ay(const double* __restrict__ A, int64_t lda, int r0, int m,
+                                            const double* __restrict__ Vx, int kchunk,
+                                            double* __restrict__ Y) {
+  constexpr int KC = 32, LDA_S = KC + 2;
+  __shared__ double As[64 * LDA_S];
+  __shared__ double Vs[KC * (B + 2)];
+  const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int i0 = blockIdx.x * 64;
+  const int k0 = blockIdx.y * kchunk, k1 = min(m, k0 + kchunk);
+  f64x4 acc[B / 16];
+#pragma unroll
+  for (int c = 0; c < B / 16; ++c) acc[c] = (f64x4){0.0, 0.0, 0.0, 0.0};
+  for (int kb = k0; kb < k1; kb += KC) {
+    for (int e = t; e < 64 * KC; e += 256) {
+      const int r = e / KC, k = e % KC;
+      const int gi = i0 + r, gk = kb + k;
+      As[r * LDA_S + k] = (gi < m && gk < k1) ? A[(int64_t)(r0 + gi) * lda + r0 + gk] : 0.0;
+    }
+    for (int e = t; e < KC * B; e += 256) {
+      const int k = e / B, c = e % B;
+      const int gk = kb + k;
+      Vs[k * (B + 2) + c] = gk < k1 ? Vx[(int64_t)gk * B + c] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < KC; kk += 4) {
+      const double a = As[(16 * wv + fr) * LDA_S + kk + fk];
+#pragma unroll
+      for (int c = 0; c < B / 16; ++c) {
+        const double b = Vs[(kk + fk) * (B + 2) + 16 * c + fr];
+        acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[c], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  double* Yb = Y + (int64_t)blockIdx.y * m * B;
+#pragma unroll
+  for (int c = 0; c < B / 16; ++c)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int gi = i0 + 16 * wv + fk + 4 * reg;
+      if (gi < m) Yb[(int64_t)gi * B + 16 * c + fr] = acc[c][reg];
+    }
+}
+
+// X = (sum_s Y_s) T, 256/B rows per block.
+template <int B>
+__global__ __launch_bounds__(256) void k_xt(const double* __restrict__ Y, int KS, int m,
+                                            const double* __restrict__ T, double* __restrict__ X) {
+  constexpr int RB = 256 / B;
+  __shared__ double Ts[B][B + 1];
+  __shared__ double Ys[RB][B + 1];
+  const int t = threadIdx.x, rr = t / B, c = t % B;
+  for (int e = t; e < B * B; e += 256) Ts[e / B][e % B] = T[e];
+  const int i = blockIdx.x * RB + rr;
+  double s = 0.0;
+  if (i < m)
+    for (int q = 0; q < KS; ++q) s += Y[((int64_t)q * m + i) * B + c];
+  Ys[rr][c] = s;
+  __syncthreads();
+  if (i >= m) return;
+  double x = 0.0;
+  for (int l = 0; l <= c; ++l) x = fma(Ys[rr][l], Ts[l][c], x);  // T upper triangular
+  X[(int64_t)i * B + c] = x;
+}
+
+// Partials of Z = Vx^T X over row chunks: block q handles rows [q*chunk, ...).
+template <int B>
+__global__ __launch_bounds__(256) void k_z(const double* __restrict__ Vx, const double* __restrict__ X, int m,
+                                           int chunk, double* __restrict__ Zp) {
+  constexpr int RT = 32;
+  __shared__ double Vs[RT][B + 1];
+  __shared__ double Xs[RT][B + 1];
+  const int t = threadIdx.x;
+  constexpr int PER = B * B / 256;  // entries per thread
+  double acc[PER > 0 ? PER : 1];
+#pragma unroll
+  for (int q = 0; q < (PER > 0 ? PER : 1); ++q) acc[q] = 0.0;
+  const int a0 = blockIdx.x * chunk, a1 = min(m, a0 + chunk);
+  for (int rb = a0; rb < a1; rb += RT) {
+    for (int e = t; e < RT * B; e += 256) {
+      const int r = e / B, c = e % B;
+      const bool ok = rb + r < a1;
+      Vs[r][c] = ok ? Vx[(int64_t)(rb + r) * B + c] : 0.0;
+      Xs[r][c] = ok ? X[(int64_t)(rb + r) * B + c] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < (PER > 0 ? PER : 1); ++q) {
+      const int e = t + 256 * q;
+      if (e < B * B) {
+        const int a = e / B, b = e % B;
+        double s = acc[q];
+        for (int r = 0; r < RT; ++r) s = fma(Vs[r][a], Xs[r][b], s);
+        acc[q] = s;
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < (PER > 0 ? PER : 1); ++q) {
+    const int e = t + 256 * q;
+    if (e < B * B) Zp[(int64_t)blockIdx.x * B * B + e] = acc[q];
+  }
+}
+
+// M = 1/2 T^T Z, Z = sum of the nz partials (in order).
+template <int B>
+__global__ __launch_bounds__(256) void k_zm(const double* __restrict__ Zp, int nz, const double* __restrict__ T,
+                                            double* __restrict__ M) {
+  __shared__ double Z[B][B + 1];
+  const int t = threadIdx.x;
+  for (int e = t; e < B * B; e += 256) {
+    double s = 0.0;
+    for (int q = 0; q < nz; ++q) s += Zp[(int64_t)q * B * B + e];
+    Z[e / B][e % B] = s;
+  }
+  __syncthreads();
+  for (int e = t; e < B * B; e += 256) {
+    const int a = e / B, b = e % B;
+    double s = 0.0;
+    for (int l = 0; l <= a; ++l) s = fma(T[l * B + a], Z[l][b], s);  // (T^T)[a][l] = T[l][a], l <= a
+    M[e] = 0.5 * s;
+  }
+}
+
+// W = X - Vx M
+template <int B>
+__global__ __launch_bounds__(256) void k_w(const double* __restrict__ X, const double* __restrict__ Vx,
+                                           const double* __restrict__ M, int m, double* __restrict__ W) {
+  constexpr int RB = 256 / B;
+  __shared__ double Ms[B][B + 1];
+  __shared__ double Vs[RB][B + 1];
+  const int t = threadIdx.x, rr = t / B, c = t % B;
+  for (int e = t; e < B * B; e += 256) Ms[e / B][e % B] = M[e];
+  const int i = blockIdx.x * RB + rr;
+  Vs[rr][c] = i < m ? Vx[(int64_t)i * B + c] : 0.0;
+  __syncthreads();
+  if (i >= m) return;
+  double s = X[(int64_t)i * B + c];
+  for (int l = 0; l < B; ++l) s = fma(-Vs[rr][l], Ms[l][c], s);
+  W[(int64_t)i * B + c] = s;
+}
+
+// A22 <- A22 - V W^T - W V^T on lower 64x64 tiles (fp64 MFMA, K = 2B), each tile written
+// to its place and, transposed through LDS, to the mirrored upper tile.
+template <int B>
+__global__ __launch_bounds__(256) void k_upd(double* __restrict__ A, int64_t lda, int r0, int m,
+                                             const double* __restrict__ Vx, const double* __restrict__ W) {
+  constexpr int K2 = 2 * B, LD = K2 + 2;
+  __shared__ double Ls[64 * LD];
+  __shared__ double Rs[64 * LD];
+  __shared__ double Ot[64][65];
+  const int L = blockIdx.x;
+  int ti = (int)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
+  while ((ti + 1) * (ti + 2) / 2 <= L) ++ti;
+  while (ti * (ti + 1) / 2 > L) --ti;
+  const int tj = L - ti * (ti + 1) / 2;
+  const int i0 = ti * 64, j0 = tj * 64;
+  const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int e = t; e < 64 * K2; e += 256) {
+    const int r = e / K2, k = e % K2;
+    const int gi = i0 + r, gj = j0 + r;
+    // L row i = [V_i, W_i], R row j = [W_j, V_j]: sum_k L_ik R_jk = V_i.W_j + W_i.V_j
+    Ls[r * LD + k] = gi < m ? (k < B ? Vx[(int64_t)gi * B + k] : W[(int64_t)gi * B + k - B]) : 0.0;
+    Rs[r * LD + k] = gj < m ? (k < B ? W[(int64_t)gj * B + k] : Vx[(int64_t)gj * B + k - B]) : 0.0;
+  }
+  __syncthreads();
+  f64x4 acc[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) acc[c] = (f64x4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+  for (int kk = 0; kk < K2; kk += 4) {
+    const double a = Ls[(16 * wv + fr) * LD + kk + fk];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const double b = Rs[(16 * c + fr) * LD + kk + fk];
+      acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[c], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int li = 16 * wv + fk + 4 * reg, lj = 16 * c + fr;
+      const int gi = i0 + li, gj = j0 + lj;
+      double v = 0.0;
+      if (gi < m && gj < m) {
+        double* p = A + (int64_t)(r0 + gi) * lda + r0 + gj;
+        v = *p - acc[c][reg];
+        if (ti > tj || lj <= li) *p = v;
+      }
+      Ot[li][lj] = v;
+    }
+  if (ti == tj) {
+    __syncthreads();
+    // diagonal tile: the upper half from the lower half (exact symmetry)
+    for (int e = t; e < 64 * 64; e += 256) {
+      const int li = e / 64, lj = e % 64;
+      const int gi = i0 + li, gj = j0 + lj;
+      if (lj > li && gi < m && gj < m) A[(int64_t)(r0 + gi) * lda + r0 + gj] = Ot[lj][li];
+    }
+    return;
+  }
+  __syncthreads();
+  for (int e = t; e < 64 * 64; e += 256) {
+    const int li = e / 64, lj = e % 64;  // upper tile element (j0 + li, i0 + lj) = lower (i0 + lj, j0 + li)
+    const int gi = j0 + li, gj = i0 + lj;
+    if (gi < m && gj < m) A[(int64_t)(r0 + gi) * lda + r0 + gj] = Ot[lj][li];
+  }
+}
+
+// Band storage: band[c * LDB + d] = A[c + d][c], d in [0, LDB) (LDB = 2B: the band plus the
+// bulge space of stage 2).
+template <int B>
+__global__ void k_band(const double* __restrict__ A, int64_t lda, int n, double* __restrict__ band) {
+  constexpr int LDB = 2 * B;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)n * LDB) return;
+  const int c = (int)(e / LDB), d = (int)(e % LDB);
+  band[e] = (d <= B && c + d < n) ? A[(int64_t)(c + d) * lda + c] : 0.0;
+}
+
+// ---------------------------------------------------------------------------------------
+// Stage 2: k_sbtrd<B>.  One wave per workgroup; workgroup g runs sweeps g, g + NG, ...
+// Task (s, k): rows R_k = [r0, r1), r0 = s+1+k*B (k = 0: the column s itself is the target);
+// the Householder annihilates A[r0+1:r1, col] (col = s for k = 0, else the first column of
+// the previous bulge, s+1+(k-1)*B) and is applied to A[R_k, col:r0] (left), A[R_k, R_k]
+// (both sides) and A[r1:r1+B, R_k] (right; the new bulge).  prog[s] counts finished tasks of
+// sweep s (0x7fffffff when done); task (s, k) waits for prog[s-1] >= k + 3.
+// Band entries are read and written with agent-scope (L2-bypassing) accesses: the tasks of
+// one region run on different CUs one after another.
+// ---------------------------------------------------------------------------------------
+template <int B>
+__global__ __launch_bounds__(64, 1) void k_sbtrd(double* __restrict__ band, int n, int NG,
+                                                 uint32_t* __restrict__ prog, uint32_t* __restrict__ abortw) {
+  static_assert(B == 32, "k_sbtrd maps a 32 x 32 block onto one wave (lane = column, half of the rows)");
+  constexpr int LDB = 2 * B, H = B / 2;
+  constexpr uint32_t DONE = 0x7fffffffu;
+  __shared__ double Ds[B][B + 1];  // the diagonal block, both triangles
+  __shared__ double vs[B];
+  const int lane = threadIdx.x, c = lane & (B - 1), h = lane >> 5;
+  auto idx = [&](int r, int cc) -> int { return cc * LDB + (r - cc); };
+  const __amdgpu_buffer_rsrc_t rb = rsrc(band, (int64_t)n * LDB);
+  // lane (c, h) holds rows [16h, 16h+16) of column c of each block:
+  //   L[i][c] (rows R_k, column col + c), D[i][c] (column r0 + c), R[c][j] (row r1 + c, j in its half)
+  for (int s = blockIdx.x; s < n - 2; s += NG) {
+    for (int k = 0;; ++k) {
+      const int r0 = s + 1 + k * B;
+      if (r0 >= n - 1) break;
+      const int r1 = min(r0 + B, n), len = r1 - r0;
+      const int col = k == 0 ? s : s + 1 + (k - 1) * B;
+      const int nl = r0 - col;
+      const int r2 = min(r1 + B, n), nr = r2 - r1;
+      if (s > 0 && lane == 0) {
+        int spin = 0;
+        for (;;) {
+          const uint32_t p = ld_f(prog + s - 1);
+          if (p == DONE || p >= (uint32_t)(k + 3)) break;
+          if (++spin > SPIN_LIMIT) {
+            st_f(abortw, 1u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      // ---- loads (all issued, one wait) -------------------------------------------------
+      double L[H], D[H], R[H];
+#pragma unroll
+      for (int q = 0; q < H; ++q) {
+        const int i = H * h + q;
+        L[q] = (c < nl && i < len) ? bld(rb, idx(r0 + i, col + c)) : 0.0;
+        D[q] = (c < len && i < len && i >= c) ? bld(rb, idx(r0 + i, r0 + c)) : 0.0;
+        R[q] = (c < nr && i < len) ? bld(rb, idx(r1 + c, r0 + i)) : 0.0;  // R[c][j = i]
+      }
+#pragma unroll
+      for (int q = 0; q < H; ++q) {  // the upper triangle of D from the lower one
+        const int i = H * h + q;
+        if (i >= c) Ds[i][c] = D[q];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int q = 0; q < H; ++q) {
+        const int i = H * h + q;
+        if (i < c && c < len) D[q] = Ds[c][i];
+      }
+      // ---- Householder of x = L[:, 0] (column col) --------------------------------------
+      const double x0 = __shfl(L[0], 0);  // lane 0 = (c 0, h 0): row 0
+      double sq = 0.0;
+      if (c == 0) {
+#pragma unroll
+        for (int q = 0; q < H; ++q) {
+          const int i = H * h + q;
+          if (i >= 1) sq = fma(L[q], L[q], sq);
+        }
+      }
+      sq += __shfl_xor(sq, 32);
+      sq = __shfl(sq, 0);
+      double beta = x0, tau = 0.0, scal = 0.0;
+      if (sq != 0.0) {
+        beta = -copysign(sqrt(fma(x0, x0, sq)), x0);
+        tau = (beta - x0) / beta;
+        scal = 1.0 / (x0 - beta);
+      }
+      if (c == 0) {
+#pragma unroll
+        for (int q = 0; q < H; ++q) {
+          const int i = H * h + q;
+          if (i < len) vs[i] = i == 0 ? 1.0 : L[q] * scal;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      double v[H];
+#pragma unroll
+      for (int q = 0; q < H; ++q) {
+        const int i = H * h + q;
+        v[q] = i < len ? vs[i] : 0.0;
+      }
+      // ---- left: column c of rows R_k -----------------------------------------------------
+      {
+        double d = 0.0;
+#pragma unroll
+        for (int q = 0; q < H; ++q) d = fma(v[q], L[q], d);
+        d += __shfl_xor(d, 32);
+        const double f = tau * d;
+#pragma unroll
+        for (int q = 0; q < H; ++q) {
+          const int i = H * h + q;
+          L[q] = c == 0 ? (i == 0 ? beta : 0.0) : fma(-f, v[q], L[q]);
+        }
+      }
+      // ---- both sides on D: p = tau D v, w = p - 1/2 tau (p.v) v, D -= v w^T + w v^T -------
+      {
+        // p_c = tau sum_i D[i][c] v_i (D symmetric: column c = row c)
+        double pc = 0.0;
+#pragma unroll
+        for (int q = 0; q < H; ++q) pc = fma(D[q], v[q], pc);
+        pc += __shfl_xor(pc, 32);
+        pc *= tau;
+        const double vc = c < len ? vs[c] : 0.0;
+        double pv = h == 0 ? pc * vc : 0.0;
+        for (int o = 16; o >= 1; o >>= 1) pv += __shfl_xor(pv, o);
+        pv += __shfl_xor(pv, 32);
+        const double wc = fma(-0.5 * tau * pv, vc, pc);  // w_c
+        if (h == 0 && c < len) Ds[0][c] = wc;             // reuse row 0 of Ds as the w vector
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < H; ++q) {
+          const int i = H * h + q;
+          const double wi = i < len ? Ds[0][i] : 0.0;
+          D[q] = D[q] - v[q] * wc - wi * vc;
+        }
+      }
+      // ---- right: row r1 + c times H: R[c][j] -= tau (R[c] . v) v_j ------------------------
+      {
+        double d = 0.0;
+#pragma unroll
+        for (int q = 0; q < H; ++q) d = fma(R[q], v[q], d);
+        d += __shfl_xor(d, 32);
+        const double f = tau * d;
+#pragma unroll
+        for (int q = 0; q < H; ++q) R[q] = fma(-f, v[q], R[q]);
+      }
+      // ---- stores (lower triangle of D) -------------------------------------------------
+#pragma unroll
+      for (int q = 0; q < H; ++q) {
+        const int i = H * h + q;
+        if (c < nl && i < len) bst(rb, idx(r0 + i, col + c), L[q]);
+        if (c < len && i < len && i >= c) bst(rb, idx(r0 + i, r0 + c), D[q]);
+        if (c < nr && i < len) bst(rb, idx(r1 + c, r0 + i), R[q]);
+      }
+      drain();
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) st_f(prog + s, (uint32_t)(k + 1));
+    }
+    drain();
+    if (lane == 0) st_f(prog + s, DONE);
+  }
+}
+
+// D, E of the reduced band (band[c*LDB + 0], band[c*LDB + 1]).
+template <int B>
+__global__ void k_tri_out(const double* __restrict__ band, int n, double* __restrict__ D, double* __restrict__ E) {
+  constexpr int LDB = 2 * B;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  D[c] = ld_c(band + (int64_t)c * LDB);
+  if (c < n - 1) E[c] = ld_c(band + (int64_t)c * LDB + 1);
+}
+
+// ---------------------------------------------------------------------------------------
+// Inverse iteration on the band matrix Bm (the stage-1 band, lower bandwidth B, in `band`
+// before stage 2 ran -- a separate copy) for lam_desc[k], one workgroup per eigenvalue.
+// LU with partial pivoting of Bm - lam I (dgbtrf: kl = B, ku = 2B after the row swaps),
+// kept as U rows (n x (2B+1)) and L multipliers (n x B) + pivots in the workspace; the
+// active (B+1) x (2B+1) window lives in LDS.  Two solves from a fixed start vector
+// (dstein's), normalised.
+// ---------------------------------------------------------------------------------------
+template <int B>
+__global__ __launch_bounds__(256) void k_band_invit(const double* __restrict__ bnd, int n,
+                                                    const double* __restrict__ lam_desc,
+                                                    double* __restrict__ work, int* __restrict__ ipiv_all,
+                                                    double* __restrict__ Y, int ldy) {
+  static_assert(2 * B <= 64, "the backward solve keeps 2B values in one wave");
+  constexpr int LDB = 2 * B, KU = 2 * B, WC = KU + 1, WR = B + 1;
+  // circular window: matrix row j+r in row slot (j+r) % WR, column j+c in slot (j+c) % WC
+  __shared__ double win[WR][WC + 1];
+  __shared__ double lmul[WR];
+  __shared__ int piv_i;
+  __shared__ double red[8];
+  const int k = blockIdx.x, t = threadIdx.x;
+  const double lam = lam_desc[k];
+  double* U = work + (int64_t)k * n * (WC + B + 1);  // n x WC, then L (n x B), then x (n)
+  double* Lm = U + (int64_t)n * WC;
+  double* x = Lm + (int64_t)n * B;
+  int* ipiv = ipiv_all + (int64_t)k * n;
+  auto bval = [&](int i, int j) -> double {  // (Bm - lam I)[i][j]
+    if (i < 0 || j < 0 || i >= n || j >= n) return 0.0;
+    const int d = i - j;
+    if (d > B || d < -B) return 0.0;
+    const double v = d >= 0 ? bnd[(int64_t)j * LDB + d] : bnd[(int64_t)i * LDB - d];
+    return i == j ? v - lam : v;
+  };
+  double nrm = 0.0;
+  for (int e = t; e < n; e += 256) nrm = fmax(nrm, fabs(bnd[(int64_t)e * LDB]) + 2.0 * fabs(bnd[(int64_t)e * LDB + 1]));
+  for (int o = 32; o >= 1; o >>= 1) nrm = fmax(nrm, __shfl_xor(nrm, o));
+  if ((t & 63) == 0) red[t >> 6] = nrm;
+  __syncthreads();
+  nrm = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+  const double floor_ = 2.220446049250313e-16 * fmax(nrm, 1e-300);
+  for (int e = t; e < WR * WC; e += 256) {
+    const int r = e / WC, c = e % WC;
+    win[r][c] = bval(r, c);
+  }
+  __syncthreads();
+  for (int j = 0; j < n; ++j) {
+    const int nrow = min(B, n - 1 - j);
+    const int sj = j % WR, cj = j % WC;
+    // the row entering at the end of this step (independent of the elimination): load now
+    const double nrv = t < WC ? bval(j + 1 + B, j + 1 + t) : 0.0;
+    if (t < 64) {
+      double best = -1.0;
+      int bi = 0;
+      if (t <= nrow) {
+        best = fabs(win[(j + t) % WR][cj]);
+        bi = t;
+      }
+      for (int o = 32; o >= 1; o >>= 1) {
+        const double ob = __shfl_xor(best, o);
+        const int oi = __shfl_xor(bi, o);
+        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+      }
+      if (t == 0) piv_i = bi;
+    }
+    __syncthreads();
+    const int pr = piv_i;
+    const int sp = (j + pr) % WR;
+    if (pr != 0 && t < WC) {
+      const double a = win[sj][t];
+      win[sj][t] = win[sp][t];
+      win[sp][t] = a;
+    }
+    __syncthreads();
+    double d0 = win[sj][cj];
+    if (fabs(d0) < floor_) d0 = d0 < 0.0 ? -floor_ : floor_;
+    if (t >= 1 && t <= nrow) lmul[t] = win[(j + t) % WR][cj] / d0;
+    if (t < WC) U[(int64_t)j * WC + t] = t == 0 ? d0 : win[sj][(j + t) % WC];
+    if (t == 0) ipiv[j] = j + pr;
+    __syncthreads();
+    if (t < B) Lm[(int64_t)j * B + t] = (t + 1 <= nrow) ? lmul[t + 1] : 0.0;
+    for (int e = t; e < nrow * KU; e += 256) {
+      const int r = 1 + e / KU, c = 1 + e % KU;
+      const int sr = (j + r) % WR, sc = (j + c) % WC;
+      win[sr][sc] = fma(-lmul[r], win[sj][sc], win[sr][sc]);
+    }
+    __syncthreads();
+    // row j leaves: its slot takes matrix row j+1+B; column slot cj becomes column j+1+2B
+    if (t < WC) win[sj][(j + 1 + t) % WC] = nrv;
+    if (t >= 1 && t <= B) win[(j + t) % WR][cj] = 0.0;
+    __syncthreads();
+  }
+  // ---- two solves from a pseudo-random start (dlarnv-like), one wave, register windows ---
+  for (int e = t; e < n; e += 256) {
+    uint32_t hh = (uint32_t)e * 2654435761u ^ 0x9e3779b9u;
+    hh ^= hh >> 15; hh *= 2246822519u; hh ^= hh >> 13; hh *= 3266489917u; hh ^= hh >> 16;
+    x[e] = (double)hh * (2.0 / 4294967296.0) - 1.0;
+  }
+  __syncthreads();
+  for (int it = 0; it < 2; ++it) {
+    if (t < 64) {
+      const int lane = t;
+      // forward: lanes 0..B hold x[j..j+B] (lane 0 = x[j])
+      double wv = lane <= B && lane < n ? x[lane] : 0.0;
+      for (int j = 0; j < n; ++j) {
+        const int p = ipiv[j] - j;
+        const double v0 = __shfl(wv, 0), vp = __shfl(wv, p);
+        if (lane == 0) wv = vp;
+        if (lane == p) wv = v0;
+        const double xj = __shfl(wv, 0);
+        if (lane >= 1 && lane <= B) wv = fma(-Lm[(int64_t)j * B + lane - 1], xj, wv);
+        if (lane == 0) x[j] = xj;
+        const double nxt = __shfl_down(wv, 1);
+        wv = lane < B ? nxt : ((j + 1 + B < n) ? x[j + 1 + B] : 0.0);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      // backward: lanes 0..2B-1 hold x[j+1..j+2B]
+      double wb = 0.0;
+      for (int j = n - 1; j >= 0; --j) {
+        const double uj = (j + 1 + lane < n) ? U[(int64_t)j * WC + 1 + lane] : 0.0;
+        double sdot = uj * wb;
+        for (int o = 32; o >= 1; o >>= 1) sdot += __shfl_xor(sdot, o);
+        const double xj = (x[j] - sdot) / U[(int64_t)j * WC];
+        if (lane == 0) x[j] = xj;
+        const double up = __shfl_up(wb, 1);
+        wb = lane == 0 ? xj : up;
+      }
+    }
+    __syncthreads();
+    double mx = 0.0;
+    for (int e = t; e < n; e += 256) mx = fmax(mx, fabs(x[e]));
+    for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+    if ((t & 63) == 0) red[t >> 6] = mx;
+    __syncthreads();
+    mx = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+    __syncthreads();
+    double ss = 0.0;
+    for (int e = t; e < n; e += 256) {
+      const double v = x[e] / mx;
+      ss = fma(v, v, ss);
+    }
+    for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
+    if ((t & 63) == 0) red[4 + (t >> 6)] = ss;
+    __syncthreads();
+    const double nrm2 = sqrt(red[4] + red[5] + red[6] + red[7]);
+    for (int e = t; e < n; e += 256) x[e] = x[e] / mx / nrm2;
+    __syncthreads();
+  }
+  for (int e = t; e < n; e += 256) Y[(int64_t)e * ldy + k] = x[e];
+}
+
+// Back-transformation Y[r0:] <- Q_p Y[r0:] = Y - Vx (T (Vx^T Y)), panels applied last first.
+// k_bt_z: partial Vx^T Y over row chunks -> Zp; k_bt_u: Z = sum, Z2 = T Z, Y -= Vx Z2.
+template <int B>
+__global__ __launch_bounds__(256) void k_bt_z(const double* __restrict__ Vx, const double* __restrict__ Y, int ldy,
+                                              int r0, int m, int nvec, int chunk, double* __restrict__ Zp) {
+  // thread (a = column of V, g = row group of 256/B): partial sums over rows r = g (mod 256/B)
+  // of V[r][a] * Y[r][c] for every c (nvec <= 64 accumulators), then an LDS reduction
+  constexpr int RG = 256 / B;
+  __shared__ double red[RG][B][65];
+  const int t = threadIdx.x, a = t % B, g = t / B;
+  const int a0 = blockIdx.x * chunk, a1 = min(m, a0 + chunk);
+  double acc[64];
+#pragma unroll
+  for (int c = 0; c < 64; ++c) acc[c] = 0.0;
+  for (int r = a0 + g; r < a1; r += RG) {
+    const double v = Vx[(int64_t)r * B + a];
+    const double* yr = Y + (int64_t)(r0 + r) * ldy;
+#pragma unroll
+    for (int c = 0; c < 64; ++c)
+      if (c < nvec) acc[c] = fma(v, yr[c], acc[c]);
+  }
+#pragma unroll
+  for (int c = 0; c < 64; ++c)
+    if (c < nvec) red[g][a][c] = acc[c];
+  __syncthreads();
+  for (int e = t; e < B * nvec; e += 256) {
+    const int aa = e / nvec, c = e % nvec;
+    double s2 = 0.0;
+    for (int q = 0; q < RG; ++q) s2 += red[q][aa][c];
+    Zp[(int64_t)blockIdx.x * B * nvec + e] = s2;
+  }
+}
+
+template <int B>
+__global__ __launch_bounds__(256) void k_bt_t(const double* __restrict__ T, const double* __restrict__ Zp, int nz,
+                                              int nvec, double* __restrict__ Z2) {
+  extern __shared__ double shz[];
+  double* Z = shz;  // B x nvec
+  const int t = threadIdx.x;
+  for (int e = t; e < B * nvec; e += 256) {
+    double s = 0.0;
+    for (int q = 0; q < nz; ++q) s += Zp[(int64_t)q * B * nvec + e];
+    Z[e] = s;
+  }
+  __syncthreads();
+  for (int e = t; e < B * nvec; e += 256) {
+    const int a = e / nvec, c = e % nvec;
+    double s = 0.0;
+    for (int l = a; l < B; ++l) s = fma(T[a * B + l], Z[l * nvec + c], s);  // T upper
+    Z2[e] = s;
+  }
+}
+
+template <int B>
+__global__ __launch_bounds__(256) void k_bt_u(const double* __restrict__ Vx, const double* __restrict__ Z2g,
+                                              double* __restrict__ Y, int ldy, int r0, int m, int nvec) {
+  extern __shared__ double shz[];
+  double* Z2 = shz;  // B x nvec
+  const int t = threadIdx.x;
+  for (int e = t; e < B * nvec; e += 256) Z2[e] = Z2g[e];
+  __syncthreads();
+  const int64_t tot = (int64_t)m * nvec;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + t; e < tot; e += (int64_t)gridDim.x * 256) {
+    const int r = (int)(e / nvec), c = (int)(e % nvec);
+    double s = Y[(int64_t)(r0 + r) * ldy + c];
+    for (int l = 0; l < B; ++l) s = fma(-Vx[(int64_t)r * B + l], Z2[l * nvec + c], s);
+    Y[(int64_t)(r0 + r) * ldy + c] = s;
+  }
+}
+
+}  // namespace sb
+
+// ---------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------
+int sy2sb_band() { return 32; }
+int syev2_max_n() { return 8192; }
+
+size_t sy2sb_work_doubles(int n, int nvec, SyevdPlan* plan) {
+  constexpr int B = 32;
+  SyevdPlan p{};
+  p.B = B;
+  p.np = 0;
+  int64_t vx = 0;
+  for (int c0 = 0; c0 < n - B - 1; c0 += B) {
+    vx += (int64_t)(n - c0 - B) * B;
+    ++p.np;
+  }
+  p.KS = 4;
+  p.NZ = 16;
+  p.RP = 256;
+  const int64_t nn = (int64_t)n * n;
+  p.off_aw = 0;
+  p.off_vx = p.off_aw + nn;
+  p.off_t = p.off_vx + vx;
+  p.off_tau = p.off_t + (int64_t)std::max(p.np, 1) * B * B;
+  p.off_y = p.off_tau + (int64_t)std::max(p.np, 1) * B;
+  p.off_x = p.off_y + (int64_t)p.KS * n * B;
+  p.off_w = p.off_x + (int64_t)n * B;
+  p.off_zp = p.off_w + (int64_t)n * B;
+  p.off_m = p.off_zp + (int64_t)std::max<int64_t>(p.NZ * B * B, (int64_t)p.NZ * B * std::max(nvec, 1));
+  p.off_pub = p.off_m + (int64_t)B * std::max(B, nvec);
+  p.off_band = p.off_pub + 2LL * 64 * 2 * B;
+  p.off_band0 = p.off_band + (int64_t)n * 2 * B;
+  p.off_de = p.off_band0 + (int64_t)n * 2 * B;
+  p.off_inv = p.off_de + 4LL * n + 8;
+  p.off_end = p.off_inv + (int64_t)std::max(nvec, 1) * ((int64_t)n * (2 * B + 1 + B) + n);
+  if (plan) *plan = p;
+  return (size_t)p.off_end;
+}
+
+hipError_t launch_syevd2(const double* C, int n, int nvec, double* ws, const SyevdPlan& p, uint32_t* flags,
+                         uint32_t epoch, int* ipiv, int* grid_cnt, double* lam_desc, double* vec, hipStream_t st) {
+  constexpr int B = 32;
+  double* Aw = ws + p.off_aw;
+  hipError_t e = hipMemcpyAsync(Aw, C, (size_t)n * n * sizeof(double), hipMemcpyDeviceToDevice, st);
+  if (e != hipSuccess) return e;
+  uint32_t* pflags = flags;        // 64 panel-QR flags
+  uint32_t* abortw = flags + 64;   // [0] panel QR, [1] stage 2
+  uint32_t* prog = flags + 128;    // n sweep counters
+  e = hipMemsetAsync(prog, 0, (size_t)n * sizeof(uint32_t), st);
+  if (e != hipSuccess) return e;
+  int64_t vxo = 0;
+  int pi = 0;
+  const char* lim = std::getenv("PODS_SY2SB_PANELS");  // diagnostics: stop stage 1 early
+  const int maxp = lim ? std::atoi(lim) : 1 << 30;
+  for (int c0 = 0; c0 < n - B - 1 && pi < maxp; c0 += B, ++pi) {
+    const int r0 = c0 + B, m = n - r0;
+    double* Vx = ws + p.off_vx + vxo;
+    double* T = ws + p.off_t + (int64_t)pi * B * B;
+    double* tau = ws + p.off_tau + (int64_t)pi * B;
+    const int NW = std::max(1, std::min(64, (m + p.RP - 1) / p.RP));
+    const int RP = (m + NW - 1) / NW;
+    hipLaunchKernelGGL(sb::k_pqr<B>, dim3(NW), dim3(256), 0, st, Aw, (int64_t)n, r0, c0, m, RP, NW,
+                       ws + p.off_pub, pflags, epoch * 1024u + (uint32_t)pi, abortw, Vx, tau, ws + p.off_zp, T);
+    const int kchunk = ((m + p.KS - 1) / p.KS + 31) / 32 * 32;
+    hipLaunchKernelGGL(sb::k_ay<B>, dim3((m + 63) / 64, p.KS), dim3(256), 0, st, Aw, (int64_t)n, r0, m, Vx,
+                       kchunk, ws + p.off_y);
+    hipLaunchKernelGGL(sb::k_xt<B>, dim3((m + 256 / B - 1) / (256 / B)), dim3(256), 0, st, ws + p.off_y, p.KS, m,
+                       T, ws + p.off_x);
+    const int zchunk = (m + p.NZ - 1) / p.NZ;
+    hipLaunchKernelGGL(sb::k_z<B>, dim3(p.NZ), dim3(256), 0, st, Vx, ws + p.off_x, m, zchunk, ws + p.off_zp);
+    hipLaunchKernelGGL(sb::k_zm<B>, dim3(1), dim3(256), 0, st, ws + p.off_zp, p.NZ, T, ws + p.off_m);
+    hipLaunchKernelGGL(sb::k_w<B>, dim3((m + 256 / B - 1) / (256 / B)), dim3(256), 0, st, ws + p.off_x, Vx,
+                       ws + p.off_m, m, ws + p.off_w);
+    const int tiles = (m + 63) / 64;
+    hipLaunchKernelGGL(sb::k_upd<B>, dim3(tiles * (tiles + 1) / 2), dim3(256), 0, st, Aw, (int64_t)n, r0, m, Vx,
+                       ws + p.off_w);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    vxo += (int64_t)m * B;
+  }
+  double* band = ws + p.off_band;
+  double* band0 = ws + p.off_band0;
+  const int64_t nb = (int64_t)n * 2 * B;
+  hipLaunchKernelGGL(sb::k_band<B>, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, Aw, (int64_t)n, n, band);
+  e = hipMemcpyAsync(band0, band, (size_t)nb * sizeof(double), hipMemcpyDeviceToDevice, st);
+  if (e != hipSuccess) return e;
+  const int NG = std::max(1, std::min(256, n - 2));
+  if (n > 2) hipLaunchKernelGGL(sb::k_sbtrd<B>, dim3(NG), dim3(64), 0, st, band, n, NG, prog, abortw + 1);
+  double* D = ws + p.off_de;
+  double* E = D + n;
+  double* bounds = D + 2 * (int64_t)n;
+  hipLaunchKernelGGL(sb::k_tri_out<B>, dim3((n + 255) / 256), dim3(256), 0, st, band, n, D, E);
+  e = launch_tri_eigvals(D, E, n, bounds, lam_desc, grid_cnt, st);
+  if (e != hipSuccess || nvec <= 0) return e;
+  double* inv = ws + p.off_inv;
+  hipLaunchKernelGGL(sb::k_band_invit<B>, dim3(nvec), dim3(256), 0, st, band0, n, lam_desc, inv, ipiv, vec, nvec);
+  e = launch_orth(lam_desc, bounds, n, nvec, vec, nvec, st);
+  if (e != hipSuccess) return e;
+  // Y <- Q_0 Q_1 ... Q_{np-1} Y
+  if (std::getenv("PODS_SY2SB_NOBT")) return hipGetLastError();  // diagnostics: band eigenvectors
+  for (int q = p.np - 1; q >= 0; --q) {
+    int64_t off = 0;
+    for (int r = 0; r < q; ++r) off += (int64_t)(n - r * B - B) * B;
+    const int r0 = q * B + B, m = n - r0;
+    const double* Vx = ws + p.off_vx + off;
+    const double* T = ws + p.off_t + (int64_t)q * B * B;
+    const int nz = std::min(p.NZ, std::max(1, m / 256));
+    const int chunk = (m + nz - 1) / nz;
+    hipLaunchKernelGGL(sb::k_bt_z<B>, dim3(nz), dim3(256), 0, st, Vx, vec, nvec, r0, m, nvec, chunk, ws + p.off_zp);
+    const size_t lds = (size_t)B * nvec * sizeof(double);
+    hipLaunchKernelGGL(sb::k_bt_t<B>, dim3(1), dim3(256), lds, st, T, ws + p.off_zp, nz, nvec, ws + p.off_m);
+    const int gu = std::max(1, std::min(512, (int)(((int64_t)m * nvec + 255) / 256)));
+    hipLaunchKernelGGL(sb::k_bt_u<B>, dim3(gu), dim3(256), lds, st, Vx, ws + p.off_m, vec, nvec, r0, m, nvec);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace pods

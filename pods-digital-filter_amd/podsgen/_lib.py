@@ -55,6 +55,9 @@ SIGNATURES = {
     "pods_syev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "pods_sytrd": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "pods_syev_status": (c_int, [c_void_p]),
+    "pods_syev2": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "pods_syev2_status": (c_int, [c_void_p]),
+    "pods_syev2_inspect": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_i64]),
     "pods_sytrd_trace": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "pods_spatial_modes": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "pods_fourier": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_dbl, c_void_p]),

@@ -10,11 +10,12 @@ Multi-GPU: one process per GPU.  Each rank owns a contiguous slab of inlet rows
 all_reduce (RCCL over xGMI with the "nccl" backend).  Rank 0 solves the eigenproblem
 and broadcasts lambda and T[:, :nm]; every rank then forms its slab of the spatial modes.
 
-Eigensolve: pods_syev (register-resident tridiagonalisation + bisection + inverse
-iteration, all eigenvalues and the nm leading vectors) whenever only the truncated temporal
-modes are needed (ns <= 4096, 0 <= nm <= 64); torch.linalg.eigh (rocSOLVER dsyevd) when the
-full temporal-mode matrix is requested (verbose output), for ns > 4096, or with
-PODS_EIGEN=torch.
+Eigensolve: pods_syev (register-resident tridiagonalisation + bisection + twisted
+factorisation, all eigenvalues and the nm leading vectors) whenever only the truncated
+temporal modes are needed (ns <= 4096, 0 <= nm <= 64); pods_syev2 (two-stage: band
+reduction on fp64 MFMA, bulge chasing, bisection, band inverse iteration) for
+4096 < ns <= 8192; torch.linalg.eigh (rocSOLVER dsyevd) when the full temporal-mode matrix
+is requested (verbose output), beyond 8192, or with PODS_EIGEN=torch.
 
 PyTorch is used for device memory, the stream, torch.distributed and that fallback
 eigensolve -- nothing else.
@@ -194,6 +195,7 @@ def allreduce_correlation(dist, C, ns, divide):
 
 
 SYEV_MAX_N = 4096   # pods_syev's on-chip limit (trd_plan)
+SYEV2_MAX_N = 8192  # pods_syev2 (two-stage): the bisection's LDS limit
 SYEV_MAX_VEC = 64
 
 
@@ -205,20 +207,25 @@ def eigen_modes(ctx: Context, C, ns, nm, tol_CN, full_temporal, tm=None):
     tm = tm or (lambda name: _NullCtx())
     lib, dev = ctx.lib, C.device
     method = os.environ.get("PODS_EIGEN", "auto")
-    if method not in ("auto", "pods", "torch"):
-        raise ValueError("PODS_EIGEN must be auto, pods or torch")
+    if method not in ("auto", "pods", "pods2", "torch"):
+        raise ValueError("PODS_EIGEN must be auto, pods, pods2 or torch")
     nvec = max(min(nm, ns), 1) if nm >= 0 else ns
-    use_pods = (method != "torch" and not full_temporal and ns <= SYEV_MAX_N
-                and nvec <= SYEV_MAX_VEC)
-    if method == "pods" and not use_pods:
-        raise ValueError("PODS_EIGEN=pods needs ns <= %d, nm <= %d and truncated temporal modes"
-                         % (SYEV_MAX_N, SYEV_MAX_VEC))
-    if use_pods:
+    fits = not full_temporal and nvec <= SYEV_MAX_VEC
+    use_pods = method in ("auto", "pods") and fits and ns <= SYEV_MAX_N
+    use_pods2 = fits and 3 <= ns <= SYEV2_MAX_N and (method == "pods2" or (method == "auto" and not use_pods))
+    if method in ("pods", "pods2") and not (use_pods or use_pods2):
+        raise ValueError("PODS_EIGEN=%s needs ns <= %d, nm <= %d and truncated temporal modes"
+                         % (method, SYEV_MAX_N if method == "pods" else SYEV2_MAX_N, SYEV_MAX_VEC))
+    if use_pods or use_pods2:
         lam_t = torch.empty(ns, dtype=torch.float64, device=dev)
         Y = torch.empty((ns, nvec), dtype=torch.float64, device=dev)
         with tm("eigh"):
-            check(lib.pods_syev(ctx.h, ptr(C), ns, nvec, ptr(lam_t), ptr(Y)), "pods_syev")
-            check(lib.pods_syev_status(ctx.h), "pods_syev")
+            if use_pods:
+                check(lib.pods_syev(ctx.h, ptr(C), ns, nvec, ptr(lam_t), ptr(Y)), "pods_syev")
+                check(lib.pods_syev_status(ctx.h), "pods_syev")
+            else:  # two-stage (band reduction + bulge chasing) beyond the on-chip limit
+                check(lib.pods_syev2(ctx.h, ptr(C), ns, nvec, ptr(lam_t), ptr(Y)), "pods_syev2")
+                check(lib.pods_syev2_status(ctx.h), "pods_syev2")
             lam_desc = lam_t.cpu().numpy()
         nvalid = num_valid_modes(lam_desc, ns, tol_CN)
         nmt = nm if (0 <= nm <= nvalid) else nvalid
