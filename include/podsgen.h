@@ -151,10 +151,10 @@ int pods_sytrd_trace(pods_ctx* ctx, const double* C_dev, int n, int wg, int64_t*
 int pods_syev_status(pods_ctx* ctx);
 
 /* Two-stage eigensolver for correlation matrices beyond pods_syev's on-chip limit (BASELINE
- * configs 4/5, PODFS.py:1309-1310 at ns = 8192): dense -> band (bandwidth 32, fp64 MFMA
+ * configs 4/5, PODFS.py:1309-1310 at ns = 8192, 16384): dense -> band (bandwidth 32, fp64 MFMA
  * blocked updates), band -> tridiagonal (bulge chasing), bisection, inverse iteration on the
  * band matrix, back-transformation.  Same arguments and outputs as pods_syev; 3 <= n <=
- * 8192, nvec <= 64.  Asynchronous on the bound stream; pods_syev2_status reports a hand-off
+ * 16384, nvec <= 64.  Asynchronous on the bound stream; pods_syev2_status reports a hand-off
  * timeout after the stream has drained. */
 int pods_syev2(pods_ctx* ctx, const double* C_dev, int n, int nvec, double* lambda_desc_dev,
                double* vec_dev);

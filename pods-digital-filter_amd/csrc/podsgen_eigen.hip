@@ -660,14 +660,26 @@ __device__ __forceinline__ double grid_shift(int s, double gl, double gu) {
   return tn * exp2(-56.5 * (double)(2 * NSH - 1 - s) / (double)NSH);  // ascending in s
 }
 
+// {d_i, e_{i-1}^2} in global memory for tridiagonals too long for LDS (n > 10240)
+__global__ void k_de_fill(const double* __restrict__ D, const double* __restrict__ E, int n,
+                          double2* __restrict__ deg) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double e = i > 0 ? E[i - 1] : 0.0;
+  deg[i] = make_double2(D[i], e * e);
+}
+
 __global__ __launch_bounds__(256) void k_sturm_grid(const double* __restrict__ D,
                                                     const double* __restrict__ E, int n,
                                                     const double* __restrict__ bounds,
-                                                    int* __restrict__ cnt) {
-  extern __shared__ double2 de[];
-  for (int i = threadIdx.x; i < n; i += 256) {
-    const double e = i > 0 ? E[i - 1] : 0.0;
-    de[i] = make_double2(D[i], e * e);
+                                                    int* __restrict__ cnt, const double2* __restrict__ deg) {
+  extern __shared__ double2 desh[];
+  const double2* de = deg ? deg : desh;
+  if (!deg) {
+    for (int i = threadIdx.x; i < n; i += 256) {
+      const double e = i > 0 ? E[i - 1] : 0.0;
+      desh[i] = make_double2(D[i], e * e);
+    }
   }
   __syncthreads();
   const int s = blockIdx.x * 256 + threadIdx.x;
@@ -705,12 +717,15 @@ __global__ __launch_bounds__(256) void k_bisect(const double* __restrict__ D,
                                                 const double* __restrict__ E, int n,
                                                 const double* __restrict__ bounds,
                                                 double* __restrict__ lam_desc, int k0, int k1,
-                                                const int* __restrict__ gcnt) {
-  extern __shared__ double2 de[];
+                                                const int* __restrict__ gcnt, const double2* __restrict__ deg) {
+  extern __shared__ double2 desh[];
+  const double2* de = deg ? deg : desh;
   const int t = threadIdx.x, lane = t & 63;
-  for (int i = t; i < n; i += 256) {
-    const double e = i > 0 ? E[i - 1] : 0.0;
-    de[i] = make_double2(D[i], e * e);
+  if (!deg) {
+    for (int i = t; i < n; i += 256) {
+      const double e = i > 0 ? E[i - 1] : 0.0;
+      desh[i] = make_double2(D[i], e * e);
+    }
   }
   __syncthreads();
   const double gl = bounds[0], gu = bounds[1], pivmin = bounds[2], atol = bounds[3];
@@ -1334,15 +1349,22 @@ hipError_t launch_tri_bounds(const double* D, const double* E, int n, double* bo
 // Eigenvalues with ascending indices [k0, k1) (written to lam_desc[n-1-k]); bounds from
 // launch_tri_bounds.
 hipError_t launch_tri_bisect(const double* D, const double* E, int n, const double* bounds,
-                             double* lam_desc, int k0, int k1, int* grid_cnt, hipStream_t st) {
+                             double* lam_desc, int k0, int k1, int* grid_cnt, hipStream_t st, double2* deg) {
   if (k1 <= k0) return hipSuccess;
-  const size_t lds = (size_t)n * sizeof(double2);
+  size_t lds = (size_t)n * sizeof(double2);
+  if (lds > 160 * 1024) {
+    if (!deg) return hipErrorInvalidValue;  // the caller must supply the global {d, e^2} array
+    hipLaunchKernelGGL(eig::k_de_fill, dim3((n + 255) / 256), dim3(256), 0, st, D, E, n, deg);
+    lds = 0;
+  } else {
+    deg = nullptr;
+  }
   if (grid_cnt) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&eig::k_sturm_grid),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(eig::k_sturm_grid, dim3(2 * eig::NSH / 256), dim3(256), lds, st, D, E, n, bounds,
-                       grid_cnt);
+                       grid_cnt, deg);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -1351,17 +1373,17 @@ hipError_t launch_tri_bisect(const double* D, const double* E, int n, const doub
   if (e != hipSuccess) return e;
   const int per = 256 / eig::BL;
   hipLaunchKernelGGL(eig::k_bisect, dim3((k1 - k0 + per - 1) / per), dim3(256), lds, st, D, E, n,
-                     bounds, lam_desc, k0, k1, grid_cnt);
+                     bounds, lam_desc, k0, k1, grid_cnt, deg);
   return hipGetLastError();
 }
 
 size_t tri_grid_bytes() { return (size_t)2 * eig::NSH * sizeof(int); }
 
 hipError_t launch_tri_eigvals(const double* D, const double* E, int n, double* bounds,
-                              double* lam_desc, int* grid_cnt, hipStream_t st) {
+                              double* lam_desc, int* grid_cnt, hipStream_t st, double2* deg) {
   hipError_t e = launch_tri_bounds(D, E, n, bounds, st);
   if (e != hipSuccess) return e;
-  return launch_tri_bisect(D, E, n, bounds, lam_desc, 0, n, grid_cnt, st);
+  return launch_tri_bisect(D, E, n, bounds, lam_desc, 0, n, grid_cnt, st, deg);
 }
 
 hipError_t launch_tri_eigvecs(const double* D, const double* E, int n, const double* lam_desc,

@@ -70,13 +70,15 @@ int trd_plan(int n, int* R, int* G, int64_t* slab_doubles);
 hipError_t launch_trd(const TrdArgs& a, int R, hipStream_t st);
 // bounds: 4 doubles {gl, gu, pivmin, atol}; lam_desc: n eigenvalues of T, descending
 // grid_cnt (tri_grid_bytes(), may be null): counts at shared shifts for the first brackets
+// deg: 2n doubles of scratch, needed when n > 10240 ({d, e^2} then live in global memory)
 hipError_t launch_tri_eigvals(const double* D, const double* E, int n, double* bounds,
-                              double* lam_desc, int* grid_cnt, hipStream_t st);
+                              double* lam_desc, int* grid_cnt, hipStream_t st, double2* deg = nullptr);
 size_t tri_grid_bytes();
 // the same in two parts: Gershgorin bounds, then the eigenvalues with ascending index [k0, k1)
 hipError_t launch_tri_bounds(const double* D, const double* E, int n, double* bounds, hipStream_t st);
 hipError_t launch_tri_bisect(const double* D, const double* E, int n, const double* bounds,
-                             double* lam_desc, int k0, int k1, int* grid_cnt, hipStream_t st);
+                             double* lam_desc, int k0, int k1, int* grid_cnt, hipStream_t st,
+                             double2* deg = nullptr);
 // Z: n x nvec row-major eigenvectors of T for lam_desc[0..nvec); X: nvec x n scratch
 hipError_t launch_tri_eigvecs(const double* D, const double* E, int n, const double* lam_desc,
                               const double* bounds, int nvec, double* X, double* Z, hipStream_t st);
@@ -94,10 +96,10 @@ hipError_t launch_orth(const double* lam_desc, const double* bounds, int n, int 
 struct SyevdPlan {
   int B, np, KS, NZ, RP;
   int64_t off_aw, off_vx, off_t, off_tau, off_y, off_x, off_w, off_zp, off_m, off_pub, off_band, off_band0,
-      off_de, off_inv, off_end;
+      off_de, off_deg, off_inv, off_end;
 };
 int sy2sb_band();
-int syev2_max_n();  // the bisection keeps the tridiagonal in LDS
+int syev2_max_n();  // k_pqr: 64 workgroups x 256 panel rows
 // doubles of workspace for n, nvec (and the offsets inside it)
 size_t sy2sb_work_doubles(int n, int nvec, SyevdPlan* plan);
 // flags: 128 + n uint32 (zeroed once at allocation); ipiv: nvec * n ints; epoch: a counter

@@ -902,7 +902,7 @@ __global__ __launch_bounds__(256) void k_bt_u(const double* __restrict__ Vx, con
 // host side
 // ---------------------------------------------------------------------------------------
 int sy2sb_band() { return 32; }
-int syev2_max_n() { return 8192; }
+int syev2_max_n() { return 16384; }
 
 size_t sy2sb_work_doubles(int n, int nvec, SyevdPlan* plan) {
   constexpr int B = 32;
@@ -931,7 +931,8 @@ size_t sy2sb_work_doubles(int n, int nvec, SyevdPlan* plan) {
   p.off_band = p.off_pub + 2LL * 64 * 2 * B;
   p.off_band0 = p.off_band + (int64_t)n * 2 * B;
   p.off_de = p.off_band0 + (int64_t)n * 2 * B;
-  p.off_inv = p.off_de + 4LL * n + 8;
+  p.off_deg = p.off_de + 4LL * n + 8;
+  p.off_inv = p.off_deg + 2LL * n + 2;
   p.off_end = p.off_inv + (int64_t)std::max(nvec, 1) * ((int64_t)n * (2 * B + 1 + B) + n);
   if (plan) *plan = p;
   return (size_t)p.off_end;
@@ -990,7 +991,7 @@ hipError_t launch_syevd2(const double* C, int n, int nvec, double* ws, const Sye
   double* E = D + n;
   double* bounds = D + 2 * (int64_t)n;
   hipLaunchKernelGGL(sb::k_tri_out<B>, dim3((n + 255) / 256), dim3(256), 0, st, band, n, D, E);
-  e = launch_tri_eigvals(D, E, n, bounds, lam_desc, grid_cnt, st);
+  e = launch_tri_eigvals(D, E, n, bounds, lam_desc, grid_cnt, st, reinterpret_cast<double2*>(ws + p.off_deg));
   if (e != hipSuccess || nvec <= 0) return e;
   double* inv = ws + p.off_inv;
   hipLaunchKernelGGL(sb::k_band_invit<B>, dim3(nvec), dim3(256), 0, st, band0, n, lam_desc, inv, ipiv, vec, nvec);

@@ -14,8 +14,8 @@ Eigensolve: pods_syev (register-resident tridiagonalisation + bisection + twiste
 factorisation, all eigenvalues and the nm leading vectors) whenever only the truncated
 temporal modes are needed (ns <= 4096, 0 <= nm <= 64); pods_syev2 (two-stage: band
 reduction on fp64 MFMA, bulge chasing, bisection, band inverse iteration) for
-4096 < ns <= 8192; torch.linalg.eigh (rocSOLVER dsyevd) when the full temporal-mode matrix
-is requested (verbose output), beyond 8192, or with PODS_EIGEN=torch.
+4096 < ns <= 16384; torch.linalg.eigh (rocSOLVER dsyevd) when the full temporal-mode matrix
+is requested (verbose output), beyond 16384, or with PODS_EIGEN=torch.
 
 PyTorch is used for device memory, the stream, torch.distributed and that fallback
 eigensolve -- nothing else.
@@ -195,7 +195,7 @@ def allreduce_correlation(dist, C, ns, divide):
 
 
 SYEV_MAX_N = 4096   # pods_syev's on-chip limit (trd_plan)
-SYEV2_MAX_N = 8192  # pods_syev2 (two-stage): the bisection's LDS limit
+SYEV2_MAX_N = 16384  # pods_syev2 (two-stage): 64 panel workgroups x 256 rows
 SYEV_MAX_VEC = 64
 
 

@@ -36,7 +36,7 @@ def test_syev2_pod_like(ctx, n):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("n", [4096, 8192])
+@pytest.mark.parametrize("n", [4096, 8192, 16384])
 def test_syev2_large(ctx, n):
     C = pod_like(n, seed=7)
     lam, Y = solve2(ctx, C, 20)
