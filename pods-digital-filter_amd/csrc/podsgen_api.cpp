@@ -229,6 +229,7 @@ struct pods_ctx {
   int nprog_mean = 0;
   bool mean_valid = false;
   bool have_snapshots = false;  // A holds ns x rowlen snapshots (generated or loaded)
+  bool gen_fused = false;       // pods_df_generate runs k_filter_xyz (no T1 planes)
   bool centered = false;        // A holds A - mean (pods_center); consumers subtract zero
   DevBuf zero;                  // rowpad zeros: the mean operand once A is centred
   std::vector<double> stage;  // host staging for small uploads
@@ -349,6 +350,17 @@ int pods_synchronize(pods_ctx* c) {
   return PODS_OK;
 }
 
+namespace {
+// np.mean's pairwise program over ns snapshots (k_mean), uploaded once per snapshot count.
+int upload_mean_program(pods_ctx* c, int ns) {
+  std::vector<int> prog = pairwise_program(ns);
+  c->nprog_mean = (int)prog.size() / 2;
+  PODS_HIP(ensure(c->prog_mean, prog.size() * sizeof(int)));
+  PODS_HIP(hipMemcpy(c->prog_mean.p, prog.data(), prog.size() * sizeof(int), hipMemcpyHostToDevice));
+  return PODS_OK;
+}
+}  // namespace
+
 int pods_df_configure(pods_ctx* c, const pods_df_params* prm, const double* bx, const double* by,
                       const double* bz, const double* lund_host, const double* rot_host) {
   PODS_TRY
@@ -382,7 +394,11 @@ int pods_df_configure(pods_ctx* c, const pods_df_params* prm, const double* bx, 
   const int64_t ntot = nplanes * c->S;  // doubles of the stream that reach A
   c->layout = make_layout(ntot);
   PODS_HIP(ensure(c->R, (size_t)nplanes * c->Sl * sizeof(double)));
-  PODS_HIP(ensure(c->T1, (size_t)3 * p.ns * c->Sl * sizeof(double)));
+  // PODS_GEN_FUSED=1 selects the fused x+y+z pass (k_filter_xyz: no x-filtered planes, bit
+  // identical); the default two-pass path (k_filter_x2 + k_filter_yz) is faster
+  const char* fz = std::getenv("PODS_GEN_FUSED");
+  c->gen_fused = pods::filter_xyz_supported(c->NX, c->NY, c->NZ) && fz && std::atoi(fz) == 1;
+  if (!c->gen_fused) PODS_HIP(ensure(c->T1, (size_t)3 * p.ns * c->Sl * sizeof(double)));
   PODS_HIP(ensure(c->A, (size_t)p.ns * c->rowpad * sizeof(double)));
   PODS_HIP(ensure(c->mean, (size_t)c->rowpad * sizeof(double)));
   // padded K columns of the K-tiled snapshot matrix (and of the mean) stay zero
@@ -411,10 +427,7 @@ int pods_df_configure(pods_ctx* c, const pods_df_params* prm, const double* bx, 
   double r9[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
   if (p.rotate) std::memcpy(r9, rot_host, sizeof(r9));
   PODS_HIP(hipMemcpy(c->rot.p, r9, sizeof(r9), hipMemcpyHostToDevice));
-  std::vector<int> prog = pairwise_program(p.ns);
-  c->nprog_mean = (int)prog.size() / 2;
-  PODS_HIP(ensure(c->prog_mean, prog.size() * sizeof(int)));
-  PODS_HIP(hipMemcpy(c->prog_mean.p, prog.data(), prog.size() * sizeof(int), hipMemcpyHostToDevice));
+  if (int e = upload_mean_program(c, p.ns)) return e;
   if (int e = upload_rng(c, c->layout, p.seed, c->rng)) return e;
   c->configured = true;
   c->have_snapshots = false;
@@ -435,12 +448,23 @@ int pods_df_generate(pods_ctx* c) {
   PODS_HIP(pods::launch_mt_generate(c->rng.states.as<uint32_t>(), L.G, L.Bs, L.ntot, c->S, c->Kp, p.j0,
                                     p.j1 + 2 * p.nfy, c->Sl, p.rng_low, p.rng_range, c->R.as<double>(),
                                     c->stream));
+  const double* taps = c->taps.as<double>();
+  if (c->gen_fused) {
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    PODS_HIP(pods::launch_filter_xyz(c->NX, c->NY, c->NZ, c->R.as<double>(), taps, p.ns, c->jl, p.kma, c->Kp,
+                                     c->Sl, c->lund.as<double>(), c->lund_sj, p.lund_mode, c->rot.as<double>(),
+                                     p.rotate, c->A.as<double>(), cus, c->stream));
+    c->have_snapshots = true;
+    c->mean_valid = false;
+    c->centered = false;
+    return PODS_OK;
+  }
   // x pass: enough (component, point, step-chunk) threads to fill the chip
   const int64_t pts = 3 * c->Sl;
   int64_t nch = (256LL * 2048 + pts - 1) / pts;
   nch = std::max<int64_t>(1, std::min<int64_t>(nch, std::max(1, p.ns / 16)));
   const int chunk = (int)((p.ns + nch - 1) / nch);
-  const double* taps = c->taps.as<double>();
   PODS_HIP(pods::launch_filter_x(c->NX, c->R.as<double>(), taps, p.ns, c->Sl, 3, chunk,
                                  c->T1.as<double>(), c->stream));
   PODS_HIP(pods::launch_filter_yz(c->NY, c->T1.as<double>(), taps + c->NX, taps + c->NX + c->NY,
@@ -480,10 +504,7 @@ int pods_set_snapshots(pods_ctx* c, const double* at, int ns, int64_t rowlen) {
   PODS_HIP(ensure(c->mean, (size_t)rowpad * sizeof(double)));
   PODS_HIP(hipMemset(c->mean.p, 0, (size_t)rowpad * sizeof(double)));
   PODS_HIP(hipMemcpy(c->A.p, tiled.data(), tiled.size() * sizeof(double), hipMemcpyHostToDevice));
-  std::vector<int> prog = pairwise_program(ns);
-  c->nprog_mean = (int)prog.size() / 2;
-  PODS_HIP(ensure(c->prog_mean, prog.size() * sizeof(int)));
-  PODS_HIP(hipMemcpy(c->prog_mean.p, prog.data(), prog.size() * sizeof(int), hipMemcpyHostToDevice));
+  if (int e = upload_mean_program(c, ns)) return e;
   c->p = pods_df_params{};
   c->p.ns = ns;
   c->rowlen = rowlen;

@@ -669,13 +669,17 @@ __global__ void k_de_fill(const double* __restrict__ D, const double* __restrict
   deg[i] = make_double2(D[i], e * e);
 }
 
+// GDE: {d, e^2} read from global memory (n too long for LDS).  A compile-time choice: a
+// runtime select between the two would make every Sturm load a flat load (2.17 vs 1.41 ms
+// of k_bisect at n = 4096).
+template <bool GDE>
 __global__ __launch_bounds__(256) void k_sturm_grid(const double* __restrict__ D,
                                                     const double* __restrict__ E, int n,
                                                     const double* __restrict__ bounds,
                                                     int* __restrict__ cnt, const double2* __restrict__ deg) {
   extern __shared__ double2 desh[];
-  const double2* de = deg ? deg : desh;
-  if (!deg) {
+  const double2* de = GDE ? deg : desh;
+  if (!GDE) {
     for (int i = threadIdx.x; i < n; i += 256) {
       const double e = i > 0 ? E[i - 1] : 0.0;
       desh[i] = make_double2(D[i], e * e);
@@ -713,15 +717,16 @@ constexpr int NCH = 1;  // shifts per lane: 16 shifts per step split the bracket
 // Eigenvalue k (ascending) of T by multisection: shift s = c*BL + l (chain c of lane l) sits
 // at lo + (s+1) (hi-lo)/(BL*NCH+1).  Output lam_desc[n-1-k].  LDS: n x {d_i, e_{i-1}^2}.
 // (The kernel is fp64-issue bound, so fewer shifts per step -- less work per bit -- win.)
+template <bool GDE>
 __global__ __launch_bounds__(256) void k_bisect(const double* __restrict__ D,
                                                 const double* __restrict__ E, int n,
                                                 const double* __restrict__ bounds,
                                                 double* __restrict__ lam_desc, int k0, int k1,
                                                 const int* __restrict__ gcnt, const double2* __restrict__ deg) {
   extern __shared__ double2 desh[];
-  const double2* de = deg ? deg : desh;
+  const double2* de = GDE ? deg : desh;
   const int t = threadIdx.x, lane = t & 63;
-  if (!deg) {
+  if (!GDE) {
     for (int i = t; i < n; i += 256) {
       const double e = i > 0 ? E[i - 1] : 0.0;
       desh[i] = make_double2(D[i], e * e);
@@ -1359,21 +1364,32 @@ hipError_t launch_tri_bisect(const double* D, const double* E, int n, const doub
   } else {
     deg = nullptr;
   }
+  const bool gde = deg != nullptr;
   if (grid_cnt) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&eig::k_sturm_grid),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    const void* kg = gde ? reinterpret_cast<const void*>(&eig::k_sturm_grid<true>)
+                         : reinterpret_cast<const void*>(&eig::k_sturm_grid<false>);
+    hipError_t e = hipFuncSetAttribute(kg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(eig::k_sturm_grid, dim3(2 * eig::NSH / 256), dim3(256), lds, st, D, E, n, bounds,
-                       grid_cnt, deg);
+    if (gde)
+      hipLaunchKernelGGL(eig::k_sturm_grid<true>, dim3(2 * eig::NSH / 256), dim3(256), lds, st, D, E, n, bounds,
+                         grid_cnt, deg);
+    else
+      hipLaunchKernelGGL(eig::k_sturm_grid<false>, dim3(2 * eig::NSH / 256), dim3(256), lds, st, D, E, n, bounds,
+                         grid_cnt, deg);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&eig::k_bisect),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const void* kb = gde ? reinterpret_cast<const void*>(&eig::k_bisect<true>)
+                       : reinterpret_cast<const void*>(&eig::k_bisect<false>);
+  hipError_t e = hipFuncSetAttribute(kb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   const int per = 256 / eig::BL;
-  hipLaunchKernelGGL(eig::k_bisect, dim3((k1 - k0 + per - 1) / per), dim3(256), lds, st, D, E, n,
-                     bounds, lam_desc, k0, k1, grid_cnt, deg);
+  if (gde)
+    hipLaunchKernelGGL(eig::k_bisect<true>, dim3((k1 - k0 + per - 1) / per), dim3(256), lds, st, D, E, n,
+                       bounds, lam_desc, k0, k1, grid_cnt, deg);
+  else
+    hipLaunchKernelGGL(eig::k_bisect<false>, dim3((k1 - k0 + per - 1) / per), dim3(256), lds, st, D, E, n,
+                       bounds, lam_desc, k0, k1, grid_cnt, deg);
   return hipGetLastError();
 }
 

@@ -15,6 +15,10 @@ hipError_t launch_mt_generate(const uint32_t* states, int G, int64_t Bs, int64_t
 hipError_t launch_filter_x(int NX, const double* R, const double* bx, int ns, int64_t Sl, int ncomp,
                            int chunk, double* T1, hipStream_t st);
 // lund_sj: j-stride of the 9 x Pl Lund table (0 = the same row of parameters for every j)
+bool filter_xyz_supported(int NX, int NY, int NZ);
+hipError_t launch_filter_xyz(int NX, int NY, int NZ, const double* R, const double* taps, int ns, int jl, int K,
+                             int Kp, int64_t Sl, const double* lund, int64_t lund_sj, int lund_mode,
+                             const double* rot, int rotate, double* AT, int cus, hipStream_t st);
 hipError_t launch_filter_yz(int NY, const double* T1, const double* by, const double* bz, int NZ,
                             int ns, int jl, int K, int Kp, int64_t Sl, int ncomp,
                             const double* lund, int64_t lund_sj, int lund_mode, const double* rot,

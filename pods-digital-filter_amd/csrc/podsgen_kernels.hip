@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 
 #include "podsgen_kernels.h"
 

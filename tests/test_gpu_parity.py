@@ -288,6 +288,18 @@ def test_center_in_place(ctx):
     assert torch.equal(C0, C1)
 
 
+@pytest.mark.parametrize("kw", [dict(jma=32, kma=32, ns=64, seed=12345),
+                                dict(jma=40, kma=27, ns=30, seed=5, normal=(1.0, -0.4, 0.2)),
+                                dict(jma=256, kma=256, ns=24, seed=4242)])
+def test_generate_fused_xyz_opt_in(ctx, monkeypatch, kw):
+    """The opt-in fused x+y+z generator pass (PODS_GEN_FUSED=1, k_filter_xyz: no x-filtered
+    planes in HBM) is bit-exact against the oracle: full tiles, ragged edge tiles (40 x 27) with
+    a rotated normal, and the 256^2 inlet."""
+    monkeypatch.setenv("PODS_GEN_FUSED", "1")
+    A = E.Generator(podsgen.DFSetup(**kw), ctx=ctx).generate().to_host()
+    assert np.array_equal(A, O.generate(O.DFConfig(**kw)))
+
+
 def test_medium_case_vs_oracle(ctx):
     """256 x 256 inlet, 24 steps: generation bit-exact against the oracle."""
     s = podsgen.DFSetup(jma=256, kma=256, ns=24, seed=4242)
