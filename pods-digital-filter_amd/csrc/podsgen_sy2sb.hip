@@ -8,7 +8,7 @@
 //                       rows + the pivot row are published, every workgroup forms the reflector
 //                       redundantly); writes the explicit V (m x B), tau and R, and
 //                       (one more hop: partial V^T V) T (dlarft 'F','C')
-//            k_ay       Y = A22 V on fp64 MFMA (split K)      \
+//            k_ay2      Y = A22 V on fp64 MFMA (split K)      \
 //            k_xt       X = Y T                                |  W = X - 1/2 V T^T V^T X
 //            k_z/k_zm   Z = V^T X, M = 1/2 T^T Z               |  (LAPACK dsytrd blocking)
 //            k_w        W = X - V M                           /
@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 
 #include "podsgen_kernels.h"
@@ -71,6 +72,15 @@ __device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t r, int idx, double v)
 
 constexpr int SPIN_LIMIT = 1 << 22;
 
+// tagged granules: the tag rides in the two lowest mantissa bits of the published double
+__device__ __forceinline__ double tagged(double v, uint32_t tag) {
+  const long long b = (__double_as_longlong(v) & ~3ll) | (long long)(tag & 3u);
+  return __longlong_as_double(b);
+}
+__device__ __forceinline__ bool tag_ok(double v, uint32_t tag) {
+  return ((uint32_t)__double2loint(v) & 3u) == (tag & 3u);
+}
+
 // ---------------------------------------------------------------------------------------
 // k_pqr<B>: Householder QR of the panel P = A[r0:r0+m, c0:c0+B] (row-major A, ld lda).
 // Workgroup w holds panel rows [w*RP, min((w+1)*RP, m)) in LDS.  Column j: partial
@@ -84,7 +94,7 @@ constexpr int SPIN_LIMIT = 1 << 22;
 template <int B>
 __global__ __launch_bounds__(256, 1) void k_pqr(double* __restrict__ A, int64_t lda, int r0, int c0, int m,
                                                int RP, int NW, double* __restrict__ pub,
-                                               uint32_t* __restrict__ flags, uint32_t epoch,
+                                               uint32_t* __restrict__ flags, uint32_t epoch, uint32_t seq0,
                                                uint32_t* __restrict__ abortw, double* __restrict__ Vx,
                                                double* __restrict__ tau, double* __restrict__ gpart,
                                                double* __restrict__ Tout) {
@@ -130,25 +140,38 @@ __global__ __launch_bounds__(256, 1) void k_pqr(double* __restrict__ A, int64_t 
         if (q == i) pr = P[q];
       rowj[kq] = pr;
     }
-    __syncthreads();
-    double* pb = pub + ((int64_t)(j & 1) * NW + w) * 2 * B;
+    __syncthreads();  // B1: the row-group partials are in red
+    // Hand-off without flags: every published double carries the column's tag in its two
+    // lowest mantissa bits (the sequence number c = 16 panel + j/2 + 1 differs by 1 from the
+    // previous write to the same slot, and the slots are zeroed per call), so consumers spin
+    // on the data itself; no drain, no flag round trip.
     const __amdgpu_buffer_rsrc_t rpub = rsrc(pub, (int64_t)2 * NW * 2 * B);
     const int pbase = ((j & 1) * NW + w) * 2 * B;
+    const uint32_t tag = seq0 + (uint32_t)(j >> 1);
     if (t < B) {
-      double s = 0.0;
+      double sp = 0.0;
 #pragma unroll
-      for (int q = 0; q < RG; ++q) s += red[q][t];
-      bst(rpub, pbase + t, s);
-      if (j >= g0 && j < g1) bst(rpub, pbase + B + t, rowj[t]);
+      for (int q = 0; q < RG; ++q) sp += red[q][t];
+      bst(rpub, pbase + t, tagged(sp, tag));
+      if (j >= g0 && j < g1) bst(rpub, pbase + B + t, tagged(rowj[t], tag));
     }
-    (void)pb;
-    drain();
-    __syncthreads();
-    const uint32_t want = epoch * 256u + (uint32_t)(j + 1);
-    if (t == 0) st_f(flags + w, want);
-    if (t < NW) {
+    {
+      const int qb = (j & 1) * NW * 2 * B;
+      const int own = j / RP;  // the workgroup holding pivot row j
       int spin = 0;
-      while ((int)(ld_f(flags + t) - want) < 0) {
+      for (;;) {
+        bool ok = true;
+        for (int e = t; e < NW * B; e += 256) {
+          const double v = bld(rpub, qb + (e / B) * 2 * B + (e % B));
+          ok = ok && tag_ok(v, tag);
+          gsum[e] = v;
+        }
+        if (t < B) {
+          const double v = bld(rpub, qb + own * 2 * B + B + t);
+          ok = ok && tag_ok(v, tag);
+          rowj[t] = v;
+        }
+        if (__all(ok)) break;
         if (++spin > SPIN_LIMIT) {
           st_f(abortw, 1u);
           break;
@@ -156,19 +179,13 @@ __global__ __launch_bounds__(256, 1) void k_pqr(double* __restrict__ A, int64_t 
         __builtin_amdgcn_s_sleep(1);
       }
     }
-    __syncthreads();
-    {
-      const int qb = (j & 1) * NW * 2 * B;
-      for (int e = t; e < NW * B; e += 256) gsum[e] = bld(rpub, qb + (e / B) * 2 * B + (e % B));
-      if (t < B) rowj[t] = bld(rpub, qb + (j / RP) * 2 * B + B + t);
-    }
-    __syncthreads();
+    __syncthreads();  // B2: every partial and the pivot row are in LDS
     if (t < B) {
-      double s = 0.0;
-      for (int q = 0; q < NW; ++q) s += gsum[q * B + t];
-      S[t] = s;
+      double sacc = 0.0;
+      for (int q = 0; q < NW; ++q) sacc += gsum[q * B + t];
+      S[t] = sacc;
     }
-    __syncthreads();
+    __syncthreads();  // B3
     // ---- reflector (dlarfg), redundantly in every thread -----------------------------
     const double alpha = rowj[j], sigma = S[j];
     double beta = alpha, tj = 0.0, scal = 0.0;
@@ -277,15 +294,35 @@ __global__ __launch_bounds__(256, 1) void k_pqr(double* __restrict__ A, int64_t 
   if (t >= kc && t < B) tau[t] = 0.0;
 }
 
-// Y_s = A22[:, k-slice s] Vx[k-slice s, :] on v_mfma_f64_16x16x4 (A22 = A[r0:, r0:]).
-// Block: 64 rows x B cols, 4 waves x 16 rows; K staged through LDS 32 at a time.
+// s = ((p_0 + p_1) + p_2) + ... over n partials at stride `stride` (the order of a plain loop),
+// with the loads issued eight at a time so they are in flight together.
+__device__ __forceinline__ double sum_partials(const double* __restrict__ p, int64_t stride, int n) {
+  double s = 0.0;
+  int q = 0;
+  for (; q + 8 <= n; q += 8) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(q + u) * stride];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; q < n; ++q) s += p[(int64_t)q * stride];
+  return s;
+}
+
+// Y_s = A22[:, k-slice s] Vx[k-slice s, :], bandwidth-shaped: 64 x B output block per
+// workgroup, K staged 32 at a time through LDS with the next slice's A / V loads in flight
+// (registers) while the current one feeds the MFMAs.  Enough (row block, split) pairs to put
+// several workgroups on every CU (the A22 read is the kernel's whole cost: ~m^2 doubles).
 template <int B>
-__global__ __launch_bounds__(256) void k_ay(const double* __restrict__ A, int64_t lda, int r0, int m,
-                                            const double* __restrict__ Vx, int kchunk,
-                                            double* __restrict__ Y) {
-  constexpr int KC = 32, LDA_S = KC + 2;
+__global__ __launch_bounds__(256) void k_ay2(const double* __restrict__ A, int64_t lda, int r0, int m,
+                                             const double* __restrict__ Vx, int kchunk,
+                                             double* __restrict__ Y) {
+  constexpr int KC = 32, LDA_S = KC + 2, LDV = B + 2;
+  constexpr int AL = 64 * KC / 256;  // A loads per thread per slice: 8
+  constexpr int VL = KC * B / 256;   // V loads per thread per slice: 4
   __shared__ double As[64 * LDA_S];
-  __shared__ double Vs[KC * (B + 2)];
+  __shared__ double Vs[KC * LDV];
   const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
   const int fr = lane & 15, fk = lane >> 4;
   const int i0 = blockIdx.x * 64;
@@ -293,28 +330,45 @@ __global__ __launch_bounds__(256) void k_ay(const double* __restrict__ A, int64_
   f64x4 acc[B / 16];
 #pragma unroll
   for (int c = 0; c < B / 16; ++c) acc[c] = (f64x4){0.0, 0.0, 0.0, 0.0};
-  for (int kb = k0; kb < k1; kb += KC) {
-    for (int e = t; e < 64 * KC; e += 256) {
-      const int r = e / KC, k = e % KC;
+  double ra[AL], rv[VL];
+  auto load = [&](int kb) {
+#pragma unroll
+    for (int u = 0; u < AL; ++u) {
+      const int e = t + 256 * u, r = e / KC, k = e % KC;
       const int gi = i0 + r, gk = kb + k;
-      As[r * LDA_S + k] = (gi < m && gk < k1) ? A[(int64_t)(r0 + gi) * lda + r0 + gk] : 0.0;
+      ra[u] = (gi < m && gk < k1) ? A[(int64_t)(r0 + gi) * lda + r0 + gk] : 0.0;
     }
-    for (int e = t; e < KC * B; e += 256) {
-      const int k = e / B, c = e % B;
+#pragma unroll
+    for (int u = 0; u < VL; ++u) {
+      const int e = t + 256 * u, k = e / B, c = e % B;
       const int gk = kb + k;
-      Vs[k * (B + 2) + c] = gk < k1 ? Vx[(int64_t)gk * B + c] : 0.0;
+      rv[u] = gk < k1 ? Vx[(int64_t)gk * B + c] : 0.0;
+    }
+  };
+  if (k0 < k1) load(k0);
+  for (int kb = k0; kb < k1; kb += KC) {
+    __syncthreads();  // the previous slice's fragments are consumed
+#pragma unroll
+    for (int u = 0; u < AL; ++u) {
+      const int e = t + 256 * u;
+      As[(e / KC) * LDA_S + e % KC] = ra[u];
+    }
+#pragma unroll
+    for (int u = 0; u < VL; ++u) {
+      const int e = t + 256 * u;
+      Vs[(e / B) * LDV + e % B] = rv[u];
     }
     __syncthreads();
+    if (kb + KC < k1) load(kb + KC);  // in flight under this slice's MFMAs
 #pragma unroll
     for (int kk = 0; kk < KC; kk += 4) {
       const double a = As[(16 * wv + fr) * LDA_S + kk + fk];
 #pragma unroll
       for (int c = 0; c < B / 16; ++c) {
-        const double b = Vs[(kk + fk) * (B + 2) + 16 * c + fr];
+        const double b = Vs[(kk + fk) * LDV + 16 * c + fr];
         acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[c], 0, 0, 0);
       }
     }
-    __syncthreads();
   }
   double* Yb = Y + (int64_t)blockIdx.y * m * B;
 #pragma unroll
@@ -338,7 +392,7 @@ __global__ __launch_bounds__(256) void k_xt(const double* __restrict__ Y, int KS
   const int i = blockIdx.x * RB + rr;
   double s = 0.0;
   if (i < m)
-    for (int q = 0; q < KS; ++q) s += Y[((int64_t)q * m + i) * B + c];
+    s = sum_partials(Y + (int64_t)i * B + c, (int64_t)m * B, KS);
   Ys[rr][c] = s;
   __syncthreads();
   if (i >= m) return;
@@ -395,14 +449,17 @@ __global__ __launch_bounds__(256) void k_zm(const double* __restrict__ Zp, int n
   const int t = threadIdx.x;
   for (int e = t; e < B * B; e += 256) {
     double s = 0.0;
-    for (int q = 0; q < nz; ++q) s += Zp[(int64_t)q * B * B + e];
+    s = sum_partials(Zp + e, (int64_t)B * B, nz);
     Z[e / B][e % B] = s;
   }
+  __syncthreads();
+  __shared__ double Tl[B][B + 1];
+  for (int e = t; e < B * B; e += 256) Tl[e / B][e % B] = T[e];
   __syncthreads();
   for (int e = t; e < B * B; e += 256) {
     const int a = e / B, b = e % B;
     double s = 0.0;
-    for (int l = 0; l <= a; ++l) s = fma(T[l * B + a], Z[l][b], s);  // (T^T)[a][l] = T[l][a], l <= a
+    for (int l = 0; l <= a; ++l) s = fma(Tl[l][a], Z[l][b], s);  // (T^T)[a][l] = T[l][a], l <= a
     M[e] = 0.5 * s;
   }
 }
@@ -431,9 +488,12 @@ template <int B>
 __global__ __launch_bounds__(256) void k_upd(double* __restrict__ A, int64_t lda, int r0, int m,
                                              const double* __restrict__ Vx, const double* __restrict__ W) {
   constexpr int K2 = 2 * B, LD = K2 + 2;
-  __shared__ double Ls[64 * LD];
-  __shared__ double Rs[64 * LD];
-  __shared__ double Ot[64][65];
+  // Ls | Rs during the MFMAs, then the 64 x 65 transpose staging (aliased: 2 blocks per CU)
+  __shared__ double sh_upd[2 * 64 * LD];
+  double* Ls = sh_upd;
+  double* Rs = sh_upd + 64 * LD;
+  double (*Ot)[65] = reinterpret_cast<double (*)[65]>(sh_upd);
+  static_assert(64 * 65 <= 2 * 64 * LD, "transpose staging fits the operand buffers");
   const int L = blockIdx.x;
   int ti = (int)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
   while ((ti + 1) * (ti + 2) / 2 <= L) ++ti;
@@ -442,6 +502,16 @@ __global__ __launch_bounds__(256) void k_upd(double* __restrict__ A, int64_t lda
   const int i0 = ti * 64, j0 = tj * 64;
   const int t = threadIdx.x, wv = t >> 6, lane = t & 63;
   const int fr = lane & 15, fk = lane >> 4;
+  // the A tile's loads go out first: they overlap the V / W staging and the MFMAs
+  double aold[4][4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int li = 16 * wv + fk + 4 * reg, lj = 16 * c + fr;
+      const int gi = i0 + li, gj = j0 + lj;
+      aold[c][reg] = (gi < m && gj < m) ? A[(int64_t)(r0 + gi) * lda + r0 + gj] : 0.0;
+    }
   for (int e = t; e < 64 * K2; e += 256) {
     const int r = e / K2, k = e % K2;
     const int gi = i0 + r, gj = j0 + r;
@@ -462,6 +532,7 @@ __global__ __launch_bounds__(256) void k_upd(double* __restrict__ A, int64_t lda
       acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[c], 0, 0, 0);
     }
   }
+  __syncthreads();  // every wave's fragments are read before Ot overwrites them
 #pragma unroll
   for (int c = 0; c < 4; ++c)
 #pragma unroll
@@ -470,9 +541,8 @@ __global__ __launch_bounds__(256) void k_upd(double* __restrict__ A, int64_t lda
       const int gi = i0 + li, gj = j0 + lj;
       double v = 0.0;
       if (gi < m && gj < m) {
-        double* p = A + (int64_t)(r0 + gi) * lda + r0 + gj;
-        v = *p - acc[c][reg];
-        if (ti > tj || lj <= li) *p = v;
+        v = aold[c][reg] - acc[c][reg];
+        if (ti > tj || lj <= li) A[(int64_t)(r0 + gi) * lda + r0 + gj] = v;
       }
       Ot[li][lj] = v;
     }
@@ -517,7 +587,8 @@ __global__ void k_band(const double* __restrict__ A, int64_t lda, int n, double*
 // ---------------------------------------------------------------------------------------
 template <int B>
 __global__ __launch_bounds__(64, 1) void k_sbtrd(double* __restrict__ band, int n, int NG,
-                                                 uint32_t* __restrict__ prog, uint32_t* __restrict__ abortw) {
+                                                 uint32_t* __restrict__ prog, uint32_t* __restrict__ abortw,
+                                                 int64_t* __restrict__ trace, int trace_s) {
   static_assert(B == 32, "k_sbtrd maps a 32 x 32 block onto one wave (lane = column, half of the rows)");
   constexpr int LDB = 2 * B, H = B / 2;
   constexpr uint32_t DONE = 0x7fffffffu;
@@ -528,6 +599,16 @@ __global__ __launch_bounds__(64, 1) void k_sbtrd(double* __restrict__ band, int 
   const __amdgpu_buffer_rsrc_t rb = rsrc(band, (int64_t)n * LDB);
   // lane (c, h) holds rows [16h, 16h+16) of column c of each block:
   //   L[i][c] (rows R_k, column col + c), D[i][c] (column r0 + c), R[c][j] (row r1 + c, j in its half)
+  // operand loads batch (no volatile bit: the flag poll above them ends in a compiler barrier);
+  // sc1 stores write through, so the next sweep's workgroup on another XCD sees them
+  auto ld = [&](int idx) -> double {
+    const auto q = __builtin_amdgcn_raw_buffer_load_b64(rb, idx * 8, 0, 16u);
+    return __builtin_bit_cast(double, q);
+  };
+  auto st = [&](int idx, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(rb, 0, 0, 0)), v),
+                                          rb, idx * 8, 0, 16u);
+  };
   for (int s = blockIdx.x; s < n - 2; s += NG) {
     for (int k = 0;; ++k) {
       const int r0 = s + 1 + k * B;
@@ -536,6 +617,8 @@ __global__ __launch_bounds__(64, 1) void k_sbtrd(double* __restrict__ band, int 
       const int col = k == 0 ? s : s + 1 + (k - 1) * B;
       const int nl = r0 - col;
       const int r2 = min(r1 + B, n), nr = r2 - r1;
+      int64_t* tr = (trace && s == trace_s && lane == 0 && k < 256) ? trace + k * 6 : nullptr;
+      if (tr) tr[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
       if (s > 0 && lane == 0) {
         int spin = 0;
         for (;;) {
@@ -549,14 +632,16 @@ __global__ __launch_bounds__(64, 1) void k_sbtrd(double* __restrict__ band, int 
         }
       }
       __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");  // the operand loads stay behind the poll
+      if (tr) tr[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
       // ---- loads (all issued, one wait) -------------------------------------------------
       double L[H], D[H], R[H];
 #pragma unroll
       for (int q = 0; q < H; ++q) {
         const int i = H * h + q;
-        L[q] = (c < nl && i < len) ? bld(rb, idx(r0 + i, col + c)) : 0.0;
-        D[q] = (c < len && i < len && i >= c) ? bld(rb, idx(r0 + i, r0 + c)) : 0.0;
-        R[q] = (c < nr && i < len) ? bld(rb, idx(r1 + c, r0 + i)) : 0.0;  // R[c][j = i]
+        L[q] = (c < nl && i < len) ? ld(idx(r0 + i, col + c)) : 0.0;
+        D[q] = (c < len && i < len && i >= c) ? ld(idx(r0 + i, r0 + c)) : 0.0;
+        R[q] = (c < nr && i < len) ? ld(idx(r1 + c, r0 + i)) : 0.0;  // R[c][j = i]
       }
 #pragma unroll
       for (int q = 0; q < H; ++q) {  // the upper triangle of D from the lower one
@@ -569,6 +654,10 @@ __global__ __launch_bounds__(64, 1) void k_sbtrd(double* __restrict__ band, int 
       for (int q = 0; q < H; ++q) {
         const int i = H * h + q;
         if (i < c && c < len) D[q] = Ds[c][i];
+      }
+      if (tr) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        tr[2] = (int64_t)__builtin_amdgcn_s_memrealtime();
       }
       // ---- Householder of x = L[:, 0] (column col) --------------------------------------
       const double x0 = __shfl(L[0], 0);  // lane 0 = (c 0, h 0): row 0
@@ -649,16 +738,18 @@ __global__ __launch_bounds__(64, 1) void k_sbtrd(double* __restrict__ band, int 
 #pragma unroll
         for (int q = 0; q < H; ++q) R[q] = fma(-f, v[q], R[q]);
       }
+      if (tr) tr[3] = (int64_t)__builtin_amdgcn_s_memrealtime();
       // ---- stores (lower triangle of D) -------------------------------------------------
 #pragma unroll
       for (int q = 0; q < H; ++q) {
         const int i = H * h + q;
-        if (c < nl && i < len) bst(rb, idx(r0 + i, col + c), L[q]);
-        if (c < len && i < len && i >= c) bst(rb, idx(r0 + i, r0 + c), D[q]);
-        if (c < nr && i < len) bst(rb, idx(r1 + c, r0 + i), R[q]);
+        if (c < nl && i < len) st(idx(r0 + i, col + c), L[q]);
+        if (c < len && i < len && i >= c) st(idx(r0 + i, r0 + c), D[q]);
+        if (c < nr && i < len) st(idx(r1 + c, r0 + i), R[q]);
       }
       drain();
       __builtin_amdgcn_wave_barrier();
+      if (tr) tr[4] = (int64_t)__builtin_amdgcn_s_memrealtime();
       if (lane == 0) st_f(prog + s, (uint32_t)(k + 1));
     }
     drain();
@@ -867,7 +958,7 @@ __global__ __launch_bounds__(256) void k_bt_t(const double* __restrict__ T, cons
   const int t = threadIdx.x;
   for (int e = t; e < B * nvec; e += 256) {
     double s = 0.0;
-    for (int q = 0; q < nz; ++q) s += Zp[(int64_t)q * B * nvec + e];
+    s = sum_partials(Zp + e, (int64_t)B * nvec, nz);
     Z[e] = s;
   }
   __syncthreads();
@@ -914,8 +1005,8 @@ size_t sy2sb_work_doubles(int n, int nvec, SyevdPlan* plan) {
     vx += (int64_t)(n - c0 - B) * B;
     ++p.np;
   }
-  p.KS = 4;
-  p.NZ = 16;
+  p.KS = 16;   // k_ay2 K splits (at most; fewer for short trailing blocks)
+  p.NZ = 128;  // row chunks of the V^T X / V^T Y partial products
   p.RP = 256;
   const int64_t nn = (int64_t)n * n;
   p.off_aw = 0;
@@ -949,6 +1040,9 @@ hipError_t launch_syevd2(const double* C, int n, int nvec, double* ws, const Sye
   uint32_t* prog = flags + 128;    // n sweep counters
   e = hipMemsetAsync(prog, 0, (size_t)n * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
+  // k_pqr's tagged hand-off slots start from tag 0 (the first column's tag is 1)
+  e = hipMemsetAsync(ws + p.off_pub, 0, (size_t)2 * 64 * 2 * B * sizeof(double), st);
+  if (e != hipSuccess) return e;
   int64_t vxo = 0;
   int pi = 0;
   const char* lim = std::getenv("PODS_SY2SB_PANELS");  // diagnostics: stop stage 1 early
@@ -961,15 +1055,21 @@ hipError_t launch_syevd2(const double* C, int n, int nvec, double* ws, const Sye
     const int NW = std::max(1, std::min(64, (m + p.RP - 1) / p.RP));
     const int RP = (m + NW - 1) / NW;
     hipLaunchKernelGGL(sb::k_pqr<B>, dim3(NW), dim3(256), 0, st, Aw, (int64_t)n, r0, c0, m, RP, NW,
-                       ws + p.off_pub, pflags, epoch * 1024u + (uint32_t)pi, abortw, Vx, tau, ws + p.off_zp, T);
-    const int kchunk = ((m + p.KS - 1) / p.KS + 31) / 32 * 32;
-    hipLaunchKernelGGL(sb::k_ay<B>, dim3((m + 63) / 64, p.KS), dim3(256), 0, st, Aw, (int64_t)n, r0, m, Vx,
+                       ws + p.off_pub, pflags, epoch * 1024u + (uint32_t)pi, 16u * (uint32_t)pi + 1u, abortw, Vx,
+                       tau, ws + p.off_zp, T);
+    // ~4 workgroups per CU for the A22 read: K splits of >= 256 columns
+    const int ks = std::max(1, std::min(p.KS, (1024 + (m + 63) / 64 - 1) / ((m + 63) / 64)));
+    const int kchunk = ((m + ks - 1) / ks + 31) / 32 * 32;
+    const int ksn = (m + kchunk - 1) / kchunk;
+    hipLaunchKernelGGL(sb::k_ay2<B>, dim3((m + 63) / 64, ksn), dim3(256), 0, st, Aw, (int64_t)n, r0, m, Vx,
                        kchunk, ws + p.off_y);
-    hipLaunchKernelGGL(sb::k_xt<B>, dim3((m + 256 / B - 1) / (256 / B)), dim3(256), 0, st, ws + p.off_y, p.KS, m,
+    hipLaunchKernelGGL(sb::k_xt<B>, dim3((m + 256 / B - 1) / (256 / B)), dim3(256), 0, st, ws + p.off_y, ksn, m,
                        T, ws + p.off_x);
-    const int zchunk = (m + p.NZ - 1) / p.NZ;
-    hipLaunchKernelGGL(sb::k_z<B>, dim3(p.NZ), dim3(256), 0, st, Vx, ws + p.off_x, m, zchunk, ws + p.off_zp);
-    hipLaunchKernelGGL(sb::k_zm<B>, dim3(1), dim3(256), 0, st, ws + p.off_zp, p.NZ, T, ws + p.off_m);
+    const int nzc = std::max(1, std::min(p.NZ, (m + 63) / 64));
+    const int zchunk = (m + nzc - 1) / nzc;
+    const int nzn = (m + zchunk - 1) / zchunk;
+    hipLaunchKernelGGL(sb::k_z<B>, dim3(nzn), dim3(256), 0, st, Vx, ws + p.off_x, m, zchunk, ws + p.off_zp);
+    hipLaunchKernelGGL(sb::k_zm<B>, dim3(1), dim3(256), 0, st, ws + p.off_zp, nzn, T, ws + p.off_m);
     hipLaunchKernelGGL(sb::k_w<B>, dim3((m + 256 / B - 1) / (256 / B)), dim3(256), 0, st, ws + p.off_x, Vx,
                        ws + p.off_m, m, ws + p.off_w);
     const int tiles = (m + 63) / 64;
@@ -986,7 +1086,34 @@ hipError_t launch_syevd2(const double* C, int n, int nvec, double* ws, const Sye
   e = hipMemcpyAsync(band0, band, (size_t)nb * sizeof(double), hipMemcpyDeviceToDevice, st);
   if (e != hipSuccess) return e;
   const int NG = std::max(1, std::min(256, n - 2));
-  if (n > 2) hipLaunchKernelGGL(sb::k_sbtrd<B>, dim3(NG), dim3(64), 0, st, band, n, NG, prog, abortw + 1);
+  // PODS_SBTRD_TRACE=s: per-task timestamps of sweep s (diagnostics, printed to stderr)
+  const char* trs = std::getenv("PODS_SBTRD_TRACE");
+  int64_t* trace = nullptr;
+  if (trs) {
+    e = hipMallocAsync(reinterpret_cast<void**>(&trace), 256 * 6 * sizeof(int64_t), st);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(trace, 0, 256 * 6 * sizeof(int64_t), st);
+    if (e != hipSuccess) return e;
+  }
+  if (n > 2)
+    hipLaunchKernelGGL(sb::k_sbtrd<B>, dim3(NG), dim3(64), 0, st, band, n, NG, prog, abortw + 1, trace,
+                       trs ? std::atoi(trs) : -1);
+  if (trace) {
+    int64_t h[256 * 6];
+    e = hipMemcpyAsync(h, trace, sizeof(h), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFreeAsync(trace, st);
+    if (e != hipSuccess) return e;
+    double acc[4] = {0, 0, 0, 0};
+    int cnt = 0;
+    for (int k = 1; k < 256 && h[k * 6] != 0 && h[k * 6 + 4] != 0; ++k) {
+      for (int q = 0; q < 4; ++q) acc[q] += (double)(h[k * 6 + q + 1] - h[k * 6 + q]) * 0.01;
+      ++cnt;
+    }
+    std::fprintf(stderr, "sbtrd trace sweep %s: %d tasks, per task us: wait %.2f load %.2f compute %.2f store+drain %.2f; task-to-task %.2f\n",
+                 trs, cnt, acc[0] / std::max(cnt, 1), acc[1] / std::max(cnt, 1), acc[2] / std::max(cnt, 1),
+                 acc[3] / std::max(cnt, 1), cnt > 1 ? (double)(h[cnt * 6] - h[6]) * 0.01 / (cnt - 1) : 0.0);
+  }
   double* D = ws + p.off_de;
   double* E = D + n;
   double* bounds = D + 2 * (int64_t)n;
@@ -1005,8 +1132,9 @@ hipError_t launch_syevd2(const double* C, int n, int nvec, double* ws, const Sye
     const int r0 = q * B + B, m = n - r0;
     const double* Vx = ws + p.off_vx + off;
     const double* T = ws + p.off_t + (int64_t)q * B * B;
-    const int nz = std::min(p.NZ, std::max(1, m / 256));
-    const int chunk = (m + nz - 1) / nz;
+    const int nz0 = std::min(p.NZ, std::max(1, m / 64));
+    const int chunk = (m + nz0 - 1) / nz0;
+    const int nz = (m + chunk - 1) / chunk;
     hipLaunchKernelGGL(sb::k_bt_z<B>, dim3(nz), dim3(256), 0, st, Vx, vec, nvec, r0, m, nvec, chunk, ws + p.off_zp);
     const size_t lds = (size_t)B * nvec * sizeof(double);
     hipLaunchKernelGGL(sb::k_bt_t<B>, dim3(1), dim3(256), lds, st, T, ws + p.off_zp, nz, nvec, ws + p.off_m);
