@@ -234,11 +234,30 @@ __global__ __launch_bounds__(256) void k_mt_generate(const uint32_t* __restrict_
   }
 }
 
+// One twist cur -> nxt by 227 threads with ONE barrier after it (instead of one per phase):
+// thread t produces nxt[t], nxt[227+t] and nxt[454+t] (t < 169) in a register chain -- each
+// later phase reads exactly the word the same thread made one phase earlier -- and thread 0
+// also nxt[623] = mix(cur[623], nxt[0], nxt[396]), recomputing nxt[169] and nxt[396] (made
+// by thread 169) from cur.  Same words as the in-place sequential twist.
+__device__ __forceinline__ void twist_chain(const uint32_t* __restrict__ cur, uint32_t* __restrict__ nxt, int t) {
+  if (t >= 227) return;
+  const uint32_t a = mt_mix(cur[t], cur[t + 1], cur[t + 397]);
+  nxt[t] = a;
+  const uint32_t b = mt_mix(cur[227 + t], cur[228 + t], a);
+  nxt[227 + t] = b;
+  if (t < 169) nxt[454 + t] = mt_mix(cur[454 + t], cur[455 + t], b);
+  if (t == 0) {
+    const uint32_t n169 = mt_mix(cur[169], cur[170], cur[566]);
+    const uint32_t n396 = mt_mix(cur[396], cur[397], n169);
+    nxt[623] = mt_mix(cur[623], a, n396);
+  }
+}
+
 // Whole-plane generator (one GPU: the slab holds every row, so double D of the stream goes to
 // out[D]).  One 256-thread workgroup per substream; the state is double-buffered in LDS, so
-// the twist producing block b (cur -> nxt, three dependent phases) and the tempering + 16-B
-// stores of block b-1 (reading cur) run in the same phases: 4 barriers per 624-word block
-// and four waves per substream to hide the LDS and store latency.
+// the twist producing block b (cur -> nxt, twist_chain) and the tempering + 16-B stores of
+// block b-1 (reading cur) run side by side: one barrier per 624-word block, four waves per
+// substream to hide the LDS and store latency.
 __global__ __launch_bounds__(256) void k_mt_generate_full(const uint32_t* __restrict__ states, int G,
                                                           int64_t Bs, int64_t ntot, double low,
                                                           double range, double* __restrict__ out) {
@@ -255,7 +274,7 @@ __global__ __launch_bounds__(256) void k_mt_generate_full(const uint32_t* __rest
     const uint32_t* cur = buf[b & 1];
     uint32_t* nxt = buf[(b + 1) & 1];
     const bool tw = b < nb;
-    if (tw && t < 227) nxt[t] = mt_mix(cur[t], cur[t + 1], cur[t + 397]);
+    if (tw) twist_chain(cur, nxt, t);
     if (b >= 1 && t < 156) {
       const uint4 w = reinterpret_cast<const uint4*>(cur)[t];
       const uint32_t a0 = mt_temper(w.x) >> 5, b0 = mt_temper(w.y) >> 6;
@@ -269,13 +288,7 @@ __global__ __launch_bounds__(256) void k_mt_generate_full(const uint32_t* __rest
         out[D] = low + range * u0;
     }
     if (!tw) break;
-    __syncthreads();
-    if (t < 227) nxt[227 + t] = mt_mix(cur[227 + t], cur[228 + t], nxt[t]);
-    __syncthreads();
-    if (t < 169) nxt[454 + t] = mt_mix(cur[454 + t], cur[455 + t], nxt[227 + t]);
-    __syncthreads();
-    if (t == 0) nxt[623] = mt_mix(cur[623], nxt[0], nxt[396]);
-    __syncthreads();
+    __syncthreads();  // nxt complete; cur (tempered above) becomes the next nxt
   }
 }
 
@@ -305,7 +318,7 @@ __global__ __launch_bounds__(256) void k_mt_generate_slab(const uint32_t* __rest
     const uint32_t* cur = buf[b & 1];
     uint32_t* nxt = buf[(b + 1) & 1];
     const bool tw = b < nb;
-    if (tw && t < 227) nxt[t] = mt_mix(cur[t], cur[t + 1], cur[t + 397]);
+    if (tw) twist_chain(cur, nxt, t);
     if (b >= 1) {
       // block b-1 spans offsets [o0, o0 + 312) of plane q0 (wrapping into plane q0 + 1)
       const int64_t e0 = o0 + 311;
@@ -334,13 +347,7 @@ __global__ __launch_bounds__(256) void k_mt_generate_slab(const uint32_t* __rest
       }
     }
     if (!tw) break;
-    __syncthreads();
-    if (t < 227) nxt[227 + t] = mt_mix(cur[227 + t], cur[228 + t], nxt[t]);
-    __syncthreads();
-    if (t < 169) nxt[454 + t] = mt_mix(cur[454 + t], cur[455 + t], nxt[227 + t]);
-    __syncthreads();
-    if (t == 0) nxt[623] = mt_mix(cur[623], nxt[0], nxt[396]);
-    __syncthreads();
+    __syncthreads();  // nxt complete; cur (tempered above) becomes the next nxt
   }
 }
 
