@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <vector>
 #include <cstdlib>
 
 #include "podsgen_kernels.h"
@@ -757,6 +758,335 @@ __global__ __launch_bounds__(64, 1) void k_sbtrd(double* __restrict__ band, int 
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Stage 2, windowed: k_sbtrd_win<B, G>.  The tasks (s, k) of k_sbtrd with its arithmetic,
+// scheduled so the chase runs out of LDS:
+//   * a workgroup runs a GROUP of G consecutive sweeps s0 .. s0+G-1 in lock step: at step
+//     tau, task wave g runs task (s0+g, tau - 3g).  The 3-task lag is k_sbtrd's dependency
+//     ((s, k) after (s-1, k+2)) and the tasks of one step touch disjoint band elements, so
+//     one workgroup barrier per step orders everything;
+//   * the group's band columns live in an LDS ring of W = 9B column slots (64 doubles each,
+//     16-B pairs XOR-swizzled per column so a task wave's 32 columns spread over the banks),
+//     in blocks b = [s0 + bB, s0 + (b+1)B): block b is first touched at step b - 1, and is
+//     final for this group after step b + 4 (the trailing sweep's next column has passed it);
+//   * a LOADER wave requests block tau+4 by LDS-DMA during step tau (the source address
+//     carries the swizzle) into the slots of block tau-5, once the WRITER has read those, and
+//     makes sure block tau+2 has landed before the step's barrier (a fixed vmcnt: every step
+//     issues exactly one block of DMA, past the matrix into a junk slot);
+//   * the WRITER wave writes block tau-5 back (one block of 16-B stores every step, into a
+//     scratch block when none is due) and publishes gprog[q] = the end of the block it stored
+//     two steps earlier (a fixed vmcnt drain, never a fresh store);
+//   * a POLLER wave polls gprog[q-1] (the previous group's written-back boundary) into LDS,
+//     where the loader waits for it.
+//   Workgroup w runs groups w, w + P, ... (persistent grid).
+// ---------------------------------------------------------------------------------------
+// Cross-lane helpers for one wave64 (gfx950): lane l's partner l ^ 32 and l ^ 16 by the
+// permlane swaps, a 32-lane sum by a DPP butterfly (xor 1, 2, then the mirrors, which pair
+// lanes holding equal partial sums) and the permlane16 swap; a lane broadcast by readlane.
+__device__ __forceinline__ double lane_read(double x, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
+                          __builtin_amdgcn_readlane(__double2loint(x), l));
+}
+__device__ __forceinline__ double lane_xor32(double x) {
+  const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+  const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  const bool up = __lane_id() >= 32;
+  return __hiloint2double((int)(up ? b[0] : b[1]), (int)(up ? a[0] : a[1]));
+}
+__device__ __forceinline__ double lane_xor16(double x) {
+  const unsigned lo = (unsigned)__double2loint(x), hi = (unsigned)__double2hiint(x);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const bool odd = (__lane_id() >> 4) & 1;
+  return __hiloint2double((int)(odd ? b[0] : b[1]), (int)(odd ? a[0] : a[1]));
+}
+template <int CTL>
+__device__ __forceinline__ double lane_dpp(double x) {
+  return __hiloint2double(__builtin_amdgcn_mov_dpp(__double2hiint(x), CTL, 0xf, 0xf, false),
+                          __builtin_amdgcn_mov_dpp(__double2loint(x), CTL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ double lane_sum32(double x) {
+  x += lane_dpp<0xB1>(x);   // quad_perm [1, 0, 3, 2]: l ^ 1
+  x += lane_dpp<0x4E>(x);   // quad_perm [2, 3, 0, 1]: l ^ 2
+  x += lane_dpp<0x141>(x);  // row_half_mirror: the other quad of the eight
+  x += lane_dpp<0x140>(x);  // row_mirror: the other eight of the row
+  x += lane_xor16(x);
+  return x;
+}
+
+template <int B, int G>
+struct SbWin {
+  static constexpr int LDB = 2 * B;
+  static constexpr int NBLK = 9;               // ring blocks: tau-5 .. tau+3 (+ tau+4 reusing tau-5)
+  static constexpr int W = NBLK * B;
+  static constexpr int NT = 64 * (G + 3);      // G task waves, loader, writer, poller
+  static constexpr int PER = B * LDB / 2 / 64;  // 16-B pieces per lane per block: 16
+  static constexpr size_t lds_bytes = (size_t)(LDB + W * LDB + 2 * LDB + G * 2 * B) * sizeof(double);
+};
+
+template <int B, int G>
+__global__ __launch_bounds__(64 * (G + 3), 1) void k_sbtrd_win(double* __restrict__ band, int n, int ngroups,
+                                                                uint32_t* __restrict__ gprog,
+                                                                uint32_t* __restrict__ abortw,
+                                                                double* __restrict__ scratch,
+                                                                int64_t* __restrict__ wtr, int wq0) {
+  static_assert(B == 32, "the task maps a 32 x 32 block onto one wave (lane = column, half of the rows)");
+  using P = SbWin<B, G>;
+  constexpr int LDB = P::LDB, W = P::W, H = B / 2, PER = P::PER;
+  constexpr int LOADER = G, WRITER = G + 1, POLLER = G + 2;
+  extern __shared__ __attribute__((aligned(1024))) double sb_sh[];
+  double* ring = sb_sh + LDB;         // [W][LDB], after a zero pad: stray task reads stay finite
+  double* junk = ring + W * LDB;       // two slots: the DMA target past the matrix
+  double* wv_all = junk + 2 * LDB;     // per task wave: vs[B], wvec[B]
+  __shared__ int s_avail, s_wread;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int c = lane & (B - 1), h = lane >> 5;
+  typedef double double2v __attribute__((ext_vector_type(2)));
+  const int nbytes = n * LDB * 8;
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(band, 0, nbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(scratch + (int64_t)blockIdx.x * B * LDB, 0,
+                                                                       B * LDB * 8, 0x00020000);
+  const uint32_t ring_lds = (uint32_t)(uintptr_t)ring, junk_lds = (uint32_t)(uintptr_t)junk;
+  // Every LDS double a task may read is finite: the pad, the ring and the vectors start at zero
+  // and only ever receive band values, so a task reads whole rows/columns unmasked and lets
+  // zero entries of v (and of w) cancel what lies outside its block; its stores outside the
+  // block go to a junk slot per lane instead of being masked.
+  for (int i = t; i < (int)(P::lds_bytes / sizeof(double)); i += P::NT) sb_sh[i] = 0.0;
+  const int jk = W * LDB + lane;  // this lane's junk element (ring-relative)
+  // element d of band column cc in the ring
+  auto ri = [&](int cc, int d) -> int { return (cc % W) * LDB + d; };
+  auto ntask = [&](int s) -> int { return s < n - 2 ? (n - 2 - s + B - 1) / B : 0; };
+  for (int q = blockIdx.x; q < ngroups; q += gridDim.x) {
+    const int s0 = q * G;  // even: the two columns of one DMA share an even slot pair
+    const int gq = min(G, n - 2 - s0);
+    const int tend = ntask(s0) + 3 * (gq - 1);
+    const int nblk = (n - s0 + B - 1) / B;
+    auto blk_end = [&](int b) -> int { return min(n, s0 + (b + 1) * B); };
+    if (t == 0) {
+      s_avail = q == 0 ? n : 0;
+      s_wread = -1;
+    }
+    __syncthreads();
+    auto dma_blk = [&](int b) {  // 16 DMA instructions, always
+      const int half = lane >> 5, p2 = 2 * (lane & 31);
+      const bool real = b < nblk;
+#pragma unroll
+      for (int i = 0; i < B / 2; ++i) {
+        const int cc0 = s0 + b * B + 2 * i;
+        const int cc = cc0 + half;
+        const double* src = band + (int64_t)min(cc, n - 1) * LDB + p2;
+        const uint32_t dst = real ? ring_lds + (uint32_t)((cc0 % W) * LDB * 8) : junk_lds;
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(uintptr_t)dst, 16, 0, 16);
+      }
+    };
+    auto store_blk = [&](int b) {  // 16 store instructions, always
+      const bool real = b >= 0 && b < nblk;
+      // lane l holds 16 B of every two columns: column cb + 2u + l / 32, doubles 2 (l % 32) + {0, 1}
+      const int cb = s0 + b * B;
+      double2v tmp[PER];
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int cc = cb + 2 * u + (lane >> 5);
+        tmp[u] = real ? *reinterpret_cast<const double2v*>(ring + ri(cc, 2 * (lane & 31))) : (double2v){0.0, 0.0};
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the ring reads are done ...
+      if (lane == 0) __hip_atomic_store(&s_wread, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int cc = cb + 2 * u + (lane >> 5);
+        const auto v = __builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b128(rb, 0, 0, 0)), tmp[u]);
+        if (real)
+          __builtin_amdgcn_raw_buffer_store_b128(v, rb, cc < n ? (cc * LDB + 2 * (lane & 31)) * 8 : nbytes, 0, 16u);
+        else
+          __builtin_amdgcn_raw_buffer_store_b128(v, rsc, (lane + 64 * u) * 16, 0, 0u);
+      }
+    };
+    auto lds_wait = [&](int* word, int need) {
+      int spin = 0;
+      while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need && ++spin < SPIN_LIMIT)
+        __builtin_amdgcn_s_sleep(1);
+    };
+    auto poll_until = [&](int need) {  // poller
+      need = min(need, n);
+      if (lane == 0 && q > 0) {
+        int got = __hip_atomic_load(&s_avail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), spin = 0;
+        while (got < need) {
+          got = (int)ld_f(gprog + q - 1);
+          if (got >= need) break;
+          if (++spin > SPIN_LIMIT || ld_f(abortw) != 0) {
+            st_f(abortw, 1u);
+            got = n;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        __hip_atomic_store(&s_avail, got, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    };
+    // ---- prologue: blocks 0 .. 3 requested, 0 and 1 landed --------------------------------
+    if (wave == POLLER) poll_until(blk_end(3));
+    __syncthreads();
+    if (wave == LOADER) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) dma_blk(b);
+      asm volatile("s_waitcnt vmcnt(32)" ::: "memory");  // blocks 0, 1 landed; 2, 3 may fly
+    }
+    __syncthreads();
+    int pend = -1;  // block stored two steps ago (writer)
+    int prev = -1;
+    int64_t* tq = (wtr && q >= wq0 && q < wq0 + 4) ? wtr + (int64_t)(q - wq0) * 512 * 12 : nullptr;
+    for (int tau = 0; tau < tend; ++tau) {
+      int64_t* tr = (tq && tau < 512 && lane == 0) ? tq + tau * 12 : nullptr;
+      if (wave == LOADER) {
+        // block tau+4 into the slots of block tau-5 once the writer has read them; then
+        // block tau+2 (needed from step tau+1) must have landed: blocks tau+3, tau+4 may fly
+        if (tr) tr[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
+        lds_wait(&s_avail, blk_end(tau + 4));
+        if (tr) tr[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // block tau+2 landed (tau+3 may fly)
+        if (tr) tr[2] = (int64_t)__builtin_amdgcn_s_memrealtime();
+        if (tau >= 5) lds_wait(&s_wread, tau - 5);
+        dma_blk(tau + 4);
+        if (tr) tr[3] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      } else if (wave == WRITER) {
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // the block stored two steps ago
+        if (tr) tr[4] = (int64_t)__builtin_amdgcn_s_memrealtime();
+        if (lane == 0 && pend >= 0 && pend < nblk) st_f(gprog + q, (uint32_t)blk_end(pend));
+        pend = prev;
+        prev = tau - 5;
+        store_blk(tau - 5);  // final after step tau-1; a scratch block while tau < 5
+      } else if (wave == POLLER) {
+        poll_until(blk_end(tau + 5));
+      } else if (wave < gq) {
+        const int s = s0 + wave, k = tau - 3 * wave;
+        if (k >= 0 && k < ntask(s)) {
+          const int r0 = s + 1 + k * B;
+          const int r1 = min(r0 + B, n), len = r1 - r0;
+          const int col = k == 0 ? s : r0 - B;
+          const int nl = r0 - col;
+          const int r2 = min(r1 + B, n), nr = r2 - r1;
+          int64_t* tw = (wave == 0) ? tr : nullptr;
+          if (tw) tw[6] = (int64_t)__builtin_amdgcn_s_memrealtime();
+          double* wvec = wv_all + wave * 2 * B + B;
+          // Ring addresses: element (row, cc) at slot(cc) * LDB + row - cc.  L and the lower half
+          // of D are read down one column per lane (immediate offsets); the upper half of D and R
+          // down one row per lane, whose slot steps by one per element and may wrap once.
+          const int ih = H * h;
+          const int bL = ((col + c) % W) * LDB + r0 + ih - col - c;
+          const int bD = ((r0 + c) % W) * LDB + ih - c;
+          const int u0 = (r0 + ih) % W;
+          const int bU = u0 * LDB + c - ih, thr = W - u0;
+          // branch-free selects (sign masks): a select the compiler turns into control flow
+          // keeps 16 exec masks live across the phase
+          auto pick = [](int m, int a, int b) -> int { return b + ((a - b) & m); };  // m ? a : b
+          auto iu = [&](int qq) -> int { return bU + (LDB - 1) * qq - (W * LDB & ((thr - 1 - qq) >> 31)); };
+          const int limL = c < nl ? len - ih : 0;   // qq < limL: a live element of L
+          const int limI = len - ih;                // qq < limI: row i inside the block
+          const int limD = c < len ? limI : 0;
+          const int limR = c < nr ? limI : 0;
+          // ih - c, opaque: otherwise the 16 lane-constant masks (ih + qq >= c) are hoisted
+          // out of the whole kernel loop and spilled
+          int dh = ih - c;
+          asm volatile("" : "+v"(dh));
+          // ---- every read of the task up front: its L, D and R regions are disjoint ---------
+          // (the reflector column col is read by every lane: v is formed where it is used)
+          const int b0 = (col % W) * LDB + r0 - col;  // column col, row r0
+          double L[H], V[H], Dd[H], R[H];
+#pragma unroll
+          for (int qq = 0; qq < H; ++qq) {
+            L[qq] = ring[bL + qq];
+            V[qq] = ring[b0 + ih + qq];
+            Dd[qq] = ring[pick((dh + qq) >> 31, iu(qq), bD + qq)];
+            R[qq] = ring[iu(qq) + len];
+          }
+          const double x0 = ring[b0];
+          const double xc = ring[b0 + c];
+          if (tw) tw[7] = (int64_t)__builtin_amdgcn_s_memrealtime();
+          // ---- the reflector ------------------------------------------------------------------
+          double sq = 0.0;
+#pragma unroll
+          for (int qq = 0; qq < H; ++qq)
+            if (ih + qq >= 1 && qq < limI) sq = fma(V[qq], V[qq], sq);
+          sq += lane_xor32(sq);
+          double beta = x0, tau_h = 0.0, scal = 0.0;
+          if (sq != 0.0) {
+            beta = -copysign(sqrt(fma(x0, x0, sq)), x0);
+            tau_h = (beta - x0) / beta;
+            scal = 1.0 / (x0 - beta);
+          }
+          double v[H];
+#pragma unroll
+          for (int qq = 0; qq < H; ++qq) v[qq] = qq < limI ? (ih + qq == 0 ? 1.0 : V[qq] * scal) : 0.0;
+          const double vc = c < len ? (c == 0 ? 1.0 : xc * scal) : 0.0;
+          if (tw) tw[8] = (int64_t)__builtin_amdgcn_s_memrealtime();
+          // ---- left block: the reflector applied to rows R_k of columns col .. r0-1 -----------
+          {
+            double d = 0.0;
+#pragma unroll
+            for (int qq = 0; qq < H; ++qq) d = fma(v[qq], L[qq], d);
+            d += lane_xor32(d);
+            const double f = tau_h * d;
+#pragma unroll
+            for (int qq = 0; qq < H; ++qq) {
+              L[qq] = c == 0 ? (ih + qq == 0 ? beta : 0.0) : fma(-f, v[qq], L[qq]);
+              ring[pick((qq - limL) >> 31, bL + qq, jk)] = L[qq];
+            }
+          }
+          if (tw) tw[9] = (int64_t)__builtin_amdgcn_s_memrealtime();
+          // ---- right: the rows below (the new bulge) ----------------------------------------
+          {
+            double d = 0.0;
+#pragma unroll
+            for (int qq = 0; qq < H; ++qq) d = fma(R[qq], v[qq], d);
+            d += lane_xor32(d);
+            const double f = tau_h * d;
+#pragma unroll
+            for (int qq = 0; qq < H; ++qq) {
+              R[qq] = fma(-f, v[qq], R[qq]);
+              ring[pick((qq - limR) >> 31, iu(qq) + len, jk)] = R[qq];
+            }
+          }
+          // ---- both sides on the diagonal block ---------------------------------------------
+          {
+            double pc = 0.0;
+#pragma unroll
+            for (int qq = 0; qq < H; ++qq) pc = fma(Dd[qq], v[qq], pc);
+            pc += lane_xor32(pc);
+            pc *= tau_h;
+            double pv = h == 0 ? pc * vc : 0.0;
+            pv = lane_sum32(pv);
+            pv += lane_xor32(pv);
+            const double wc = fma(-0.5 * tau_h * pv, vc, pc);
+            if (h == 0) wvec[c] = c < len ? wc : 0.0;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (tw) tw[10] = (int64_t)__builtin_amdgcn_s_memrealtime();
+#pragma unroll
+            for (int qq = 0; qq < H; ++qq) {
+              const double wi = wvec[ih + qq];
+              Dd[qq] = Dd[qq] - v[qq] * wc - wi * vc;
+              ring[pick(((qq - limD) >> 31) & ~((dh + qq) >> 31), bD + qq, jk)] = Dd[qq];
+            }
+          }
+        }
+        if (wave == 0 && tr) tr[5] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      }
+      __syncthreads();  // step tau done; block tau+2 (first touched at step tau+1) landed
+    }
+    // ---- epilogue: the blocks not yet written back, then the group is done ----------------
+    if (wave == LOADER) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wave == WRITER) {
+      for (int b = max(0, tend - 5); b < nblk; ++b) store_blk(b);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) st_f(gprog + q, (uint32_t)n);
+    }
+    __syncthreads();  // the ring is reused by the next group of this workgroup
+  }
+}
+
 // D, E of the reduced band (band[c*LDB + 0], band[c*LDB + 1]).
 template <int B>
 __global__ void k_tri_out(const double* __restrict__ band, int n, double* __restrict__ D, double* __restrict__ E) {
@@ -1025,6 +1355,7 @@ size_t sy2sb_work_doubles(int n, int nvec, SyevdPlan* plan) {
   p.off_deg = p.off_de + 4LL * n + 8;
   p.off_inv = p.off_deg + 2LL * n + 2;
   p.off_end = p.off_inv + (int64_t)std::max(nvec, 1) * ((int64_t)n * (2 * B + 1 + B) + n);
+  p.off_end += 256LL * B * 2 * B;  // k_sbtrd_win's per-workgroup scratch block (the last 4 MB)
   if (plan) *plan = p;
   return (size_t)p.off_end;
 }
@@ -1095,9 +1426,70 @@ hipError_t launch_syevd2(const double* C, int n, int nvec, double* ws, const Sye
     e = hipMemsetAsync(trace, 0, 256 * 6 * sizeof(int64_t), st);
     if (e != hipSuccess) return e;
   }
-  if (n > 2)
+  if (n > 2 && (trs || std::getenv("PODS_SBTRD_OLD"))) {  // the per-task chase over L2 (diagnostics)
     hipLaunchKernelGGL(sb::k_sbtrd<B>, dim3(NG), dim3(64), 0, st, band, n, NG, prog, abortw + 1, trace,
                        trs ? std::atoi(trs) : -1);
+  } else if (n > 2) {
+    constexpr int GW = 2;
+    using SW = sb::SbWin<B, GW>;
+    const int ngroups = (n - 2 + GW - 1) / GW;
+    int cus = 256, dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int P = std::max(1, std::min(ngroups, cus));
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sb::k_sbtrd_win<B, GW>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)SW::lds_bytes);
+    if (e != hipSuccess) return e;
+    // PODS_SBWIN_TRACE=q0: per-step timestamps of groups q0 .. q0+3 (diagnostics, stderr)
+    const char* wts = std::getenv("PODS_SBWIN_TRACE");
+    int64_t* wtr = nullptr;
+    const size_t wtn = 4 * 512 * 12;
+    if (wts) {
+      e = hipMallocAsync(reinterpret_cast<void**>(&wtr), wtn * sizeof(int64_t), st);
+      if (e == hipSuccess) e = hipMemsetAsync(wtr, 0, wtn * sizeof(int64_t), st);
+      if (e != hipSuccess) return e;
+    }
+    const int wq0 = wts ? std::atoi(wts) : 0;
+    hipLaunchKernelGGL((sb::k_sbtrd_win<B, GW>), dim3(P), dim3(SW::NT), SW::lds_bytes, st, band, n, ngroups, prog,
+                       abortw + 1, ws + p.off_end - 256LL * B * 2 * B, wtr, wq0);
+    if (wtr) {
+      std::vector<int64_t> h(wtn);
+      e = hipMemcpyAsync(h.data(), wtr, wtn * sizeof(int64_t), hipMemcpyDeviceToHost, st);
+      if (e == hipSuccess) e = hipStreamSynchronize(st);
+      (void)hipFreeAsync(wtr, st);
+      if (e != hipSuccess) return e;
+      for (int g = 0; g < 4; ++g) {
+        const int64_t* T = h.data() + (size_t)g * 512 * 12;
+        double a[6] = {0, 0, 0, 0, 0, 0};
+        int cnt = 0;
+        double ph[5] = {0, 0, 0, 0, 0};
+        int pc = 0;
+        for (int k = 0; k + 1 < 512 && T[(k + 1) * 12] != 0; ++k, ++cnt) {
+          const int64_t* R = T + k * 12;
+          a[0] += (R[1] - R[0]) * 0.01;           // loader: wait for the previous group
+          a[1] += (R[2] - R[1]) * 0.01;           // loader: wait for the writer's read
+          a[2] += (R[3] - R[2]) * 0.01;           // loader: DMA issue + landing
+          a[3] += (R[4] - R[0]) * 0.01;           // writer: store drain
+          a[4] += (R[5] - R[0]) * 0.01;           // task wave 0
+          a[5] += (T[(k + 1) * 12] - R[0]) * 0.01;  // step to step
+          if (R[6] != 0) {
+            ph[0] += (R[6] - R[0]) * 0.01;  // task start
+            for (int z = 1; z < 5; ++z) ph[z] += (R[6 + z] - R[5 + z]) * 0.01;
+            ++pc;
+          }
+        }
+        pc = std::max(pc, 1);
+        std::fprintf(stderr, "sbwin group %d task phases us: start %.2f loads %.2f reflector %.2f left %.2f right+w %.2f\n", wq0 + g,
+                     ph[0] / pc, ph[1] / pc, ph[2] / pc, ph[3] / pc, ph[4] / pc);
+        const double lag = g > 0 ? (T[0] - h[(size_t)(g - 1) * 512 * 12]) * 0.01 : 0.0;
+        cnt = std::max(cnt, 1);
+        std::fprintf(stderr,
+                     "sbwin group %d: %d steps, start lag %.2f us; per step us: avail %.2f wread %.2f dma %.2f "
+                     "drain %.2f task %.2f step %.2f\n",
+                     wq0 + g, cnt, lag, a[0] / cnt, a[1] / cnt, a[2] / cnt, a[3] / cnt, a[4] / cnt, a[5] / cnt);
+      }
+    }
+  }
   if (trace) {
     int64_t h[256 * 6];
     e = hipMemcpyAsync(h, trace, sizeof(h), hipMemcpyDeviceToHost, st);
