@@ -765,17 +765,18 @@ __global__ __launch_bounds__(64, 1) void k_sbtrd(double* __restrict__ band, int 
 //     tau, task wave g runs task (s0+g, tau - 3g).  The 3-task lag is k_sbtrd's dependency
 //     ((s, k) after (s-1, k+2)) and the tasks of one step touch disjoint band elements, so
 //     one workgroup barrier per step orders everything;
-//   * the group's band columns live in an LDS ring of W = 9B column slots (64 doubles each,
-//     16-B pairs XOR-swizzled per column so a task wave's 32 columns spread over the banks),
-//     in blocks b = [s0 + bB, s0 + (b+1)B): block b is first touched at step b - 1, and is
-//     final for this group after step b + 4 (the trailing sweep's next column has passed it);
-//   * a LOADER wave requests block tau+4 by LDS-DMA during step tau (the source address
-//     carries the swizzle) into the slots of block tau-5, once the WRITER has read those, and
-//     makes sure block tau+2 has landed before the step's barrier (a fixed vmcnt: every step
-//     issues exactly one block of DMA, past the matrix into a junk slot);
+//   * the group's band columns live in an LDS ring of W = 8B column slots of 64 doubles
+//     (element (row, cc) at slot(cc) * 64 + row - cc: a task lane reading down its column, or
+//     a task row across columns, meets 32 different bank pairs), in blocks
+//     b = [s0 + bB, s0 + (b+1)B): block b is first touched at step b - 1, and is final for
+//     this group after step b + 4 (the trailing sweep's next column has passed it);
+//   * a LOADER wave requests block tau+3 by LDS-DMA during step tau into the slots of block
+//     tau-5, once the WRITER has read those, and makes sure block tau+2 has landed before the
+//     step's barrier (a fixed vmcnt: every step issues exactly one block of DMA, past the
+//     matrix into a junk slot);
 //   * the WRITER wave writes block tau-5 back (one block of 16-B stores every step, into a
 //     scratch block when none is due) and publishes gprog[q] = the end of the block it stored
-//     two steps earlier (a fixed vmcnt drain, never a fresh store);
+//     one step earlier, after draining those stores;
 //   * a POLLER wave polls gprog[q-1] (the previous group's written-back boundary) into LDS,
 //     where the loader waits for it.
 //   Workgroup w runs groups w, w + P, ... (persistent grid).
@@ -818,7 +819,7 @@ __device__ __forceinline__ double lane_sum32(double x) {
 template <int B, int G>
 struct SbWin {
   static constexpr int LDB = 2 * B;
-  static constexpr int NBLK = 9;               // ring blocks: tau-5 .. tau+3 (+ tau+4 reusing tau-5)
+  static constexpr int NBLK = 8;               // ring blocks: tau-5 .. tau+2 (+ tau+3 reusing tau-5)
   static constexpr int W = NBLK * B;
   static constexpr int NT = 64 * (G + 3);      // G task waves, loader, writer, poller
   static constexpr int PER = B * LDB / 2 / 64;  // 16-B pieces per lane per block: 16
@@ -924,40 +925,38 @@ __global__ __launch_bounds__(64 * (G + 3), 1) void k_sbtrd_win(double* __restric
         __hip_atomic_store(&s_avail, got, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     };
-    // ---- prologue: blocks 0 .. 3 requested, 0 and 1 landed --------------------------------
-    if (wave == POLLER) poll_until(blk_end(3));
+    // ---- prologue: blocks 0 .. 2 requested, 0 and 1 landed --------------------------------
+    if (wave == POLLER) poll_until(blk_end(2));
     __syncthreads();
     if (wave == LOADER) {
 #pragma unroll
-      for (int b = 0; b < 4; ++b) dma_blk(b);
-      asm volatile("s_waitcnt vmcnt(32)" ::: "memory");  // blocks 0, 1 landed; 2, 3 may fly
+      for (int b = 0; b < 3; ++b) dma_blk(b);
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // blocks 0, 1 landed; 2 may fly
     }
     __syncthreads();
-    int pend = -1;  // block stored two steps ago (writer)
-    int prev = -1;
+    int prev = -1;  // block stored one step ago (writer)
     int64_t* tq = (wtr && q >= wq0 && q < wq0 + 4) ? wtr + (int64_t)(q - wq0) * 512 * 12 : nullptr;
     for (int tau = 0; tau < tend; ++tau) {
       int64_t* tr = (tq && tau < 512 && lane == 0) ? tq + tau * 12 : nullptr;
       if (wave == LOADER) {
-        // block tau+4 into the slots of block tau-5 once the writer has read them; then
-        // block tau+2 (needed from step tau+1) must have landed: blocks tau+3, tau+4 may fly
+        // block tau+3 into the slots of block tau-5 once the writer has read them; block
+        // tau+2 (first touched at step tau+1) must land within this step: tau+3 may fly
         if (tr) tr[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
-        lds_wait(&s_avail, blk_end(tau + 4));
+        lds_wait(&s_avail, blk_end(tau + 3));
         if (tr) tr[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // block tau+2 landed (tau+3 may fly)
-        if (tr) tr[2] = (int64_t)__builtin_amdgcn_s_memrealtime();
         if (tau >= 5) lds_wait(&s_wread, tau - 5);
-        dma_blk(tau + 4);
+        if (tr) tr[2] = (int64_t)__builtin_amdgcn_s_memrealtime();
+        dma_blk(tau + 3);
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
         if (tr) tr[3] = (int64_t)__builtin_amdgcn_s_memrealtime();
       } else if (wave == WRITER) {
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // the block stored two steps ago
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the block stored one step ago
         if (tr) tr[4] = (int64_t)__builtin_amdgcn_s_memrealtime();
-        if (lane == 0 && pend >= 0 && pend < nblk) st_f(gprog + q, (uint32_t)blk_end(pend));
-        pend = prev;
+        if (lane == 0 && prev >= 0 && prev < nblk) st_f(gprog + q, (uint32_t)blk_end(prev));
         prev = tau - 5;
         store_blk(tau - 5);  // final after step tau-1; a scratch block while tau < 5
       } else if (wave == POLLER) {
-        poll_until(blk_end(tau + 5));
+        poll_until(blk_end(tau + 4));
       } else if (wave < gq) {
         const int s = s0 + wave, k = tau - 3 * wave;
         if (k >= 0 && k < ntask(s)) {
