@@ -816,6 +816,17 @@ __device__ __forceinline__ double lane_sum32(double x) {
   return x;
 }
 
+// sum over qq of a[qq] * b[qq], two interleaved chains
+__device__ __forceinline__ double dot16(const double (&a)[16], const double (&b)[16]) {
+  double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+  for (int qq = 0; qq < 16; qq += 2) {
+    s0 = fma(a[qq], b[qq], s0);
+    s1 = fma(a[qq + 1], b[qq + 1], s1);
+  }
+  return s0 + s1;
+}
+
 template <int B, int G>
 struct SbWin {
   static constexpr int LDB = 2 * B;
@@ -991,22 +1002,30 @@ __global__ __launch_bounds__(64 * (G + 3), 1) void k_sbtrd_win(double* __restric
           // ---- every read of the task up front: its L, D and R regions are disjoint ---------
           // (the reflector column col is read by every lane: v is formed where it is used)
           const int b0 = (col % W) * LDB + r0 - col;  // column col, row r0
+          // a full task (k > 0, no tail) stores every element it holds; the others send the
+          // elements outside their block to the junk slot
+          const bool full = k > 0 && len == B && nr == B;
           double L[H], V[H], Dd[H], R[H];
+          int ad[H];  // D: column c below the diagonal, row c above it (the mirror element)
 #pragma unroll
           for (int qq = 0; qq < H; ++qq) {
+            ad[qq] = pick((dh + qq) >> 31, iu(qq), bD + qq);
             L[qq] = ring[bL + qq];
             V[qq] = ring[b0 + ih + qq];
-            Dd[qq] = ring[pick((dh + qq) >> 31, iu(qq), bD + qq)];
+            Dd[qq] = ring[ad[qq]];
             R[qq] = ring[iu(qq) + len];
           }
           const double x0 = ring[b0];
           const double xc = ring[b0 + c];
           if (tw) tw[7] = (int64_t)__builtin_amdgcn_s_memrealtime();
           // ---- the reflector ------------------------------------------------------------------
-          double sq = 0.0;
+          double sq0 = 0.0, sq1 = 0.0;
 #pragma unroll
-          for (int qq = 0; qq < H; ++qq)
-            if (ih + qq >= 1 && qq < limI) sq = fma(V[qq], V[qq], sq);
+          for (int qq = 0; qq < H; qq += 2) {
+            if (ih + qq >= 1 && qq < limI) sq0 = fma(V[qq], V[qq], sq0);
+            if (qq + 1 < limI) sq1 = fma(V[qq + 1], V[qq + 1], sq1);
+          }
+          double sq = sq0 + sq1;
           sq += lane_xor32(sq);
           double beta = x0, tau_h = 0.0, scal = 0.0;
           if (sq != 0.0) {
@@ -1021,36 +1040,38 @@ __global__ __launch_bounds__(64 * (G + 3), 1) void k_sbtrd_win(double* __restric
           if (tw) tw[8] = (int64_t)__builtin_amdgcn_s_memrealtime();
           // ---- left block: the reflector applied to rows R_k of columns col .. r0-1 -----------
           {
-            double d = 0.0;
-#pragma unroll
-            for (int qq = 0; qq < H; ++qq) d = fma(v[qq], L[qq], d);
+            double d = dot16(v, L);
             d += lane_xor32(d);
             const double f = tau_h * d;
 #pragma unroll
-            for (int qq = 0; qq < H; ++qq) {
-              L[qq] = c == 0 ? (ih + qq == 0 ? beta : 0.0) : fma(-f, v[qq], L[qq]);
-              ring[pick((qq - limL) >> 31, bL + qq, jk)] = L[qq];
+            for (int qq = 0; qq < H; ++qq) L[qq] = c == 0 ? (ih + qq == 0 ? beta : 0.0) : fma(-f, v[qq], L[qq]);
+            if (full) {
+#pragma unroll
+              for (int qq = 0; qq < H; ++qq) ring[bL + qq] = L[qq];
+            } else {
+#pragma unroll
+              for (int qq = 0; qq < H; ++qq) ring[pick((qq - limL) >> 31, bL + qq, jk)] = L[qq];
             }
           }
           if (tw) tw[9] = (int64_t)__builtin_amdgcn_s_memrealtime();
           // ---- right: the rows below (the new bulge) ----------------------------------------
           {
-            double d = 0.0;
-#pragma unroll
-            for (int qq = 0; qq < H; ++qq) d = fma(R[qq], v[qq], d);
+            double d = dot16(R, v);
             d += lane_xor32(d);
             const double f = tau_h * d;
 #pragma unroll
-            for (int qq = 0; qq < H; ++qq) {
-              R[qq] = fma(-f, v[qq], R[qq]);
-              ring[pick((qq - limR) >> 31, iu(qq) + len, jk)] = R[qq];
+            for (int qq = 0; qq < H; ++qq) R[qq] = fma(-f, v[qq], R[qq]);
+            if (full) {
+#pragma unroll
+              for (int qq = 0; qq < H; ++qq) ring[iu(qq) + len] = R[qq];
+            } else {
+#pragma unroll
+              for (int qq = 0; qq < H; ++qq) ring[pick((qq - limR) >> 31, iu(qq) + len, jk)] = R[qq];
             }
           }
           // ---- both sides on the diagonal block ---------------------------------------------
           {
-            double pc = 0.0;
-#pragma unroll
-            for (int qq = 0; qq < H; ++qq) pc = fma(Dd[qq], v[qq], pc);
+            double pc = dot16(Dd, v);
             pc += lane_xor32(pc);
             pc *= tau_h;
             double pv = h == 0 ? pc * vc : 0.0;
@@ -1061,11 +1082,19 @@ __global__ __launch_bounds__(64 * (G + 3), 1) void k_sbtrd_win(double* __restric
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
             if (tw) tw[10] = (int64_t)__builtin_amdgcn_s_memrealtime();
+            // D - (v w' + w v'), symmetric in (i, c) bit for bit: the lane holding the mirror
+            // element computes and stores the same value to the same address
 #pragma unroll
             for (int qq = 0; qq < H; ++qq) {
               const double wi = wvec[ih + qq];
-              Dd[qq] = Dd[qq] - v[qq] * wc - wi * vc;
-              ring[pick(((qq - limD) >> 31) & ~((dh + qq) >> 31), bD + qq, jk)] = Dd[qq];
+              Dd[qq] = Dd[qq] - (v[qq] * wc + wi * vc);
+            }
+            if (full) {
+#pragma unroll
+              for (int qq = 0; qq < H; ++qq) ring[ad[qq]] = Dd[qq];
+            } else {
+#pragma unroll
+              for (int qq = 0; qq < H; ++qq) ring[pick((qq - limD) >> 31, ad[qq], jk)] = Dd[qq];
             }
           }
         }
