@@ -513,12 +513,29 @@ __global__ __launch_bounds__(256) void k_upd(double* __restrict__ A, int64_t lda
       const int gi = i0 + li, gj = j0 + lj;
       aold[c][reg] = (gi < m && gj < m) ? A[(int64_t)(r0 + gi) * lda + r0 + gj] : 0.0;
     }
-  for (int e = t; e < 64 * K2; e += 256) {
-    const int r = e / K2, k = e % K2;
-    const int gi = i0 + r, gj = j0 + r;
-    // L row i = [V_i, W_i], R row j = [W_j, V_j]: sum_k L_ik R_jk = V_i.W_j + W_i.V_j
-    Ls[r * LD + k] = gi < m ? (k < B ? Vx[(int64_t)gi * B + k] : W[(int64_t)gi * B + k - B]) : 0.0;
-    Rs[r * LD + k] = gj < m ? (k < B ? W[(int64_t)gj * B + k] : Vx[(int64_t)gj * B + k - B]) : 0.0;
+  // L row i = [V_i, W_i], R row j = [W_j, V_j]: sum_k L_ik R_jk = V_i.W_j + W_i.V_j.
+  // All 2 x 16 operand loads of a thread go out before any LDS store (a rolled load -> store
+  // loop paid one L2 round trip per element pair: 26 us per tile, 2 TB/s for the kernel).
+  static_assert(K2 == 64, "thread t stages column k = t % 64 of rows 4 it + t / 64");
+  {
+    constexpr int NIT = 64 * K2 / 256;
+    const int k = t & (K2 - 1), rb = t >> 6;
+    const double* lsrc = k < B ? Vx + k : W + (k - B);
+    const double* rsrc = k < B ? W + k : Vx + (k - B);
+    double lv[NIT], rv[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int r = 4 * it + rb;
+      const int gi = i0 + r, gj = j0 + r;
+      lv[it] = gi < m ? lsrc[(int64_t)gi * B] : 0.0;
+      rv[it] = gj < m ? rsrc[(int64_t)gj * B] : 0.0;
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int r = 4 * it + rb;
+      Ls[r * LD + k] = lv[it];
+      Rs[r * LD + k] = rv[it];
+    }
   }
   __syncthreads();
   f64x4 acc[4];
