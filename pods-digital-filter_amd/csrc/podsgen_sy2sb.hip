@@ -98,7 +98,7 @@ __global__ __launch_bounds__(256, 1) void k_pqr(double* __restrict__ A, int64_t 
                                                uint32_t* __restrict__ flags, uint32_t epoch, uint32_t seq0,
                                                uint32_t* __restrict__ abortw, double* __restrict__ Vx,
                                                double* __restrict__ tau, double* __restrict__ gpart,
-                                               double* __restrict__ Tout) {
+                                               double* __restrict__ Tout, int64_t* __restrict__ ptrace) {
   static_assert(B == 32, "k_pqr: one half-wave per panel row group (lane = column)");
   constexpr int RG = 256 / B;   // 8 row groups (half-waves)
   constexpr int NR = 256 / RG;  // rows per thread: RP <= 256
@@ -120,17 +120,31 @@ __global__ __launch_bounds__(256, 1) void k_pqr(double* __restrict__ A, int64_t 
     P[i] = r < nl ? A[(int64_t)(r0 + g0 + r) * lda + c0 + kq] : 0.0;
   }
   const int kc = min(m, B);
+  int64_t* ptr = (ptrace && w == 0 && t == 0) ? ptrace : nullptr;  // diagnostics: per-column stamps
+  auto stamp = [&](int j, int q) {
+    if (ptr) ptr[j * 8 + q] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  };
   for (int j = 0; j < kc; ++j) {
+    stamp(j, 0);
     // column j of my rows, from lane j of the half-wave
     double pj[NR];
 #pragma unroll
     for (int i = 0; i < NR; ++i) pj[i] = __shfl(P[i], src0 + j);
-    double acc = 0.0;
+    // rows rg + RG i with i >= B / RG lie past row B > j in every workgroup, and rows past
+    // the panel hold zeros: only the first B / RG slots need the row conditions
+    constexpr int IG = B / RG;
+    double acc = 0.0, acc1 = 0.0;
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
+    for (int i = 0; i < IG; ++i) {
       const int gr = g0 + rg + RG * i;
       if (gr > j && rg + RG * i < nl) acc = fma(pj[i], P[i], acc);
     }
+#pragma unroll
+    for (int i = IG; i < NR; i += 2) {
+      acc = fma(pj[i], P[i], acc);
+      acc1 = fma(pj[i + 1], P[i + 1], acc1);
+    }
+    acc += acc1;
     red[rg][kq] = kq >= j ? acc : 0.0;
     // the pivot row's owner keeps row j for the publish
     if (j >= g0 && j < g1 && rg == (j - g0) % RG) {
@@ -141,7 +155,9 @@ __global__ __launch_bounds__(256, 1) void k_pqr(double* __restrict__ A, int64_t 
         if (q == i) pr = P[q];
       rowj[kq] = pr;
     }
+    stamp(j, 1);
     __syncthreads();  // B1: the row-group partials are in red
+    stamp(j, 2);
     // Hand-off without flags: every published double carries the column's tag in its two
     // lowest mantissa bits (the sequence number c = 16 panel + j/2 + 1 differs by 1 from the
     // previous write to the same slot, and the slots are zeroed per call), so consumers spin
@@ -156,6 +172,7 @@ __global__ __launch_bounds__(256, 1) void k_pqr(double* __restrict__ A, int64_t 
       bst(rpub, pbase + t, tagged(sp, tag));
       if (j >= g0 && j < g1) bst(rpub, pbase + B + t, tagged(rowj[t], tag));
     }
+    stamp(j, 3);
     {
       const int qb = (j & 1) * NW * 2 * B;
       const int own = j / RP;  // the workgroup holding pivot row j
@@ -180,13 +197,22 @@ __global__ __launch_bounds__(256, 1) void k_pqr(double* __restrict__ A, int64_t 
         __builtin_amdgcn_s_sleep(1);
       }
     }
+    stamp(j, 4);
     __syncthreads();  // B2: every partial and the pivot row are in LDS
-    if (t < B) {
+    {  // S[k] = sum over workgroups: 8 interleaved partial sums (fixed order everywhere)
       double sacc = 0.0;
-      for (int q = 0; q < NW; ++q) sacc += gsum[q * B + t];
-      S[t] = sacc;
+      for (int q = rg; q < NW; q += RG) sacc += gsum[q * B + kq];
+      red[rg][kq] = sacc;
     }
     __syncthreads();  // B3
+    if (t < B) {
+      double sacc = red[0][t];
+#pragma unroll
+      for (int q = 1; q < RG; ++q) sacc += red[q][t];
+      S[t] = sacc;
+    }
+    __syncthreads();  // B3b
+    stamp(j, 5);
     // ---- reflector (dlarfg), redundantly in every thread -----------------------------
     const double alpha = rowj[j], sigma = S[j];
     double beta = alpha, tj = 0.0, scal = 0.0;
@@ -202,15 +228,27 @@ __global__ __launch_bounds__(256, 1) void k_pqr(double* __restrict__ A, int64_t 
     const double wk = (kq > j) ? fma(scal, S[kq], rowj[kq]) : 0.0;
     const double f = -tj * wk;
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
+    for (int i = 0; i < IG; ++i) {
       const int gr = g0 + rg + RG * i;
       if (gr < j) continue;
       const double v = gr == j ? 1.0 : scal * pj[i];
       if (kq > j) P[i] = fma(f, v, P[i]);
       else if (kq == j) P[i] = gr == j ? beta : v;
     }
+    {  // rows past B: P <- P + f v (columns k > j; f = 0 below), v itself in column j
+      const double fe = kq > j ? f : 0.0;
+      const bool cj = kq == j;
+#pragma unroll
+      for (int i = IG; i < NR; ++i) {
+        const double v = scal * pj[i];
+        const double u = fma(fe, v, P[i]);
+        P[i] = cj ? v : u;
+      }
+    }
+    stamp(j, 6);
     __syncthreads();  // rowj / S are rewritten by the next column
   }
+  if (ptr) ptr[kc * 8] = (int64_t)__builtin_amdgcn_s_memrealtime();
   // ---- outputs: explicit V and R; V (explicit) kept in registers for the Gram ----------
 #pragma unroll
   for (int i = 0; i < NR; ++i) {
@@ -1430,9 +1468,36 @@ hipError_t launch_syevd2(const double* C, int n, int nvec, double* ws, const Sye
     double* tau = ws + p.off_tau + (int64_t)pi * B;
     const int NW = std::max(1, std::min(64, (m + p.RP - 1) / p.RP));
     const int RP = (m + NW - 1) / NW;
+    // PODS_PQR_TRACE=pi: per-column phase stamps of workgroup 0 in panel pi (diagnostics, stderr)
+    const char* pqt = std::getenv("PODS_PQR_TRACE");
+    int64_t* ptrace = nullptr;
+    if (pqt && std::atoi(pqt) == pi) {
+      e = hipMallocAsync(reinterpret_cast<void**>(&ptrace), (B * 8 + 1) * sizeof(int64_t), st);
+      if (e == hipSuccess) e = hipMemsetAsync(ptrace, 0, (B * 8 + 1) * sizeof(int64_t), st);
+      if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(sb::k_pqr<B>, dim3(NW), dim3(256), 0, st, Aw, (int64_t)n, r0, c0, m, RP, NW,
                        ws + p.off_pub, pflags, epoch * 1024u + (uint32_t)pi, 16u * (uint32_t)pi + 1u, abortw, Vx,
-                       tau, ws + p.off_zp, T);
+                       tau, ws + p.off_zp, T, ptrace);
+    if (ptrace) {
+      int64_t h[B * 8 + 1];
+      e = hipMemcpyAsync(h, ptrace, sizeof(h), hipMemcpyDeviceToHost, st);
+      if (e == hipSuccess) e = hipStreamSynchronize(st);
+      (void)hipFreeAsync(ptrace, st);
+      if (e != hipSuccess) return e;
+      double a[7] = {0, 0, 0, 0, 0, 0, 0};
+      for (int j = 0; j < B; ++j) {
+        const int64_t* R = h + j * 8;
+        const int64_t nx = j + 1 < B ? h[(j + 1) * 8] : h[B * 8];
+        for (int q = 0; q < 6; ++q) a[q] += (R[q + 1] - R[q]) * 0.01;
+        a[6] += (nx - R[6]) * 0.01;
+      }
+      std::fprintf(stderr,
+                   "k_pqr panel %d (m = %d, NW = %d, RP = %d) per column us: shfl+dot %.2f B1 %.2f publish %.2f "
+                   "hop %.2f B2+sum+B3 %.2f reflector+update %.2f B4 %.2f; total %.2f\n",
+                   pi, m, NW, RP, a[0] / B, a[1] / B, a[2] / B, a[3] / B, a[4] / B, a[5] / B, a[6] / B,
+                   (h[B * 8] - h[0]) * 0.01 / B);
+    }
     // ~4 workgroups per CU for the A22 read: K splits of >= 256 columns
     const int ks = std::max(1, std::min(p.KS, (1024 + (m + 63) / 64 - 1) / ((m + 63) / 64)));
     const int kchunk = ((m + ks - 1) / ks + 31) / 32 * 32;
