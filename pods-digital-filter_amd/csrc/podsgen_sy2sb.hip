@@ -104,8 +104,11 @@ __global__ __launch_bounds__(256, 1) void k_pqr(double* __restrict__ A, int64_t 
   constexpr int NR = 256 / RG;  // rows per thread: RP <= 256
   constexpr int LDP = B + 1;
   __shared__ double red[RG][B];
-  __shared__ double S[B], rowj[B], taul[B];
+  __shared__ double S[B], rowjb[2][B], taul[B];
   __shared__ double gsum[64 * B];
+  // column j of each row group, written by the lane holding it (kq == j) during column j-1's
+  // update and read back by its half-wave (same wave: no barrier) in place of 32 shuffles
+  __shared__ __attribute__((aligned(16))) double colb[RG][NR];
   __shared__ double G[B][LDP], Ts[B][LDP];
   const int w = blockIdx.x, t = threadIdx.x;
   const int kq = t % B, rg = t / B;
@@ -124,12 +127,24 @@ __global__ __launch_bounds__(256, 1) void k_pqr(double* __restrict__ A, int64_t 
   auto stamp = [&](int j, int q) {
     if (ptr) ptr[j * 8 + q] = (int64_t)__builtin_amdgcn_s_memrealtime();
   };
+  if (kq == 0) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i) colb[rg][i] = P[i];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
   for (int j = 0; j < kc; ++j) {
     stamp(j, 0);
-    // column j of my rows, from lane j of the half-wave
+    double* rowj = rowjb[j & 1];  // double-buffered: no barrier at the end of the column
+    // column j of my rows (lane j of the half-wave), broadcast from colb
     double pj[NR];
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-    for (int i = 0; i < NR; ++i) pj[i] = __shfl(P[i], src0 + j);
+    for (int i = 0; i < NR; i += 2) {
+      const double2 q = *reinterpret_cast<const double2*>(&colb[rg][i]);
+      pj[i] = q.x;
+      pj[i + 1] = q.y;
+    }
     // rows rg + RG i with i >= B / RG lie past row B > j in every workgroup, and rows past
     // the panel hold zeros: only the first B / RG slots need the row conditions
     constexpr int IG = B / RG;
@@ -245,8 +260,15 @@ __global__ __launch_bounds__(256, 1) void k_pqr(double* __restrict__ A, int64_t 
         P[i] = cj ? v : u;
       }
     }
+    if (kq == j + 1) {  // the next column, for this half-wave
+#pragma unroll
+      for (int i = 0; i < NR; i += 2)
+        *reinterpret_cast<double2*>(&colb[rg][i]) = make_double2(P[i], P[i + 1]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     stamp(j, 6);
-    __syncthreads();  // rowj / S are rewritten by the next column
+    // no barrier here: rowj alternates, S and red are rewritten only after the next B1
   }
   if (ptr) ptr[kc * 8] = (int64_t)__builtin_amdgcn_s_memrealtime();
   // ---- outputs: explicit V and R; V (explicit) kept in registers for the Gram ----------
