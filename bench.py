@@ -15,7 +15,7 @@ N > 1 runs one process per GPU under torch.distributed.run; the inlet rows are s
 into N slabs (strong scaling: the same 256^2 x 4096 problem at every N).
 
 Extra JSON objects (rank 0):
-  roofline      the dominant kernel (pods_corr: k_syrk_glds + k_syrk_reduce), fp64 MFMA
+  roofline      the dominant kernel (pods_corr: k_syrk_g128 + k_syrk_reduce), fp64 MFMA
                 bound; achieved = 3*P*ns*(ns+1) algorithmic flops per launch / mean launch
                 time from HIP events recorded around it on its stream inside the timed
                 steps; traffic from the committed rocprofv3 PMC summary (profiles/) when
@@ -263,7 +263,7 @@ def main():
                      "synthetic (seeded MT19937 random field, built tanh/top-hat profile)"),
             "config": {"workload": desc, "jma": J, "kma": K, "ns": ns, "nm": setup.nm,
                        "nf": [setup.nfx, setup.nfy, setup.nfz], "parallelism": "row-slab dp%d" % world},
-            "roofline": {"kernel": "pods_corr (k_syrk_glds + k_syrk_reduce), rank 0",
+            "roofline": {"kernel": "pods_corr (k_syrk_g128 + k_syrk_reduce), rank 0",
                          "bound": "mfma", "achieved": round(achieved, 3),
                          "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / FP64_MFMA_PEAK_TFLOPS, 4),

@@ -169,8 +169,9 @@ struct RngBuffers {
 };
 
 // SYRK work items {bi, bj, split, 0}: split-major, then 8x8 super-blocks of 128x128 tiles
-// in the lower triangle, tiles row-major inside a super-block.  Consecutive items go to one
-// XCD, so the 64 workgroups an XCD holds at once cover one super-block: 16 panels, one K range.
+// in the lower triangle, tiles row-major inside a super-block (kernels 1 and 3).  Consecutive
+// items go to one XCD, so the 64 workgroups an XCD holds at once (two per CU) cover one
+// super-block: 16 panels, one K range.
 std::vector<int> syrk_items(int kernel, int ns, int nsplit) {
   std::vector<int> it;
   auto push = [&](int bi, int bj, int s) {
@@ -201,9 +202,13 @@ std::vector<int> syrk_items(int kernel, int ns, int nsplit) {
   return it;
 }
 
+// 3 (default): 128 x 128 tiles, two workgroups per CU; 2: 256 x 128 tiles, one per CU
+// (1.9 ms slower at C3); 1: the register-staged v1.
 int syrk_kernel_choice() {
   const char* e = std::getenv("PODS_SYRK_KERNEL");
-  return (e && e[0] == '1') ? 1 : 2;
+  if (e && e[0] == '1') return 1;
+  if (e && e[0] == '2') return 2;
+  return 3;
 }
 
 }  // namespace
@@ -561,7 +566,7 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
   const int ns = c->p.ns;
   const int kern = syrk_kernel_choice();
   const int nsplit = pods::syrk_plan(kern, ns, c->rowpad, &ksplit);
-  if (nsplit > 1 || kern == 2) PODS_HIP(ensure(c->cwork, (size_t)nsplit * ns * ns * sizeof(double)));
+  if (nsplit > 1 || kern >= 2) PODS_HIP(ensure(c->cwork, (size_t)nsplit * ns * ns * sizeof(double)));
   const int64_t key = ((int64_t)kern << 40) | ((int64_t)ns << 20) | nsplit;
   if (c->items_key != key) {
     std::vector<int> items = syrk_items(kern, ns, nsplit);

@@ -961,6 +961,113 @@ __global__ __launch_bounds__(512, 1) void k_syrk_glds(const double* __restrict__
       }
 }
 
+// SYRK v3: one 128 x 128 tile per 256-thread workgroup, TWO workgroups per CU (2-stage
+// LDS-DMA ring, 66.5 KB each): the two workgroups' K-tile barriers are independent, so one
+// keeps the fp64 MFMA pipe fed while the other waits at its barrier (v2 stalls all 8 waves of
+// its single workgroup at every barrier).  Same operand layout, swizzle, mean slot and
+// lower-triangle partial output as v2; 4 waves as 2 x 2, each 64 x 64.
+namespace syrk3 {
+constexpr int BM = 128, BN = 128, KT = 16, NST = 2, NW = 4;
+constexpr int XB = BM * KT * 8;            // 16 KB
+constexpr int YB = BN * KT * 8;            // 16 KB
+constexpr int MBYTES = NW * 128;
+constexpr int STAGE = XB + YB + MBYTES;
+constexpr int XP = XB / 1024 / NW;         // 4
+constexpr int YP = YB / 1024 / NW;         // 4
+}  // namespace syrk3
+
+template <int CENTRED>
+__global__ __launch_bounds__(256, 2) void k_syrk_g128(const double* __restrict__ AT, int ns,
+                                                      int64_t Kdim, const double* __restrict__ mean,
+                                                      const int4* __restrict__ items, int nitems,
+                                                      int64_t ksplit, double* __restrict__ work,
+                                                      int64_t ldc, int64_t slab) {
+  using namespace syrk3;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int b = blockIdx.x;
+  const int xcd = b & 7, qq = nitems >> 3, rr = nitems & 7;
+  const int logical = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
+  const int4 it = items[logical];
+  const int bi = it.x, bj = it.y, sp = it.z;
+  const int i0 = bi * BM, j0 = bj * BN;
+  const int64_t kt0 = (int64_t)sp * (ksplit / KT);
+  const int64_t kt1 = min(Kdim, (int64_t)(sp + 1) * ksplit) / KT;
+  const int nt = (int)(kt1 - kt0);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave >> 1, wc = wave & 1;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+  const int lrow = lane >> 3, lslot = lane & 7;
+  int64_t xsrc[XP], ysrc[YP];
+#pragma unroll
+  for (int q = 0; q < XP; ++q) {
+    const int R = (wave * XP + q) * 8 + lrow;
+    xsrc[q] = ((int64_t)min(i0 + R, ns - 1) << 4) + ((lslot ^ ((R >> 1) & 7)) << 1);
+  }
+#pragma unroll
+  for (int q = 0; q < YP; ++q) {
+    const int R = (wave * YP + q) * 8 + lrow;
+    ysrc[q] = ((int64_t)min(j0 + R, ns - 1) << 4) + ((lslot ^ ((R >> 1) & 7)) << 1);
+  }
+  const int64_t blk = (int64_t)ns << 4;
+  auto issue = [&](int t) {
+    const int64_t kt = kt0 + t;
+    const uint32_t base = lds0 + (uint32_t)((t % NST) * STAGE);
+    const double* g = AT + kt * blk;
+#pragma unroll
+    for (int q = 0; q < XP; ++q) glds16(g + xsrc[q], base + (wave * XP + q) * 1024);
+#pragma unroll
+    for (int q = 0; q < YP; ++q) glds16(g + ysrc[q], base + XB + (wave * YP + q) * 1024);
+    if (lane < 8) glds16(mean + kt * KT + (lane << 1), base + XB + YB + wave * 128);
+  };
+  f64x4 acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = (f64x4){0.0, 0.0, 0.0, 0.0};
+  if (nt > 0) issue(0);
+  const int fr = lane & 15, fk = lane >> 4, fs = (fr >> 1) & 7;
+  const int xrow = (wr * 64 + fr) << 4, yrow = (wc * 64 + fr) << 4;
+  for (int t = 0; t < nt; ++t) {
+    // K-tile t landed (the only DMA outstanding); after the barrier every wave has also
+    // finished reading stage (t+1) % 2 (K-tile t-1), which K-tile t+1 now overwrites
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < nt) issue(t + 1);
+    const char* st = smem + (t % NST) * STAGE;
+    const double* Xs = reinterpret_cast<const double*>(st);
+    const double* Ys = reinterpret_cast<const double*>(st + XB);
+    const double* Ms = reinterpret_cast<const double*>(st + XB + YB + wave * 128);
+#pragma unroll
+    for (int kk = 0; kk < KT; kk += 4) {
+      const int k = kk + fk;
+      const int koff = ((((k >> 1) ^ fs)) << 1) + (k & 1);
+      const double mk = Ms[k];
+      double a[4], bv[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) a[m] = CENTRED ? Xs[xrow + koff + m * 256] : Xs[xrow + koff + m * 256] - mk;
+#pragma unroll
+      for (int n = 0; n < 4; ++n) bv[n] = CENTRED ? Ys[yrow + koff + n * 256] : Ys[yrow + koff + n * 256] - mk;
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], bv[n], acc[m][n], 0, 0, 0);
+    }
+  }
+  double* dst = work + (int64_t)sp * slab;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int gi = i0 + wr * 64 + m * 16 + fk + 4 * reg;
+        const int gj = j0 + wc * 64 + n * 16 + fr;
+        if (gi < ns && gj <= gi) dst[(int64_t)gi * ldc + gj] = acc[m][n][reg];
+      }
+}
+
 // C[i][j] = (sum_s part_s[max][min]) [/ ns], splits summed in order.
 // Sum of the split-K slabs (split order: v = ((p0 + p1) + p2) + ...) over 64x64 tiles of the
 // lower triangle; each tile is written to C and, through LDS, transposed into the upper
@@ -1462,6 +1569,22 @@ hipError_t launch_syrk(int kernel, const double* AT, int64_t ld, int ns, int64_t
                        double* C, int64_t ldc, int divide, double* work, int centred, hipStream_t st) {
   const int64_t slab = (int64_t)ns * ldc;
   const int final_write = nsplit == 1;
+  if (kernel == 3) {
+    auto launch = [&](auto kern) -> hipError_t {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         syrk3::NST * syrk3::STAGE);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(kern, dim3(nitems), dim3(256), syrk3::NST * syrk3::STAGE, st, AT, ns, Kdim,
+                         mean, reinterpret_cast<const int4*>(items), nitems, ksplit, work, ldc, slab);
+      return hipGetLastError();
+    };
+    hipError_t le = centred ? launch(k_syrk_g128<1>) : launch(k_syrk_g128<0>);
+    if (le != hipSuccess) return le;
+    hipLaunchKernelGGL(k_syrk_reduce, dim3(((ns + 63) / 64) * ((ns + 63) / 64 + 1) / 2), dim3(256), 0, st, work, nsplit, slab,
+                       ns, ldc, C, divide);
+    return hipGetLastError();
+  }
   if (kernel == 2) {
     auto launch = [&](auto kern) -> hipError_t {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
