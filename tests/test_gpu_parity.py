@@ -219,10 +219,14 @@ def test_fourier_rank_matches_host(ctx, et):
         assert np.array_equal(E.fc_rows(c, ci, cc), ref_FC), ns
 
 
-def test_syrk_mfma_layout(ctx):
-    """Asymmetric data through pods_set_snapshots: catches row/col swaps in the MFMA C map."""
+@pytest.mark.parametrize("kernel", ["3", "2", "1"])
+def test_syrk_mfma_layout(ctx, monkeypatch, kernel):
+    """Asymmetric data through pods_set_snapshots: catches row/col swaps in the MFMA C map,
+    for each SYRK kernel (3: 128x128 tiles, two workgroups per CU, the default; 2: 256x128;
+    1: register-staged), including a case with several tile rows and K splits."""
+    monkeypatch.setenv("PODS_SYRK_KERNEL", kernel)
     rng = np.random.default_rng(3)
-    for ns, rows in [(64, 300), (100, 1000), (130, 77), (1, 5)]:
+    for ns, rows in [(64, 300), (100, 1000), (130, 77), (1, 5), (300, 5000)]:
         A = rng.standard_normal((rows, ns)) * np.arange(1, ns + 1)[None, :] + np.arange(rows)[:, None]
         snap = E.load_snapshots(A, ctx=ctx)
         mean = torch.empty(rows, dtype=torch.float64, device="cuda")
