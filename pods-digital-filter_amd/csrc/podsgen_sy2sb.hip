@@ -1303,30 +1303,69 @@ __global__ __launch_bounds__(256) void k_band_invit(const double* __restrict__ b
   for (int it = 0; it < 2; ++it) {
     if (t < 64) {
       const int lane = t;
+      // The loads of both solves do not depend on the recurrence: they run PD rows ahead
+      // in registers (a load inside the chain cost one memory round trip per row).
+      constexpr int PD = 8;
       // forward: lanes 0..B hold x[j..j+B] (lane 0 = x[j])
       double wv = lane <= B && lane < n ? x[lane] : 0.0;
-      for (int j = 0; j < n; ++j) {
-        const int p = ipiv[j] - j;
-        const double v0 = __shfl(wv, 0), vp = __shfl(wv, p);
-        if (lane == 0) wv = vp;
-        if (lane == p) wv = v0;
-        const double xj = __shfl(wv, 0);
-        if (lane >= 1 && lane <= B) wv = fma(-Lm[(int64_t)j * B + lane - 1], xj, wv);
-        if (lane == 0) x[j] = xj;
-        const double nxt = __shfl_down(wv, 1);
-        wv = lane < B ? nxt : ((j + 1 + B < n) ? x[j + 1 + B] : 0.0);
+      {
+        double lq[PD], xq[PD];
+        int pq[PD];
+        auto fetch = [&](int d, int j) {
+          const bool in = j < n;
+          lq[d] = (in && lane >= 1 && lane <= B) ? Lm[(int64_t)j * B + lane - 1] : 0.0;
+          xq[d] = (in && j + 1 + B < n) ? x[j + 1 + B] : 0.0;
+          pq[d] = in ? ipiv[j] - j : 0;
+        };
+#pragma unroll
+        for (int d = 0; d < PD; ++d) fetch(d, d);
+        for (int j0 = 0; j0 < n; j0 += PD) {
+#pragma unroll
+          for (int d = 0; d < PD; ++d) {
+            const int j = j0 + d;
+            if (j < n) {
+              const int p = __builtin_amdgcn_readfirstlane(pq[d]);
+              const double v0 = lane_read(wv, 0), vp = lane_read(wv, p);
+              if (lane == 0) wv = vp;
+              if (lane == p) wv = v0;
+              const double xj = lane_read(wv, 0);
+              if (lane >= 1 && lane <= B) wv = fma(-lq[d], xj, wv);
+              if (lane == 0) x[j] = xj;
+              const double nxt = __shfl_down(wv, 1);
+              wv = lane < B ? nxt : xq[d];
+            }
+            fetch(d, j + PD);
+          }
+        }
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
       // backward: lanes 0..2B-1 hold x[j+1..j+2B]
       double wb = 0.0;
-      for (int j = n - 1; j >= 0; --j) {
-        const double uj = (j + 1 + lane < n) ? U[(int64_t)j * WC + 1 + lane] : 0.0;
-        double sdot = uj * wb;
-        for (int o = 32; o >= 1; o >>= 1) sdot += __shfl_xor(sdot, o);
-        const double xj = (x[j] - sdot) / U[(int64_t)j * WC];
-        if (lane == 0) x[j] = xj;
-        const double up = __shfl_up(wb, 1);
-        wb = lane == 0 ? xj : up;
+      {
+        double uq[PD], dq[PD], xq[PD];
+        auto fetch = [&](int d, int j) {
+          const bool in = j >= 0;
+          uq[d] = (in && j + 1 + lane < n) ? U[(int64_t)j * WC + 1 + lane] : 0.0;
+          dq[d] = in ? U[(int64_t)j * WC] : 1.0;
+          xq[d] = in ? x[j] : 0.0;  // the forward result: row j is rewritten only at step j
+        };
+#pragma unroll
+        for (int d = 0; d < PD; ++d) fetch(d, n - 1 - d);
+        for (int j0 = n - 1; j0 >= 0; j0 -= PD) {
+#pragma unroll
+          for (int d = 0; d < PD; ++d) {
+            const int j = j0 - d;
+            if (j >= 0) {
+              double sdot = uq[d] * wb;
+              for (int o = 32; o >= 1; o >>= 1) sdot += __shfl_xor(sdot, o);
+              const double xj = (xq[d] - sdot) / dq[d];
+              if (lane == 0) x[j] = xj;
+              const double up = __shfl_up(wb, 1);
+              wb = lane == 0 ? xj : up;
+            }
+            fetch(d, j - PD);
+          }
+        }
       }
     }
     __syncthreads();
