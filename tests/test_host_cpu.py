@@ -304,3 +304,27 @@ def test_gloo_multirank_correlation_and_gather(world):
     full = np.frombuffer(out[0][1]).reshape(3 * J * K, ns + 1)
     assert np.array_equal(full[:, 0], mean)
     assert np.array_equal(full[:, 1:], Ac)
+
+
+def test_num_valid_modes_vectorised_matches_reference_loop():
+    """host.num_valid_modes (vectorised, on the step's critical path) against the literal
+    PODFS.py:1312-1317 loop: sorted/unsorted spectra, zeros, negatives, energy[0] = 0,
+    every ns parity, three tolerances."""
+    import warnings
+    from podsgen.host import num_valid_modes, num_valid_modes_loop
+    rng = np.random.default_rng(0)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for ns in list(range(1, 12)) + [50, 51, 4096, 4097]:
+            for trial in range(120 if ns < 60 else 10):
+                e = np.sort(rng.standard_normal(ns) * 10.0 ** rng.uniform(-20, 3, ns))[::-1].copy()
+                if trial % 5 == 0:
+                    e = np.abs(e)
+                if trial % 7 == 0 and ns > 3:
+                    e[rng.integers(ns)] = 0.0
+                if trial % 11 == 0:
+                    e[0] = 0.0
+                if trial % 13 == 0:
+                    e = np.abs(rng.standard_normal(ns))
+                for tol in (1e-15, 1e-3, 0.5):
+                    assert num_valid_modes(e, ns, tol) == num_valid_modes_loop(e, ns, tol), (ns, tol, trial)
