@@ -242,7 +242,9 @@ def main():
     P_local = (gen.j1 - gen.j0) * K
     flops = 3.0 * P_local * ns * (ns + 1)
     achieved = flops / (corr_ms * 1e-3) / 1e12
-    traffic = load_traffic(args.config, ns, rank)
+    # the committed PMC summary is for the one-GPU launch; a rank's launch at N > 1 covers
+    # only its row slab, so no measured figure applies there
+    traffic = load_traffic(args.config, ns, rank) if world == 1 else None
     if world > 1:
         dist.barrier()
     if rank == 0:

@@ -389,8 +389,11 @@ __global__ __launch_bounds__(256) void k_filter_x(const double* __restrict__ R,
 }
 
 // The same x pass on two adjacent points per thread (16-B loads and stores; Sl even, so every
-// plane starts 16-B aligned).  Per point the arithmetic is identical to k_filter_x.
-template <int NX>
+// plane starts 16-B aligned).  Per point the arithmetic is identical to k_filter_x.  The plane
+// that enters the window at step i is loaded PD steps ahead (a register queue), so each wave
+// keeps PD loads in flight instead of waiting for one load per step (the compiler issued the
+// step's load and then drained vmcnt(0) before its last tap).
+template <int NX, int PD>
 __global__ __launch_bounds__(256) void k_filter_x2(const double* __restrict__ R,
                                                    const double* __restrict__ bx, int ns,
                                                    int64_t Sl, int steps_per_chunk,
@@ -410,8 +413,16 @@ __global__ __launch_bounds__(256) void k_filter_x2(const double* __restrict__ R,
   double2 w[NX];
 #pragma unroll
   for (int a = 0; a < NX - 1; ++a) w[a] = R2[stream_plane(c, i0 + a, NX) * Sl2 + pp];
+  // pf[d] = the plane entering the window at step i + d (planes up to i1 + NX - 2 exist)
+  double2 pf[PD];
+#pragma unroll
+  for (int d = 0; d < PD; ++d)
+    pf[d] = i0 + d < i1 ? R2[stream_plane(c, i0 + d + NX - 1, NX) * Sl2 + pp] : make_double2(0.0, 0.0);
   for (int i = i0; i < i1; ++i) {
-    w[NX - 1] = R2[stream_plane(c, i + NX - 1, NX) * Sl2 + pp];
+    w[NX - 1] = pf[0];
+#pragma unroll
+    for (int d = 0; d < PD - 1; ++d) pf[d] = pf[d + 1];
+    if (i + PD < i1) pf[PD - 1] = R2[stream_plane(c, i + PD + NX - 1, NX) * Sl2 + pp];
     double ax = 0.0, ay = 0.0;
 #pragma unroll
     for (int a = 0; a < NX; ++a) {
@@ -1398,10 +1409,18 @@ static hipError_t launch_fx(const double* R, const double* bx, int ns, int64_t S
   if (Sl % 2 == 0 && ((uintptr_t)R & 15) == 0 && ((uintptr_t)T1 & 15) == 0 &&
       std::getenv("PODS_FX_SCALAR") == nullptr) {
     // point pairs: half the threads, so twice the step chunks keep the same parallelism
-    const int chunk2 = std::max(1, (chunk + 1) / 2);
+    // with PD loads in flight per wave, about four resident workgroups per CU suffice: step
+    // chunks so the grid is one round of ~1024 workgroups (a partial second round of a
+    // longer grid left most CUs idle at the end)
+    (void)chunk;
+    const int64_t bx_ = (Sl / 2 + 255) / 256;
+    const char* env = std::getenv("PODS_FX_WG");
+    const int64_t want = env ? std::max(1, std::atoi(env)) : 1024;
+    const int64_t nch0 = std::max<int64_t>(1, std::min<int64_t>(ns, want / std::max<int64_t>(1, bx_ * ncomp)));
+    const int chunk2 = (int)((ns + nch0 - 1) / nch0);
     const int nch = (ns + chunk2 - 1) / chunk2;
-    dim3 grid((unsigned)((Sl / 2 + 255) / 256), (unsigned)ncomp, (unsigned)nch);
-    hipLaunchKernelGGL(k_filter_x2<NX>, grid, dim3(256), 0, st, R, bx, ns, Sl, chunk2, T1);
+    dim3 grid((unsigned)bx_, (unsigned)ncomp, (unsigned)nch);
+    hipLaunchKernelGGL((k_filter_x2<NX, 8>), grid, dim3(256), 0, st, R, bx, ns, Sl, chunk2, T1);
     return hipGetLastError();
   }
   const int nch = (ns + chunk - 1) / chunk;
