@@ -453,14 +453,25 @@ __global__ __launch_bounds__(NT) void k_filter_yz(
     const double* __restrict__ T1, const double* __restrict__ by, const double* __restrict__ bz,
     int NZr, int ns, int jl, int K, int Kp, int64_t Sl, int ncomp,
     const double* __restrict__ lund, int64_t lund_sj, int lund_mode, const double* __restrict__ rot,
-    int rotate, double* __restrict__ AT, int nsb) {
+    int rotate, double* __restrict__ AT, int nsb, int xcd_remap) {
   extern __shared__ __attribute__((aligned(16))) double t2[];  // TJ x ldt
   constexpr int YR = TJ < 16 ? TJ : 16;  // rows per y-pass item
   constexpr int NZMAX = NZC > 0 ? NZC : 25;
   const int NZ = NZC > 0 ? NZC : NZr;
   constexpr int WIN = 16 + NZMAX - 1;
   const int ldt = kpad(Kp + 16) + 1;
-  const int jt = blockIdx.x * TJ;
+  // XCD-aware block order: blocks are dealt round-robin over the 8 XCDs (b and b+8 share one),
+  // so the row tiles of one step group -- whose y halos are each other's rows -- would land on
+  // 8 different L2s.  Renumber so each XCD walks consecutive (step group, tile) pairs: the
+  // neighbouring tiles of a step group run together on one XCD and the halo rows hit its L2.
+  // Any map is correct (blocks are independent); this one is only for speed.
+  int lin = blockIdx.y * gridDim.x + blockIdx.x;
+  if (xcd_remap) {
+    const int nfull = (int)(gridDim.x * gridDim.y) & ~7;
+    if (lin < nfull) lin = (lin & 7) * (nfull >> 3) + (lin >> 3);
+  }
+  const int tile_x = lin % gridDim.x, group_y = lin / gridDim.x;
+  const int jt = tile_x * TJ;
   const int tid0 = threadIdx.x;
   const int rows = min(TJ, jl - jt);
   const int64_t Pl = (int64_t)jl * K;
@@ -484,7 +495,7 @@ __global__ __launch_bounds__(NT) void k_filter_yz(
   }
   // NSB consecutive steps per block: each thread's stores for one snapshot-row group then
   // land on consecutive 128-B lines of the K-tiled layout (steps are contiguous there)
-  const int ib = blockIdx.y * nsb;
+  const int ib = group_y * nsb;
   const int ie = min(ns, ib + nsb);
 #pragma clang loop unroll(disable)
   for (int i = ib; i < ie; ++i) {
@@ -1477,8 +1488,9 @@ static hipError_t launch_fyz_t(const double* T1, const double* by, const double*
   const int tiles = (jl + TJ - 1) / TJ;
   const int nsb = (int)std::max<int64_t>(1, std::min<int64_t>(16, (int64_t)tiles * ns / 512));
   const dim3 grid((unsigned)tiles, (unsigned)((ns + nsb - 1) / nsb));
+  const int xcd_remap = std::getenv("PODS_YZ_NOREMAP") == nullptr;
   hipLaunchKernelGGL((k_filter_yz<TJ, NY, NZC, NT>), grid, dim3(NT), lds, st, T1, by, bz, NZ, ns, jl, K,
-                     Kp, Sl, ncomp, lund, lund_sj, lund_mode, rot, rotate, AT, nsb);
+                     Kp, Sl, ncomp, lund, lund_sj, lund_mode, rot, rotate, AT, nsb, xcd_remap);
   return hipGetLastError();
 }
 
