@@ -175,6 +175,81 @@ __global__ __launch_bounds__(256) void k_mt_jump(const uint32_t* __restrict__ sr
   for (int i = threadIdx.x; i < MTN; i += 256) d[i] = acc[i];
 }
 
+// The same jump with the coefficients taken three at a time (a sliding-window table): for
+// each 3-bit pattern p, Y_p[k] = XOR_{i in p} x[k + i] is built once per job, so the three
+// windows of coefficients r, r+1, r+2 cost ONE LDS read (Y_p[r + w]) instead of one per set
+// bit (1.5 on average).  Pattern 0 is a row of zeros, so every group reads unconditionally
+// and the 24 reads of an 8-group chunk are independent.  XOR is exact and order-free: the
+// result is bit-identical to k_mt_jump.  LDS 47 KB: three workgroups per CU.
+__global__ __launch_bounds__(256) void k_mt_jump3(const uint32_t* __restrict__ src_base,
+                                                  const int* __restrict__ src_idx,
+                                                  const uint32_t* __restrict__ polys,
+                                                  const int* __restrict__ poly_idx,
+                                                  uint32_t* __restrict__ dst_base,
+                                                  const int* __restrict__ dst_idx, int njobs) {
+  constexpr int YS = 2 * MTN;  // row stride of the pattern table (indices r + w <= 1246)
+  __shared__ uint32_t x[2 * MTN];
+  __shared__ uint32_t Y[8 * YS];
+  __shared__ uint32_t acc[MTN];
+  __shared__ uint32_t g[MTN];
+  const int job = blockIdx.x;
+  if (job >= njobs) return;
+  const uint32_t* s = src_base + (size_t)src_idx[job] * MTN;
+  const uint32_t* gsrc = polys + (size_t)poly_idx[job] * MTN;
+  for (int i = threadIdx.x; i < MTN; i += 256) {
+    const uint32_t v = s[i];
+    x[i] = v;
+    x[MTN + i] = v;
+    acc[i] = 0u;
+    g[i] = gsrc[i];
+  }
+  __syncthreads();
+  twist_block256(x + MTN);
+  // Y_p[k] for k < 2N (entries past x's end read as zero; they are never used)
+  for (int k = threadIdx.x; k < YS; k += 256) {
+    const uint32_t a = x[k];
+    const uint32_t b = k + 1 < YS ? x[k + 1] : 0u;
+    const uint32_t c = k + 2 < YS ? x[k + 2] : 0u;
+    Y[0 * YS + k] = 0u;
+    Y[1 * YS + k] = a;
+    Y[2 * YS + k] = b;
+    Y[3 * YS + k] = a ^ b;
+    Y[4 * YS + k] = c;
+    Y[5 * YS + k] = a ^ c;
+    Y[6 * YS + k] = b ^ c;
+    Y[7 * YS + k] = a ^ b ^ c;
+  }
+  __syncthreads();
+  const int w0 = threadIdx.x, w1 = threadIdx.x + 256, w2 = threadIdx.x + 512;
+  const bool has2 = w2 < MTN;
+  const int w2c = has2 ? w2 : w0;  // a valid address for the lanes past the state
+  for (int q = 31; q >= 0; --q) {
+    if (q != 31) twist_block256(acc);
+    uint32_t v0 = 0, v1 = 0, v2 = 0;
+    // 26 chunks of 24 coefficients (8 groups of 3) cover r in [0, 624)
+    for (int rb = 0; rb < MTN; rb += 24) {
+      const int off = q * MTN + rb;
+      const int wi = off >> 5, sh = off & 31;
+      uint32_t bits = g[wi] >> sh;
+      if (sh && wi + 1 < MTN) bits |= g[wi + 1] << (32 - sh);
+      bits = __builtin_amdgcn_readfirstlane(bits);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const uint32_t* Yp = Y + ((bits >> (3 * u)) & 7u) * YS + rb + 3 * u;
+        v0 ^= Yp[w0];
+        v1 ^= Yp[w1];
+        v2 ^= Yp[w2c];
+      }
+    }
+    acc[w0] ^= v0;
+    acc[w1] ^= v1;
+    if (has2) acc[w2] ^= v2;
+    __syncthreads();
+  }
+  uint32_t* d = dst_base + (size_t)dst_idx[job] * MTN;
+  for (int i = threadIdx.x; i < MTN; i += 256) d[i] = acc[i];
+}
+
 // Substream generator: one wavefront per substream g, Bs blocks of 624 words from state
 // mt^(g*Bs).  Double D of the stream (2 words) -> uniform(low, low+range), written to the
 // slab buffer when its padded row lies in [rlo, rhi) of its plane.
@@ -1390,8 +1465,12 @@ hipError_t launch_mt_jump(const uint32_t* src, const int* src_idx, const uint32_
                           const int* poly_idx, uint32_t* dst, const int* dst_idx, int njobs,
                           hipStream_t st) {
   if (njobs <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_mt_jump, dim3(njobs), dim3(256), 0, st, src, src_idx, polys, poly_idx, dst,
-                     dst_idx, njobs);
+  if (std::getenv("PODS_MT_JUMP_BITS") == nullptr)  // default: the 3-bit window table
+    hipLaunchKernelGGL(k_mt_jump3, dim3(njobs), dim3(256), 0, st, src, src_idx, polys, poly_idx, dst,
+                       dst_idx, njobs);
+  else
+    hipLaunchKernelGGL(k_mt_jump, dim3(njobs), dim3(256), 0, st, src, src_idx, polys, poly_idx, dst,
+                       dst_idx, njobs);
   return hipGetLastError();
 }
 
