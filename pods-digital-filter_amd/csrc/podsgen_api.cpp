@@ -140,7 +140,11 @@ RngLayout make_layout(int64_t ntot) {
   RngLayout L;
   L.ntot = ntot;
   const int64_t blocks = (ntot + 311) / 312;
-  int64_t want = (blocks + 2047) / 2048;
+  // about 2048 substreams (PODS_MT_SUBSTREAMS overrides the target): more substreams shorten
+  // the generator's per-substream twist chains but add jump-ahead jobs
+  const char* env = std::getenv("PODS_MT_SUBSTREAMS");
+  const int64_t target = env ? std::max(64, std::atoi(env)) : 2048;
+  int64_t want = (blocks + target - 1) / target;
   int64_t Bs = 1024;
   while (Bs < want) Bs *= 2;
   L.Bs = Bs;
