@@ -79,7 +79,14 @@ def ctx():
     c.close()
 
 
-def test_rng_stream_bit_exact(ctx):
+@pytest.mark.parametrize("jump", ["window3", "per_bit"])
+def test_rng_stream_bit_exact(ctx, monkeypatch, jump):
+    """numpy's legacy MT19937 stream bit for bit, through both jump-ahead kernels
+    (k_mt_jump3, the default, and k_mt_jump behind PODS_MT_JUMP_BITS; read at launch)."""
+    if jump == "per_bit":
+        monkeypatch.setenv("PODS_MT_JUMP_BITS", "1")
+    else:
+        monkeypatch.delenv("PODS_MT_JUMP_BITS", raising=False)
     lib = ctx.lib
     for seed, n in [(12345, 1000), (7, 3_000_001), (2**32 - 1, 25_000_000)]:
         out = torch.empty(n, dtype=torch.float64, device="cuda")
@@ -300,6 +307,17 @@ def test_generate_fused_xyz_opt_in(ctx, monkeypatch, kw):
     planes in HBM) is bit-exact against the oracle: full tiles, ragged edge tiles (40 x 27) with
     a rotated normal, and the 256^2 inlet."""
     monkeypatch.setenv("PODS_GEN_FUSED", "1")
+    A = E.Generator(podsgen.DFSetup(**kw), ctx=ctx).generate().to_host()
+    assert np.array_equal(A, O.generate(O.DFConfig(**kw)))
+
+
+@pytest.mark.parametrize("kw", [dict(jma=40, kma=27, ns=30, seed=5, normal=(1.0, -0.4, 0.2)),
+                                dict(jma=256, kma=256, ns=40, seed=4242)])
+def test_generate_yz_xcd_order_opt_in(ctx, monkeypatch, kw):
+    """The opt-in XCD-aware block order of the y/z pass (PODS_YZ_REMAP=1) only renumbers
+    independent blocks: generation stays bit-exact against the oracle (ragged tiles and a grid
+    whose block count is not a multiple of 8, and the 256^2 inlet)."""
+    monkeypatch.setenv("PODS_YZ_REMAP", "1")
     A = E.Generator(podsgen.DFSetup(**kw), ctx=ctx).generate().to_host()
     assert np.array_equal(A, O.generate(O.DFConfig(**kw)))
 
