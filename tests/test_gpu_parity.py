@@ -79,14 +79,17 @@ def ctx():
     c.close()
 
 
-@pytest.mark.parametrize("jump", ["window3", "per_bit"])
+@pytest.mark.parametrize("jump", ["window3", "per_bit", "window3_long_substreams"])
 def test_rng_stream_bit_exact(ctx, monkeypatch, jump):
     """numpy's legacy MT19937 stream bit for bit, through both jump-ahead kernels
-    (k_mt_jump3, the default, and k_mt_jump behind PODS_MT_JUMP_BITS; read at launch)."""
+    (k_mt_jump3, the default, and k_mt_jump behind PODS_MT_JUMP_BITS; read at launch), and
+    with a different substream layout (PODS_MT_SUBSTREAMS=64: twice the blocks per substream)."""
+    monkeypatch.delenv("PODS_MT_JUMP_BITS", raising=False)
+    monkeypatch.delenv("PODS_MT_SUBSTREAMS", raising=False)
     if jump == "per_bit":
         monkeypatch.setenv("PODS_MT_JUMP_BITS", "1")
-    else:
-        monkeypatch.delenv("PODS_MT_JUMP_BITS", raising=False)
+    elif jump == "window3_long_substreams":
+        monkeypatch.setenv("PODS_MT_SUBSTREAMS", "64")
     lib = ctx.lib
     for seed, n in [(12345, 1000), (7, 3_000_001), (2**32 - 1, 25_000_000)]:
         out = torch.empty(n, dtype=torch.float64, device="cuda")
