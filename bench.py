@@ -91,15 +91,38 @@ def parse():
     ap.add_argument("--seed", type=int, default=12345)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU sampling")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo for "
+                         "CPU-transport tests of the multi-rank path, e.g. 2 ranks on one GPU)")
     return ap.parse_args()
 
 
+def spawn_ranks(args):
+    """`bench.py --gpus N` without a launcher: start N ranks as children through
+    torch.distributed.run (before anything here touches the GPU; no exec) and return their
+    exit status.  Under torch.distributed.run (WORLD_SIZE set) this is not called."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def cpu_baseline(J, K, ns, nm=20, budget=20.0):
-    """Time the oracle (test infrastructure, CPU) on a bounded sample and extrapolate."""
+    """Time the oracle (test infrastructure, CPU) on the host cores, as BASELINE.md plans it:
+    the generation loop on its first 64 steps (x ns/64: per-step cost is constant), the PODFS
+    stages in full -- mean + centring of the whole (3P, ns) A, np.dot(A.T, A) on it,
+    np.linalg.eig (dgeev, PODFS.py:1309) of the resulting ns x ns C, the spatial modes and the
+    direct DFT of all nm modes -- and the plot-only reconstruction loop on a sample (x its
+    iteration count).  `budget` only bounds the generation sample at large sizes."""
     from oracle import pods_oracle as O  # only the cpu_baseline leg imports the oracle
-    # threads actually used: the reference's Python loops (generation, reconstruction: ~95 % of
-    # the extrapolated time) run on ONE core; numpy's BLAS (SYRK, dgeev) uses its pool
-    blas_threads = 1
+    cores = len(os.sched_getaffinity(0))
+    blas_threads = None
     try:
         from threadpoolctl import threadpool_info
         blas_threads = max([1] + [int(i.get("num_threads", 1)) for i in threadpool_info()
@@ -107,51 +130,47 @@ def cpu_baseline(J, K, ns, nm=20, budget=20.0):
     except Exception:
         pass
     t_all = time.perf_counter()
-    est = {}
+    est, how = {}, {}
     # generation: reference-faithful loop (scipy convolve x3, adapt1d loop, rotate loop)
     cfg = O.DFConfig(jma=J, kma=K, ns=ns, seed=1)
-    m = 2
+    m = min(64, ns)
+    t = time.perf_counter()
+    O.generate(cfg, loops=True, steps=2)
+    per = (time.perf_counter() - t) / 2
+    if per * m > 4 * budget:  # only at sizes beyond C3
+        m = max(2, int(4 * budget / per))
     t = time.perf_counter()
     O.generate(cfg, loops=True, steps=m)
-    per = (time.perf_counter() - t) / m
-    m2 = max(2, min(64, int(0.6 * budget / max(per, 1e-6))))
-    t = time.perf_counter()
-    O.generate(cfg, loops=True, steps=m2)
-    per = (time.perf_counter() - t) / m2
-    est["generate"] = per * ns
-    # mean + correlation + spatial modes on a snapshot sample of ns_s columns
+    est["generate"] = (time.perf_counter() - t) / m * ns
+    how["generate"] = "first %d of %d steps, x ns/%d" % (m, ns, m)
+    # the PODFS stages in full on a (3P, ns) matrix of the workload's shape
     P3 = 3 * J * K
-    ns_s = min(ns, 512)
     rng = np.random.default_rng(0)
-    A = rng.standard_normal((P3, ns_s))
+    A = rng.random((P3, ns))
     t = time.perf_counter()
     mean = np.mean(A, 1)
-    Ac = A - mean[:, None]
-    t_mean = time.perf_counter() - t
+    A -= mean[:, None]
+    est["mean"] = time.perf_counter() - t
     t = time.perf_counter()
-    C = np.dot(Ac.T, Ac) / ns_s
-    t_c = time.perf_counter() - t
-    est["mean"] = t_mean * ns / ns_s
-    est["corr"] = t_c * (ns / ns_s) ** 2
-    # eigensolve (dgeev as PODFS.py:1309) at n_e, O(n^3)
-    n_e = min(ns, 1024)
-    Ce = C[:n_e, :n_e] if n_e <= ns_s else np.cov(rng.standard_normal((n_e, 2 * n_e)))
+    C = np.dot(A.T, A) / ns
+    est["corr"] = time.perf_counter() - t
     t = time.perf_counter()
-    np.linalg.eig(Ce)
-    est["eig"] = (time.perf_counter() - t) * (ns / n_e) ** 3
-    T = rng.standard_normal((ns_s, nm))
+    lam, V = np.linalg.eig(C)
+    est["eig"] = time.perf_counter() - t
+    order = np.argsort(-lam.real)
+    T = V[:, order[:nm]].real
     t = time.perf_counter()
-    np.dot(np.dot(Ac, T), np.eye(nm)) / ns_s
-    est["spatial"] = (time.perf_counter() - t) * ns / ns_s
-    # Fourier DFT (PODFS.py:1562-1571) and the y2 reconstruction loop (:1603-1612)
+    np.dot(np.dot(A, T), np.diag(np.ones(nm) / lam[order[:nm]].real)) / ns
+    est["spatial"] = time.perf_counter() - t
+    del A
     time_, period = O.time_axis(ns, 0.1)
-    y = rng.standard_normal(ns)
-    nk = 16
     t = time.perf_counter()
-    for n in range(nk):
-        k = n - ns // 2
-        (y * np.exp(-1j * 2 * k * np.pi * time_ / period)).sum() / ns
-    est["dft"] = (time.perf_counter() - t) / nk * ns * nm
+    for i in range(nm):
+        O.dft_reference(T[:, i], time_, period)
+    est["dft"] = time.perf_counter() - t
+    for k in ("mean", "corr", "eig", "spatial", "dft"):
+        how[k] = "full"
+    # the y2 reconstruction loop (PODFS.py:1603-1612), c_count ~ 0.3 ns
     c = np.zeros(ns, dtype=np.complex64)
     reps = 2000
     t = time.perf_counter()
@@ -159,20 +178,20 @@ def cpu_baseline(J, K, ns, nm=20, budget=20.0):
     for n in range(reps):
         f += c[n % ns] * np.exp(1j * 2 * 3 * np.pi * 0.5 / period)
     per_it = (time.perf_counter() - t) / reps
-    est["reconstruct"] = per_it * ns * (0.3 * ns) * nm  # c_count ~ 0.3 ns
+    est["reconstruct"] = per_it * ns * (0.3 * ns) * nm
+    how["reconstruct"] = "%d iterations, x ns * 0.3 ns * nm" % reps
     total = sum(est.values())
-    sample = ("oracle (numpy %s / scipy, reference-faithful Python loops) on host: %d of %d generation "
-              "steps at %dx%d, mean/SYRK/Phi on %d of %d snapshots (x ns, x ns^2), dgeev at n=%d (x n^3), "
-              "DFT %d of %d frequencies, reconstruction loop %d iterations; extrapolated to the full job; "
-              "sampled in %.1f s" % (np.__version__, m2, ns, J, K, ns_s, ns, n_e, nk, ns, reps,
-                                     time.perf_counter() - t_all))
-    blas_s = est["corr"] + est["eig"] + est["spatial"]
-    return {"value": J * K * ns / total / 1e6, "unit": "Mpoints/s", "cores": 1, "kind": "port",
+    sample = ("oracle (numpy %s / scipy, reference-faithful Python loops) on %d host cores: generation %s; "
+              "mean, SYRK np.dot(A.T, A) (%dx%d), dgeev n=%d, spatial modes, DFT of %d modes in full; "
+              "reconstruction loop %s; measured in %.1f s"
+              % (np.__version__, cores, how["generate"], P3, ns, ns, nm, how["reconstruct"],
+                 time.perf_counter() - t_all))
+    return {"value": J * K * ns / total / 1e6, "unit": "Mpoints/s", "cores": cores, "kind": "port",
             "blas_threads": blas_threads,
-            "threads_note": "Python loops on 1 core (%.0f of %.0f s); SYRK/dgeev/Phi on %d BLAS threads (%.0f s)"
-                            % (total - blas_s, total, blas_threads, blas_s),
-            "sample": sample, "extrapolated_seconds": round(total, 2),
-            "stages_s": {k: round(v, 3) for k, v in est.items()}}
+            "threads_note": "Python loops (generation, reconstruction) run on one core; numpy BLAS/LAPACK "
+                            "(SYRK, dgeev, spatial) on its thread pool",
+            "sample": sample, "seconds_full_job": round(total, 2),
+            "stages_s": {k: round(v, 3) for k, v in est.items()}, "stage_basis": how}
 
 
 def load_traffic(config, ns, rank):
@@ -188,8 +207,17 @@ def load_traffic(config, ns, rank):
         return None
 
 
+def metric_name(config):
+    J, K, ns, _ = CONFIGS[config]
+    if config == "c3":  # BASELINE.json's headline metric
+        return "filtered-snapshot Mpoints/s (gen+PODFS), 256^2 inlet x 4096 steps, 1/2/4/8 GPU"
+    return "filtered-snapshot Mpoints/s (gen+PODFS), %dx%d inlet x %d steps (%s)" % (J, K, ns, config)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     import torch
     import torch.distributed as dist
     import podsgen
@@ -200,17 +228,25 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
-    torch.cuda.set_device(local)
+    # gloo: the multi-rank path on however many GPUs there are (ranks may share one)
+    ndev = max(torch.cuda.device_count(), 1)
+    device = local % ndev if args.backend == "gloo" else local
+    torch.cuda.set_device(device)
+    observed_world = 1
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
+        observed_world = dist.get_world_size()
     J, K, ns, desc = CONFIGS[args.config]
     setup = make_setup(podsgen, args.config, args.seed)
-    gen = E.Generator(setup, device=local, rank=rank, world=world)
+    gen = E.Generator(setup, device=device, rank=rank, world=world)
     d = dist if world > 1 else None
 
     def step(timer=None):
-        return E.pipeline(setup, device=local, dist=d, gen=gen, timer=timer)
+        return E.pipeline(setup, device=device, dist=d, gen=gen, timer=timer)
 
     for _ in range(args.warmup):
         step()
@@ -249,7 +285,7 @@ def main():
         dist.barrier()
     if rank == 0:
         out = {
-            "metric": "filtered-snapshot Mpoints/s (gen+PODFS), 256^2 inlet x 4096 steps, 1/2/4/8 GPU",
+            "metric": metric_name(args.config),
             "value": round(value, 3),
             "unit": "Mpoints/s",
             "n_gpus": world,
@@ -264,7 +300,8 @@ def main():
                      "anisotropic x filter)" if args.config in ("c5", "c5s") else
                      "synthetic (seeded MT19937 random field, built tanh/top-hat profile)"),
             "config": {"workload": desc, "jma": J, "kma": K, "ns": ns, "nm": setup.nm,
-                       "nf": [setup.nfx, setup.nfy, setup.nfz], "parallelism": "row-slab dp%d" % world},
+                       "nf": [setup.nfx, setup.nfy, setup.nfz], "parallelism": "row-slab dp%d" % world,
+                       "backend": args.backend if world > 1 else None, "dist_world_size": observed_world},
             "roofline": {"kernel": "pods_corr (k_syrk_g128 + k_syrk_reduce), rank 0",
                          "bound": "mfma", "achieved": round(achieved, 3),
                          "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",

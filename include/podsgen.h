@@ -120,6 +120,13 @@ int pods_set_mean(pods_ctx* ctx, const double* mean_host);
 int pods_corr(pods_ctx* ctx, double* C_dev, int divide);
 /* x[i] = x[i] / divisor for n doubles on the device. */
 int pods_divide_inplace(pods_ctx* ctx, double* x_dev, int64_t n, double divisor);
+/* The multi-device all-reduce of the partial correlations (PODFS.py:1455 summed over row slabs)
+ * moves only the lower triangle: pods_pack_lower copies it from C_dev (n x n row-major) into
+ * packed_dev (n(n+1)/2 doubles, row r at r(r+1)/2); after the all-reduce pods_unpack_lower
+ * writes packed / divisor (IEEE division, numpy's `/ ns`) to both triangles of C_dev, so C is
+ * exactly symmetric.  Device pointers, stream-ordered. */
+int pods_pack_lower(pods_ctx* ctx, const double* C_dev, int n, double* packed_dev);
+int pods_unpack_lower(pods_ctx* ctx, const double* packed_dev, int n, double divisor, double* C_dev);
 
 /* Temporal modes after sort_eigenvalues + scaling (PODFS.py:1310, :1323-1325).
  * V_dev: eigenvectors from a symmetric solver in ASCENDING eigenvalue order, element
@@ -169,11 +176,18 @@ int pods_syev2_inspect(pods_ctx* ctx, int n, int nvec, int what, double* out_hos
 int pods_spatial_modes(pods_ctx* ctx, const double* T_dev, int ldT, const double* lambda_host,
                        int nm, double* phi_dev);
 
-/* Shifted direct DFT of the temporal modes (PODFS.py:1562-1571):
- * c[n][i] = sum_m T[m][i] exp(-1j 2 k pi t_m / period) / ns,  k = n - ns//2,
- * complex64 interleaved (re, im), row-major ns x nm.  t_host: ns sample times.
- * Asynchronous: enqueued on the bound stream and returns (the summation program and t are
- * kept on the device and re-uploaded only when ns or t change). */
+/* Twiddle table of the DFT below, made on the host by the reference expression itself
+ * (podsgen.host.dft_twiddles: np.exp(-1j*2*k*np.pi*time/period), PODFS.py:1566) so that the
+ * device never evaluates sin/cos: w_host holds R x ns (cos, sin) pairs, row q = k for
+ * q < nk (nk = ns/2 for even ns, ns/2 + 1 for odd), and for even ns a last row for
+ * k = -ns/2; R = nk + (ns even).  Kept on the device for (ns, t_host, period) (synchronous). */
+int pods_fourier_twiddles(pods_ctx* ctx, int ns, const double* t_host, double period, const double* w_host);
+/* Shifted direct DFT of the temporal modes (PODFS.py:1562-1571), bit-exact:
+ * c[n][i] = sum_m T[m][i] exp(-1j 2 k pi t_m / period) / ns,  k = n - ns//2, in numpy's
+ * pairwise complex summation order, complex64 interleaved (re, im), row-major ns x nm.
+ * t_host / period must be the ones of the last pods_fourier_twiddles (else PODS_ERR_STATE).
+ * Asynchronous: enqueued on the bound stream and returns (the summation program is kept on
+ * the device and re-uploaded only when ns changes). */
 int pods_fourier(pods_ctx* ctx, const double* T_dev, int ldT, int nm, int ns,
                  const double* t_host, double period, float* c_dev);
 
@@ -211,6 +225,11 @@ int pods_rng_uniform(pods_ctx* ctx, uint32_t seed, int64_t n, double low, double
 int pods_host_mt_jump_check(uint32_t seed, int64_t nblocks);
 /* Characteristic polynomial degree found by Berlekamp-Massey (expect 19937). */
 int pods_host_mt_charpoly_degree(void);
+/* The co-residency rule applied before every persistent (spin-waiting) launch -- k_trd,
+ * k_bt_fused, k_pqr, k_sbtrd_win: PODS_OK when grid <= blocks_per_cu x cus (both from the
+ * occupancy API at launch time), else PODS_ERR_UNSUPPORTED, which the solvers then return
+ * instead of launching a grid whose hand-offs could never complete. */
+int pods_host_persistent_grid_fits(int blocks_per_cu, int cus, int64_t grid);
 
 #ifdef __cplusplus
 }

@@ -12,6 +12,7 @@
 #include "mt_host.h"
 #include "podsgen.h"
 #include "podsgen_kernels.h"
+#include "podsgen_ext.h"
 
 namespace {
 
@@ -22,9 +23,14 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+// hipErrorCooperativeLaunchTooLarge comes from pods::check_persistent: a spin-waiting grid
+// that the device cannot hold resident at once is refused before launch, not left to time out
 #define PODS_HIP(expr)                                                                  \
   do {                                                                                  \
     hipError_t _e = (expr);                                                             \
+    if (_e == hipErrorCooperativeLaunchTooLarge)                                        \
+      return fail(PODS_ERR_UNSUPPORTED, std::string(#expr) +                           \
+                                            ": persistent grid cannot be co-resident on this device"); \
     if (_e != hipSuccess)                                                               \
       return fail(PODS_ERR_HIP, std::string(#expr) + " failed: " + hipGetErrorString(_e)); \
   } while (0)
@@ -226,7 +232,7 @@ struct pods_ctx {
   int64_t S = 0, Sl = 0, Pl = 0, rowlen = 0, rowpad = 0;  // rowpad: rowlen rounded up to 16
   RngLayout layout;
   RngBuffers rng;
-  DevBuf R, T1, A, mean, lund, taps, rot, prog_mean, prog_dft, tbuf, mag, lam, cwork, items, spwork, prog_rank;
+  DevBuf R, T1, A, mean, lund, taps, rot, prog_mean, prog_dft, mag, lam, cwork, items, spwork, prog_rank;
   DevBuf e_wm, e_x, e_flags, e_det, e_v, e_t, e_part, e_w2, e_inv, e_cnt;  // pods_syev workspace
   int e_G = 0;
   DevBuf e2_ws, e2_flags, e2_ipiv;  // pods_syev2 (two-stage) workspace
@@ -243,8 +249,13 @@ struct pods_ctx {
   DevBuf zero;                  // rowpad zeros: the mean operand once A is centred
   std::vector<double> stage;  // host staging for small uploads
   // device-resident DFT / ranking programs and time axis, re-uploaded only on change
-  int dft_ns = -1, dft_nprog = 0, rank_ns = -1, rank_nprog = 0;
+  int dft_ns = -1, dft_nprog = 0, dft_nleaf = 0, rank_ns = -1, rank_nprog = 0;
   std::vector<double> dft_t;
+  // host twiddle table of the DFT (pods_fourier_twiddles) and the time axis it was made for
+  DevBuf dft_w;
+  int dft_w_ns = -1;
+  double dft_w_period = 0.0;
+  std::vector<double> dft_w_t;
 };
 
 namespace {
@@ -336,10 +347,10 @@ int pods_destroy(pods_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->R, &c->T1, &c->A, &c->mean, &c->lund, &c->taps, &c->rot, &c->prog_mean,
-                    &c->prog_dft, &c->tbuf, &c->mag, &c->lam, &c->cwork, &c->items, &c->e_wm,
+                    &c->prog_dft, &c->mag, &c->lam, &c->cwork, &c->items, &c->e_wm,
                     &c->e_x, &c->e_flags, &c->e_det, &c->e_v, &c->e_t, &c->e_part, &c->e_w2,
                     &c->e_inv, &c->e_cnt, &c->spwork, &c->prog_rank, &c->zero, &c->e2_ws, &c->e2_flags,
-                    &c->e2_ipiv})
+                    &c->e2_ipiv, &c->dft_w})
     release(*b);
   c->rng.free_all();
   delete c;
@@ -659,6 +670,20 @@ int pods_divide_inplace(pods_ctx* c, double* x, int64_t n, double d) {
   return PODS_OK;
 }
 
+int pods_pack_lower(pods_ctx* c, const double* C, int n, double* packed) {
+  if (int e = check_ctx(c)) return e;
+  if (!C || !packed || n < 1) return fail(PODS_ERR_ARG, "pods_pack_lower: bad arguments");
+  PODS_HIP(pods::launch_pack_lower(C, n, n, packed, c->stream));
+  return PODS_OK;
+}
+
+int pods_unpack_lower(pods_ctx* c, const double* packed, int n, double divisor, double* C) {
+  if (int e = check_ctx(c)) return e;
+  if (!C || !packed || n < 1) return fail(PODS_ERR_ARG, "pods_unpack_lower: bad arguments");
+  PODS_HIP(pods::launch_unpack_lower(packed, n, divisor, C, n, c->stream));
+  return PODS_OK;
+}
+
 int pods_temporal_modes(pods_ctx* c, const double* V, int64_t v_rs, int64_t v_cs,
                         const double* lam_desc, int nvalid, int ncols, double* T) {
   PODS_TRY
@@ -895,32 +920,55 @@ int pods_syev_status(pods_ctx* c) {
   PODS_CATCH
 }
 
+int pods_fourier_twiddles(pods_ctx* c, int ns, const double* t_host, double period, const double* w_host) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (ns <= 0 || !t_host || !w_host) return fail(PODS_ERR_ARG, "pods_fourier_twiddles: bad arguments");
+  PODS_HIP(hipSetDevice(c->device));
+  const size_t bytes = (size_t)pods::dft_table_rows(ns) * ns * 2 * sizeof(double);
+  PODS_HIP(hipDeviceSynchronize());  // a DFT in flight (any stream) may read the old table
+  PODS_HIP(ensure(c->dft_w, bytes));
+  PODS_HIP(hipMemcpy(c->dft_w.p, w_host, bytes, hipMemcpyHostToDevice));
+  c->dft_w_ns = ns;
+  c->dft_w_period = period;
+  c->dft_w_t.assign(t_host, t_host + ns);
+  return PODS_OK;
+  PODS_CATCH
+}
+
 int pods_fourier(pods_ctx* c, const double* T, int ldT, int nm, int ns, const double* t_host,
                  double period, float* c_dev) {
   PODS_TRY
   if (int e = check_ctx(c)) return e;
   if (!T || !t_host || !c_dev || nm <= 0 || ns <= 0 || ldT < nm) return fail(PODS_ERR_ARG, "bad arguments");
+  if (c->dft_w_ns != ns || c->dft_w_period != period ||
+      std::memcmp(c->dft_w_t.data(), t_host, (size_t)ns * sizeof(double)) != 0)
+    return fail(PODS_ERR_STATE, "pods_fourier: no twiddle table for this time axis (pods_fourier_twiddles)");
   PODS_HIP(hipSetDevice(c->device));
-  // The summation program (depends on ns) and the time axis are uploaded only when they
-  // change (blocking copies, once per configuration), so the DFT itself is enqueued
-  // asynchronously on the bound stream and can overlap the caller's next work.
+  // The summation program (depends on ns) is uploaded only when ns changes (blocking copy,
+  // once per configuration), so the DFT itself is enqueued asynchronously on the bound stream
+  // and can overlap the caller's next work.  Buffer prog_dft: the program, then its leaves.
   if (c->dft_ns != ns) {
     std::vector<int> prog = cpairwise_program(ns);
-    PODS_HIP(hipDeviceSynchronize());  // a DFT still in flight (any stream) may read them
-    PODS_HIP(ensure(c->prog_dft, prog.size() * sizeof(int)));
-    PODS_HIP(hipMemcpy(c->prog_dft.p, prog.data(), prog.size() * sizeof(int), hipMemcpyHostToDevice));
-    c->dft_nprog = (int)prog.size() / 2;
-    c->dft_ns = ns;
-    c->dft_t.clear();
-  }
-  if (c->dft_t.size() != (size_t)ns || std::memcmp(c->dft_t.data(), t_host, (size_t)ns * sizeof(double))) {
+    std::vector<int> leaves;
+    for (size_t i = 0; i < prog.size(); i += 2)
+      if (prog[i] >= 0) {
+        leaves.push_back(prog[i]);
+        leaves.push_back(prog[i + 1]);
+      }
+    std::vector<int> buf(prog);
+    buf.insert(buf.end(), leaves.begin(), leaves.end());
     PODS_HIP(hipDeviceSynchronize());
-    PODS_HIP(ensure(c->tbuf, (size_t)ns * sizeof(double)));
-    PODS_HIP(hipMemcpy(c->tbuf.p, t_host, (size_t)ns * sizeof(double), hipMemcpyHostToDevice));
-    c->dft_t.assign(t_host, t_host + ns);
+    PODS_HIP(ensure(c->prog_dft, buf.size() * sizeof(int)));
+    PODS_HIP(hipMemcpy(c->prog_dft.p, buf.data(), buf.size() * sizeof(int), hipMemcpyHostToDevice));
+    c->dft_nprog = (int)prog.size() / 2;
+    c->dft_nleaf = (int)leaves.size() / 2;
+    c->dft_ns = ns;
   }
-  PODS_HIP(pods::launch_dft(T, ldT, nm, ns, c->tbuf.as<double>(), 1.0 / period, 1.0 / (double)ns,
-                            c->prog_dft.as<int>(), c->dft_nprog, reinterpret_cast<float2*>(c_dev), c->stream));
+  const int* prog = c->prog_dft.as<int>();
+  PODS_HIP(pods::launch_dft_tab(T, ldT, nm, ns, c->dft_w.as<double2>(), prog, c->dft_nprog,
+                                prog + 2 * c->dft_nprog, c->dft_nleaf, 1.0 / (double)ns,
+                                reinterpret_cast<float2*>(c_dev), c->stream));
   return PODS_OK;
   PODS_CATCH
 }
@@ -1023,5 +1071,14 @@ int pods_host_mt_jump_check(uint32_t seed, int64_t nblocks) {
 }
 
 int pods_host_mt_charpoly_degree(void) { return pods::mt::charpoly_degree(); }
+
+int pods_host_persistent_grid_fits(int blocks_per_cu, int cus, int64_t grid) {
+  if (blocks_per_cu < 0 || cus < 0 || grid < 0) return fail(PODS_ERR_ARG, "negative argument");
+  if (!pods::persistent_grid_fits(blocks_per_cu, cus, grid))
+    return fail(PODS_ERR_UNSUPPORTED, "grid of " + std::to_string(grid) + " workgroups > " +
+                                          std::to_string(blocks_per_cu) + " per CU x " + std::to_string(cus) +
+                                          " CUs");
+  return PODS_OK;
+}
 
 }  // extern "C"

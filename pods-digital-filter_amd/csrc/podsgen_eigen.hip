@@ -19,6 +19,9 @@
 // FMA is requested explicitly (the file is built with -ffp-contract=off like the others).
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+#include <vector>
+
 #include <algorithm>
 #include <cfloat>
 #include <cstdint>
@@ -170,6 +173,11 @@ __device__ __forceinline__ double tagged(double v, uint32_t tag) {
 __device__ __forceinline__ bool tag_ok(double v, uint32_t tag) {
   return ((uint32_t)__double2loint(v) & 3u) == (tag & 3u);
 }
+// the value a consumer uses: tag bits cleared, so a published 0.0 stays exactly 0.0 (not a
+// denormal) and every workgroup still sees identical bits
+__device__ __forceinline__ double untag(double v) {
+  return __longlong_as_double(__double_as_longlong(v) & ~3ll);
+}
 __device__ __forceinline__ void gst(__amdgpu_buffer_rsrc_t r, int idx, double v, uint32_t tag) {
   const double t = tagged(v, tag);
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0)), t),
@@ -317,12 +325,12 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
           const double q1 = gld(rp, in ? c : j);
           const double q2 = gld(rc, in ? c : j);
           ok = ok && tag_ok(q1, want) && tag_ok(q2, want);
-          p[m] = in ? q1 : 0.0;
-          x[m] = in ? q2 : 0.0;
+          p[m] = in ? untag(q1) : 0.0;
+          x[m] = in ? untag(q2) : 0.0;
         }
         const double qj = gld(rp, j);
         ok = ok && tag_ok(qj, want);
-        pj = qj;
+        pj = untag(qj);
         nspin = spin;
         if (__all(ok)) break;
         if ((spin & 1023) == 1023) {
@@ -557,11 +565,11 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
       for (int spin = 0; (np || nc) && spin <= SPIN_LIMIT; ++spin) {
         if (np) {
           const double q = gld(rp, j);
-          if (tag_ok(q, (uint32_t)j)) { pv = q; np = false; }
+          if (tag_ok(q, (uint32_t)j)) { pv = untag(q); np = false; }
         }
         if (nc) {
           const double q = gld(rc, j);
-          if (tag_ok(q, (uint32_t)j)) { cv = q; nc = false; }
+          if (tag_ok(q, (uint32_t)j)) { cv = untag(q); nc = false; }
         }
       }
       if (np || nc) st_flag(abortw, 1u);
@@ -1282,11 +1290,50 @@ static hipError_t launch_trd_t(const TrdArgs& a, hipStream_t st) {
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_trd<R, S, K, SG, SL>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
+  e = check_persistent(reinterpret_cast<const void*>(&k_trd<R, S, K, SG, SL>), TT, lds, a.G);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_trd<R, S, K, SG, SL>), dim3(a.G), dim3(TT), lds, st, a);
   return hipGetLastError();
 }
 
 }  // namespace eig
+
+bool persistent_grid_fits(int blocks_per_cu, int cus, int64_t grid) {
+  return blocks_per_cu > 0 && cus > 0 && grid <= (int64_t)blocks_per_cu * cus;
+}
+
+hipError_t check_persistent(const void* fn, int block, size_t lds, int64_t grid) {
+  struct Key {
+    const void* fn;
+    int block;
+    size_t lds;
+    int dev;
+    int per, cus;
+  };
+  static std::mutex mu;
+  static std::vector<Key> cache;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  int per = -1, cus = 0;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    for (const Key& k : cache)
+      if (k.fn == fn && k.block == block && k.lds == lds && k.dev == dev) {
+        per = k.per;
+        cus = k.cus;
+      }
+  }
+  if (per < 0) {
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, block, lds);
+    if (e != hipSuccess) return e;
+    e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> g(mu);
+    cache.push_back(Key{fn, block, lds, dev, per, cus});
+  }
+  return persistent_grid_fits(per, cus, grid) ? hipSuccess : hipErrorCooperativeLaunchTooLarge;
+}
 
 // Tridiagonalisation plan: rows per workgroup R (G = ceil(n/R) <= 256 workgroups),
 // S = ceil(n/512) column slots per lane.
@@ -1437,6 +1484,8 @@ hipError_t launch_back_transform(const double* V, int64_t ldv, const double* tau
                  : CR == 32 ? reinterpret_cast<const void*>(&eig::k_bt_fused<32>)
                             : reinterpret_cast<const void*>(&eig::k_bt_fused<64>);
   e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  e = check_persistent(fn, 256, lds, G);
   if (e != hipSuccess) return e;
   if (CR == 16)
     hipLaunchKernelGGL(eig::k_bt_fused<16>, dim3(G), dim3(256), lds, st, V, ldv, (const double*)Tg, n,

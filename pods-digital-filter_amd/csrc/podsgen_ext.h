@@ -1,0 +1,17 @@
+// Launchers added after the first kernel files (kept apart from podsgen_kernels.h so that
+// a change here rebuilds only its users).  All enqueue on `st`.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace pods {
+
+// ---- bit-exact shifted DFT from a host twiddle table (podsgen_dft.hip) ----------------
+// rows of the table W (ns doubles2 each): k = 0..nk-1, plus k = -ns/2 for even ns
+int dft_table_rows(int ns);
+// leaves: nleaf x {start, count} in the order cpairwise_program's leaves appear in prog
+hipError_t launch_dft_tab(const double* T, int ldT, int nm, int ns, const double2* W, const int* prog, int nprog,
+                          const int* leaves, int nleaf, double inv_n, float2* c, hipStream_t st);
+
+}  // namespace pods

@@ -6,6 +6,12 @@
 
 namespace pods {
 
+// Persistent (spin-waiting) grids hand data between workgroups, so every workgroup must be
+// resident at once.  check_persistent asks the occupancy API (cached per kernel and LDS size)
+// and returns hipErrorCooperativeLaunchTooLarge when grid > blocks per CU x CUs, before launch.
+bool persistent_grid_fits(int blocks_per_cu, int cus, int64_t grid);
+hipError_t check_persistent(const void* fn, int block, size_t lds, int64_t grid);
+
 hipError_t launch_mt_jump(const uint32_t* src, const int* src_idx, const uint32_t* polys,
                           const int* poly_idx, uint32_t* dst, const int* dst_idx, int njobs,
                           hipStream_t st);
@@ -38,6 +44,11 @@ hipError_t launch_syrk(int kernel, const double* AT, int64_t ld, int ns, int64_t
 // A <- A - mean in place (K-tiled layout, rowpad rows x ns snapshots)
 hipError_t launch_center(double* AT, int64_t rowpad, int ns, const double* mean, hipStream_t st);
 hipError_t launch_divide(double* x, int64_t n, double d, hipStream_t st);
+// packed lower triangle (row r at r(r+1)/2) of an n x n row-major C (podsgen_pack.hip)
+hipError_t launch_pack_lower(const double* C, int64_t ldc, int n, double* packed, hipStream_t st);
+// C[r][c] = C[c][r] = packed[r(r+1)/2 + c] / divisor
+hipError_t launch_unpack_lower(const double* packed, int n, double divisor, double* C, int64_t ldc,
+                               hipStream_t st);
 hipError_t launch_temporal(const double* V, int64_t v_rs, int64_t v_cs, int ns, int ncols,
                            int nvalid, const double* lam, double* mag, double* T, hipStream_t st);
 size_t spatial_work_bytes(int64_t rowlen, int ns);
@@ -47,8 +58,6 @@ hipError_t launch_spatial(const double* AT, int64_t rowlen, int ns, const double
 int rank_max_ns();
 hipError_t launch_rank(const float* c, int ns, int nm, double et, const int* prog, int nprog,
                        int32_t* c_ind, int64_t* c_count, hipStream_t st);
-hipError_t launch_dft(const double* T, int ldT, int nm, int ns, const double* t, double inv_period,
-                      double inv_n, const int* prog, int nprog, float2* c, hipStream_t st);
 
 // ---- symmetric eigensolver (podsgen_eigen.hip) ----------------------------------------
 struct TrdArgs {

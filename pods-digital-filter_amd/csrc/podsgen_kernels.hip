@@ -6,7 +6,7 @@
 //                     the adapt1d / adapt2prf expressions bit-for-bit
 //   * k_mean          reproduces np.mean's pairwise order bit-for-bit
 //   * k_syrk / k_spatial_modes use fp64 FMA (MFMA) -- tolerance-level parity
-//   * k_dft           replicates numpy's complex expression; sin/cos from OCML
+//   * the DFT (podsgen_dft.hip) uses the host's twiddle table, bit-exact
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1372,93 +1372,6 @@ __global__ __launch_bounds__(256) void k_spatial_reduce(const double* __restrict
 }
 
 // -----------------------------------------------------------------------------------------
-// shifted direct DFT (PODFS.py:1562-1571) with numpy's complex pairwise summation
-// job j < nk: k = j (k >= 0), writes n = h+k and the exact conjugate at n = h-k;
-// job j == nk (even ns): k = -ns/2 (n = 0).
-// -----------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_dft(const double* __restrict__ T, int ldT, int nm, int ns,
-                                             const double* __restrict__ t, double inv_period,
-                                             double inv_n, const int* __restrict__ prog, int nprog,
-                                             int nk, int njobs, float2* __restrict__ cout) {
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int mode = gid % nm;
-  const int job = gid / nm;
-  if (job >= njobs) return;
-  const int h = ns / 2;
-  const int k = (job < nk) ? job : -h;
-  const double zi = (-2.0 * (double)k) * 3.141592653589793;
-  const double* y = T + mode;
-  double sr_stk[24], si_stk[24];
-  int sp = 0;
-  for (int op = 0; op < nprog; ++op) {
-    const int s = prog[2 * op], n = prog[2 * op + 1];
-    if (s < 0) {
-      const double br = sr_stk[--sp], bi = si_stk[sp];
-      sr_stk[sp - 1] = sr_stk[sp - 1] + br;
-      si_stk[sp - 1] = si_stk[sp - 1] + bi;
-      continue;
-    }
-    double rr, ri;
-    if (n < 4) {
-      rr = -0.0;
-      ri = -0.0;
-      for (int m = s; m < s + n; ++m) {
-        double sv, cv;
-        sincos((zi * t[m]) * inv_period, &sv, &cv);
-        const double yv = y[(int64_t)m * ldT];
-        rr = rr + (yv * cv - 0.0 * sv);
-        ri = ri + (yv * sv + 0.0 * cv);
-      }
-    } else {
-      double r[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        double sv, cv;
-        const int m = s + e;
-        sincos((zi * t[m]) * inv_period, &sv, &cv);
-        const double yv = y[(int64_t)m * ldT];
-        r[2 * e] = yv * cv - 0.0 * sv;
-        r[2 * e + 1] = yv * sv + 0.0 * cv;
-      }
-      int i = 4;
-      for (; i < n - (n % 4); i += 4) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          double sv, cv;
-          const int m = s + i + e;
-          sincos((zi * t[m]) * inv_period, &sv, &cv);
-          const double yv = y[(int64_t)m * ldT];
-          r[2 * e] = r[2 * e] + (yv * cv - 0.0 * sv);
-          r[2 * e + 1] = r[2 * e + 1] + (yv * sv + 0.0 * cv);
-        }
-      }
-      rr = (r[0] + r[2]) + (r[4] + r[6]);
-      ri = (r[1] + r[3]) + (r[5] + r[7]);
-      for (; i < n; ++i) {
-        double sv, cv;
-        const int m = s + i;
-        sincos((zi * t[m]) * inv_period, &sv, &cv);
-        const double yv = y[(int64_t)m * ldT];
-        rr = rr + (yv * cv - 0.0 * sv);
-        ri = ri + (yv * sv + 0.0 * cv);
-      }
-    }
-    sr_stk[sp] = rr;
-    si_stk[sp] = ri;
-    ++sp;
-  }
-  const double cr = (0.0 + sr_stk[0]) * inv_n;
-  const double ci = (0.0 + si_stk[0]) * inv_n;
-  const float2 val = make_float2((float)cr, (float)ci);
-  if (job < nk) {
-    cout[(int64_t)(h + k) * nm + mode] = val;
-    if (k > 0 && h - k >= 0) cout[(int64_t)(h - k) * nm + mode] = make_float2(val.x, -val.y);
-  } else {
-    cout[mode] = val;  // n = 0, k = -ns/2
-  }
-}
-
-// -----------------------------------------------------------------------------------------
 // launchers
 // -----------------------------------------------------------------------------------------
 hipError_t launch_mt_jump(const uint32_t* src, const int* src_idx, const uint32_t* polys,
@@ -1792,15 +1705,5 @@ hipError_t launch_spatial(const double* AT, int64_t rowlen, int ns, const double
   return hipSuccess;
 }
 
-hipError_t launch_dft(const double* T, int ldT, int nm, int ns, const double* t, double inv_period,
-                      double inv_n, const int* prog, int nprog, float2* c, hipStream_t st) {
-  const int h = ns / 2;
-  const int nk = (ns % 2 == 0) ? h : h + 1;  // k = 0..nk-1
-  const int njobs = nk + ((ns % 2 == 0) ? 1 : 0);
-  const int64_t total = (int64_t)njobs * nm;
-  hipLaunchKernelGGL(k_dft, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, T, ldT, nm, ns, t,
-                     inv_period, inv_n, prog, nprog, nk, njobs, c);
-  return hipGetLastError();
-}
 
 }  // namespace pods

@@ -81,6 +81,11 @@ __device__ __forceinline__ double tagged(double v, uint32_t tag) {
 __device__ __forceinline__ bool tag_ok(double v, uint32_t tag) {
   return ((uint32_t)__double2loint(v) & 3u) == (tag & 3u);
 }
+// consumers use the value with the tag cleared: a published 0.0 stays 0.0 (tagged, it would be
+// a denormal that passes dlarfg's sigma != 0 test) and every workgroup still sees equal bits
+__device__ __forceinline__ double untag(double v) {
+  return __longlong_as_double(__double_as_longlong(v) & ~3ll);
+}
 
 // ---------------------------------------------------------------------------------------
 // k_pqr<B>: Householder QR of the panel P = A[r0:r0+m, c0:c0+B] (row-major A, ld lda).
@@ -197,12 +202,12 @@ __global__ __launch_bounds__(256, 1) void k_pqr(double* __restrict__ A, int64_t 
         for (int e = t; e < NW * B; e += 256) {
           const double v = bld(rpub, qb + (e / B) * 2 * B + (e % B));
           ok = ok && tag_ok(v, tag);
-          gsum[e] = v;
+          gsum[e] = untag(v);
         }
         if (t < B) {
           const double v = bld(rpub, qb + own * 2 * B + B + t);
           ok = ok && tag_ok(v, tag);
-          rowj[t] = v;
+          rowj[t] = untag(v);
         }
         if (__all(ok)) break;
         if (++spin > SPIN_LIMIT) {
@@ -1537,6 +1542,8 @@ hipError_t launch_syevd2(const double* C, int n, int nvec, double* ws, const Sye
       if (e == hipSuccess) e = hipMemsetAsync(ptrace, 0, (B * 8 + 1) * sizeof(int64_t), st);
       if (e != hipSuccess) return e;
     }
+    e = check_persistent(reinterpret_cast<const void*>(&sb::k_pqr<B>), 256, 0, NW);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(sb::k_pqr<B>, dim3(NW), dim3(256), 0, st, Aw, (int64_t)n, r0, c0, m, RP, NW,
                        ws + p.off_pub, pflags, epoch * 1024u + (uint32_t)pi, 16u * (uint32_t)pi + 1u, abortw, Vx,
                        tau, ws + p.off_zp, T, ptrace);
@@ -1598,6 +1605,8 @@ hipError_t launch_syevd2(const double* C, int n, int nvec, double* ws, const Sye
     if (e != hipSuccess) return e;
   }
   if (n > 2 && (trs || std::getenv("PODS_SBTRD_OLD"))) {  // the per-task chase over L2 (diagnostics)
+    e = check_persistent(reinterpret_cast<const void*>(&sb::k_sbtrd<B>), 64, 0, NG);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(sb::k_sbtrd<B>, dim3(NG), dim3(64), 0, st, band, n, NG, prog, abortw + 1, trace,
                        trs ? std::atoi(trs) : -1);
   } else if (n > 2) {
@@ -1610,6 +1619,8 @@ hipError_t launch_syevd2(const double* C, int n, int nvec, double* ws, const Sye
     const int P = std::max(1, std::min(ngroups, cus));
     e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sb::k_sbtrd_win<B, GW>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)SW::lds_bytes);
+    if (e != hipSuccess) return e;
+    e = check_persistent(reinterpret_cast<const void*>(&sb::k_sbtrd_win<B, GW>), SW::NT, SW::lds_bytes, P);
     if (e != hipSuccess) return e;
     // PODS_SBWIN_TRACE=q0: per-step timestamps of groups q0 .. q0+3 (diagnostics, stderr)
     const char* wts = std::getenv("PODS_SBWIN_TRACE");

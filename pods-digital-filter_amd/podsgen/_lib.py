@@ -51,6 +51,8 @@ SIGNATURES = {
     "pods_lund_apply": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_i64, c_void_p, c_int, c_void_p]),
     "pods_corr": (c_int, [c_void_p, c_void_p, c_int]),
     "pods_divide_inplace": (c_int, [c_void_p, c_void_p, c_i64, c_dbl]),
+    "pods_pack_lower": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
+    "pods_unpack_lower": (c_int, [c_void_p, c_void_p, c_int, c_dbl, c_void_p]),
     "pods_temporal_modes": (c_int, [c_void_p, c_void_p, c_i64, c_i64, c_void_p, c_int, c_int, c_void_p]),
     "pods_syev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "pods_sytrd": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
@@ -60,6 +62,7 @@ SIGNATURES = {
     "pods_syev2_inspect": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_i64]),
     "pods_sytrd_trace": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "pods_spatial_modes": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
+    "pods_fourier_twiddles": (c_int, [c_void_p, c_int, c_void_p, c_dbl, c_void_p]),
     "pods_fourier": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_dbl, c_void_p]),
     "pods_fourier_rank": (c_int, [c_void_p, c_void_p, c_int, c_int, c_dbl, c_void_p, c_void_p]),
     "pods_filter_block": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
@@ -67,6 +70,7 @@ SIGNATURES = {
     "pods_rng_uniform": (c_int, [c_void_p, c_u32, c_i64, c_dbl, c_dbl, c_void_p]),
     "pods_host_mt_jump_check": (c_int, [c_u32, c_i64]),
     "pods_host_mt_charpoly_degree": (c_int, []),
+    "pods_host_persistent_grid_fits": (c_int, [c_int, c_int, c_i64]),
 }
 
 _lib = None

@@ -30,7 +30,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import DFParams, check, ptr
-from .host import DFSetup, num_valid_modes, rank_and_count, row_slab, time_axis  # noqa: F401
+from .host import DFSetup, dft_twiddles, num_valid_modes, rank_and_count, row_slab, time_axis  # noqa: F401
 
 try:
     import torch
@@ -165,33 +165,33 @@ def _dist_info(dist):
     return dist, dist.get_rank(), dist.get_world_size()
 
 
-_TRIL = {}
-
-
-def _tril_index(n, device):
-    """Linear indices of the lower triangle (with the diagonal) of an n x n row-major matrix,
-    and of the mirrored upper-triangle positions, cached per (n, device)."""
-    key = (n, str(device))
-    if key not in _TRIL:
-        r, c = torch.tril_indices(n, n, device=device)
-        _TRIL[key] = (r * n + c, c * n + r)
-    return _TRIL[key]
-
-
-def allreduce_correlation(dist, C, ns, divide):
+def allreduce_correlation(dist, C, ns, pack, unpack):
     """Sum the ranks' partial correlations C_g = A_g^T A_g (row slabs) and divide by ns
     (PODFS.py:1455, np.dot(A.T, A)/ns): ONE all_reduce of the packed lower triangle
-    (ns(ns+1)/2 doubles, half of C) over RCCL/xGMI, then divide(packed, ns) and unpack into
-    both triangles, so C stays exactly symmetric.  divide is the device division
-    (pods_divide_inplace: x / ns, IEEE-rounded like numpy's)."""
-    lo, up = _tril_index(ns, C.device)
-    flat = C.view(-1)
-    packed = flat.index_select(0, lo)
+    (ns(ns+1)/2 doubles, half of C) over RCCL/xGMI.  pack(C) -> packed copies the triangle
+    out; unpack(packed, C) writes packed / ns (IEEE-rounded like numpy's) to both triangles,
+    so C stays exactly symmetric.  On the GPU these are the pods_pack_lower /
+    pods_unpack_lower kernels (no index tensors, one pass each)."""
+    packed = pack(C)
     dist.all_reduce(packed)
-    divide(packed, ns)
-    flat[lo] = packed
-    flat[up] = packed
+    unpack(packed, C)
     return C
+
+
+def device_triangle_ops(ctx):
+    """pack/unpack callables for allreduce_correlation on ctx's device (C-ABI kernels)."""
+    lib = ctx.lib
+
+    def pack(C):
+        n = C.shape[0]
+        packed = torch.empty(n * (n + 1) // 2, dtype=torch.float64, device=C.device)
+        check(lib.pods_pack_lower(ctx.h, ptr(C), n, ptr(packed)), "pods_pack_lower")
+        return packed
+
+    def unpack(packed, C):
+        n = C.shape[0]
+        check(lib.pods_unpack_lower(ctx.h, ptr(packed), n, float(n), ptr(C)), "pods_unpack_lower")
+    return pack, unpack
 
 
 SYEV_MAX_N = 4096   # pods_syev's on-chip limit (trd_plan)
@@ -273,9 +273,7 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
         check(lib.pods_corr(ctx.h, ptr(C), 1 if world == 1 else 0), "pods_corr")
     if world > 1:
         with tm("allreduce"):
-            def divide(x, d):
-                check(lib.pods_divide_inplace(ctx.h, ptr(x), x.numel(), float(d)), "pods_divide_inplace")
-            allreduce_correlation(dist, C, ns, divide)
+            allreduce_correlation(dist, C, ns, *device_triangle_ops(ctx))
     meta = torch.zeros(4, dtype=torch.int64, device=dev)
     lam_desc_t = torch.empty(ns, dtype=torch.float64, device=dev)
     T = None
@@ -352,6 +350,16 @@ def fc_rows(c, c_ind, c_count):
 RANK_MAX_NS = 16384  # pods_fourier_rank's LDS limit
 
 
+def ensure_twiddles(ctx: Context, ns, time_, period):
+    """Upload the DFT's host twiddle table (podsgen.host.dft_twiddles) once per time axis."""
+    key = (int(ns), float(period), time_.tobytes())
+    if getattr(ctx, "_dft_key", None) != key:
+        W = dft_twiddles(ns, time_, period)
+        check(ctx.lib.pods_fourier_twiddles(ctx.h, int(ns), ptr(np.ascontiguousarray(time_)), float(period),
+                                            ptr(W)), "pods_fourier_twiddles")
+        ctx._dft_key = key
+
+
 def run_fourier(ctx: Context, T, nm, ns, dt, et, timer=None):
     """fourier_coefficients (PODFS.py:1523-1659): DFT and ranking/count on the GPU
     (pods_fourier + pods_fourier_rank); FC assembled on the host from the ranked indices."""
@@ -373,6 +381,8 @@ def launch_fourier(ctx: Context, T, nm, ns, dt, et, timer=None, side=False):
         res = FourierResult(np.zeros((ns, 0), np.complex64), np.zeros((0, ns), np.int32),
                             np.zeros(0, np.int64), np.zeros((0, 3)), period, time_)
         return lambda: res
+    time_ = np.ascontiguousarray(time_, dtype=np.float64)
+    ensure_twiddles(ctx, ns, time_, period)
     main = torch.cuda.current_stream(dev)
     stream = main
     if side:

@@ -248,6 +248,40 @@ def time_axis(ns, dt):
     return time, period
 
 
+def dft_rows(ns):
+    """The k of each twiddle-table row (pods_fourier_twiddles): k = 0..nk-1 and, for even ns,
+    k = -ns/2 (the n = 0 coefficient); the negative k of the other n are exact conjugates."""
+    h = ns // 2
+    nk = h if ns % 2 == 0 else h + 1
+    return list(range(nk)) + ([-h] if ns % 2 == 0 else [])
+
+
+def dft_twiddles(ns, time, period, chunk=128):
+    """np.exp(-1j*2*k*np.pi*time/period) for every table row k -- the reference's own
+    expression (PODFS.py:1566, with k = n - num_fcs/2), evaluated by numpy on the host so the
+    GPU DFT multiplies by exactly the numbers the reference does.  Rows are evaluated in
+    chunks as (coef[:, None] * time) / period: the same complex128 ufunc loops, element for
+    element, as the per-k expression (tests/test_host_cpu.py pins the bits).
+    Returns an (R, ns, 2) float64 array of (cos, sin)."""
+    ks = dft_rows(ns)
+    time = np.asarray(time, dtype=np.float64)
+    W = np.empty((len(ks), ns, 2), dtype=np.float64)
+
+    def rows(r0):
+        coef = np.array([-1j * 2 * k * np.pi for k in ks[r0:r0 + chunk]], dtype=np.complex128)
+        E = np.exp(coef[:, None] * time[None, :] / period)
+        W[r0:r0 + len(coef), :, 0] = E.real
+        W[r0:r0 + len(coef), :, 1] = E.imag
+    starts = list(range(0, len(ks), chunk))
+    if len(starts) > 1:  # numpy releases the GIL inside the ufunc loops
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(max_workers=min(8, len(starts))) as ex:
+            list(ex.map(rows, starts))
+    else:
+        rows(0)
+    return W
+
+
 def num_valid_modes_loop(energy, ns, tol_CN=1.0e-15):
     """PODFS.py:1312-1317, literally (a Python loop over up to ns - 2 numpy scalars)."""
     n = 0

@@ -238,3 +238,54 @@ def test_verbose_cli_two_ranks_one_device(tmp_path):
         sg = np.sign(np.dot(a[:, 1], b[:, 1]))
         assert np.max(np.abs(a[:, 1] - sg * b[:, 1])) <= 1e-9 * np.max(np.abs(a[:, 1])), n
     assert (single / "PODFS" / "PODFS_mean.prf").read_text() == (multi / "PODFS" / "PODFS_mean.prf").read_text()
+
+
+def test_pack_unpack_lower_kernels():
+    """pods_pack_lower / pods_unpack_lower (the all-reduce's packed triangle): the pack is the
+    lower triangle row by row, the unpack writes packed / ns to both triangles -- exactly
+    torch's IEEE division, C exactly symmetric -- at sizes with ragged 64 x 64 edge tiles."""
+    import podsgen
+    from podsgen import engine as E
+    ctx = E.Context(0)
+    try:
+        pack, unpack = E.device_triangle_ops(ctx)
+        for n in (1, 2, 63, 64, 65, 130, 1000):
+            C = torch.randn(n, n, dtype=torch.float64, device="cuda")
+            packed = pack(C)
+            r, c = torch.tril_indices(n, n, device="cuda")
+            assert torch.equal(packed, C[r, c]), n
+            packed.mul_(3.0)
+            out = torch.full((n, n), float("nan"), dtype=torch.float64, device="cuda")
+            unpack(packed, out)
+            torch.cuda.synchronize()
+            ref = torch.zeros_like(out)
+            ref[r, c] = packed / n
+            ref[c, r] = packed / n
+            assert torch.equal(out, ref), n
+            assert torch.equal(out, out.T)
+        podsgen.check(ctx.lib.pods_synchronize(ctx.h), "sync")
+    finally:
+        ctx.close()
+
+
+@pytest.mark.timeout(600)
+def test_bench_launches_its_own_ranks():
+    """`bench.py --gpus 2` without a launcher starts 2 ranks itself (torch.distributed.run as a
+    child process); with --backend gloo both share this one GPU.  Rank 0's JSON line reports
+    the world it observed and the all-reduce stage (PODFS.py:1451-1455 summed over slabs)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                        "--config", "c1", "--steps", "2", "--warmup", "1", "--no-cpu"],
+                       capture_output=True, text=True, timeout=540, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["n_gpus"] == 2 and out["config"]["dist_world_size"] == 2
+    assert out["config"]["backend"] == "gloo"
+    assert "allreduce" in out["stages_ms"]
+    assert out["metric"].startswith("filtered-snapshot Mpoints/s") and "32x32" in out["metric"]
+    assert out["value"] > 0

@@ -60,3 +60,47 @@ def test_pipeline_two_stage_vs_reference(ctx, golden_dir, monkeypatch, name):
     _check_modes(pod, g, s)
     fo = E.run_fourier(ctx, pod.T, pod.nm, s.ns, s.dt_eff, s.et)
     assert np.array_equal(fo.c_count, g["N_FC"])
+
+
+def _structured(kind, n, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    dev = "cuda"
+    if kind == "diagonal":   # every panel column below the band is exactly zero
+        return torch.diag(torch.linspace(3.0, -1.0, n, dtype=torch.float64)).to(dev).contiguous()
+    if kind == "zero":
+        return torch.zeros((n, n), dtype=torch.float64, device=dev)
+    if kind == "banded":     # bandwidth 20 < 32: stage 1 meets zero columns under every panel
+        B = torch.randn(n, n, generator=g, dtype=torch.float64)
+        B = torch.triu(torch.tril(B, 20), -20)
+        return (0.5 * (B + B.T)).to(dev).contiguous()
+    if kind == "blockdiag":  # two dense blocks, zero coupling
+        h = n // 2
+        C = torch.zeros((n, n), dtype=torch.float64)
+        for a, b in ((0, h), (h, n)):
+            X = torch.randn(b - a, b - a, generator=g, dtype=torch.float64)
+            C[a:b, a:b] = X @ X.T / (b - a)
+        return C.to(dev).contiguous()
+    if kind == "repeated":   # I + u u^T: eigenvalue 1 with multiplicity n - 1
+        u = torch.randn(n, generator=g, dtype=torch.float64)
+        return (torch.eye(n, dtype=torch.float64) + torch.outer(u, u)).to(dev).contiguous()
+    raise ValueError(kind)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("n", [34, 4200])
+@pytest.mark.parametrize("kind", ["diagonal", "zero", "banded", "blockdiag", "repeated"])
+@pytest.mark.parametrize("nvec", [0, 1, 64])
+def test_syev2_structured(ctx, kind, n, nvec):
+    """Structured and degenerate inputs of the two-stage solver (panel columns that are exactly
+    zero below the band, clusters, exact multiplicities) against eigh; with tagged hand-off
+    values cleared on read, a zero column stays zero and its reflector is the identity."""
+    C = _structured(kind, n, seed=n + nvec)
+    lam, Y = solve2(ctx, C, min(nvec, n))
+    if kind == "zero":
+        assert np.all(lam == 0.0)
+        if nvec:
+            assert np.max(np.abs(Y.T @ Y - np.eye(Y.shape[1]))) <= 1e-12
+        return
+    check_against_eigh(C, lam, Y)
+    if Y.shape[1]:
+        assert np.max(np.abs(Y.T @ Y - np.eye(Y.shape[1]))) <= 1e-12

@@ -26,6 +26,43 @@ def test_library_exports_every_header_symbol():
     assert _lib.load().pods_abi_version() == 1
 
 
+def test_persistent_grid_rule():
+    """The co-residency rule every spin-waiting launch passes first (pods::check_persistent):
+    a grid larger than blocks-per-CU x CUs is refused with PODS_ERR_UNSUPPORTED."""
+    from podsgen import _lib
+    lib = _lib.load()
+    assert lib.pods_host_persistent_grid_fits(1, 256, 256) == 0
+    assert lib.pods_host_persistent_grid_fits(2, 256, 512) == 0
+    assert lib.pods_host_persistent_grid_fits(1, 256, 257) == -6
+    assert b"257" in lib.pods_last_error()
+    assert lib.pods_host_persistent_grid_fits(0, 256, 1) == -6   # kernel cannot run at all
+    assert lib.pods_host_persistent_grid_fits(1, 224, 256) == -6  # CU-masked / partitioned device
+    assert lib.pods_host_persistent_grid_fits(-1, 256, 1) == -1
+
+
+@pytest.mark.parametrize("ns,dt", [(4096, 0.1), (520, 0.037), (17, 0.05), (64, 0.1), (5, 0.1), (2, 0.3),
+                                   (8192, 0.0731)])
+def test_dft_twiddles_are_the_reference_expression(ns, dt):
+    """podsgen.host.dft_twiddles (the table the GPU DFT multiplies by) equals the reference's
+    np.exp(-1j*2*k*np.pi*time/period) (PODFS.py:1566) bit for bit, row by row, and the rows it
+    omits (k < 0 except -ns/2) are exact conjugates of stored ones (the kernel writes
+    c[h-k] = conj(c[h+k]))."""
+    from podsgen.host import dft_rows, dft_twiddles, time_axis
+    time_, period = time_axis(ns, dt)
+    W = dft_twiddles(ns, time_, period, chunk=7)
+    ks = dft_rows(ns)
+    assert W.shape == (len(ks), ns, 2)
+    pick = range(len(ks)) if ns <= 520 else list(range(0, len(ks), 97)) + [len(ks) - 2, len(ks) - 1]
+    for q in pick:
+        k = ks[q]
+        e = np.exp(-1j * 2 * k * np.pi * time_ / period)
+        assert np.array_equal(W[q, :, 0].view(np.uint64), e.real.view(np.uint64)), (ns, k)
+        assert np.array_equal(W[q, :, 1].view(np.uint64), e.imag.view(np.uint64)), (ns, k)
+        if 0 < k:
+            en = np.exp(-1j * 2 * (-k) * np.pi * time_ / period)
+            assert np.array_equal(en.real, e.real) and np.array_equal(en.imag, -e.imag), (ns, k)
+
+
 @pytest.mark.parametrize("seed,nblocks", [(0, 2), (12345, 3), (7, 1000), (2 ** 32 - 1, 65537)])
 def test_host_mt_jump_math(seed, nblocks):
     from podsgen import _lib
@@ -267,7 +304,16 @@ def _gloo_worker(rank, world, port, A, out):
     mean = np.mean(Al, 1)
     Ac = Al - mean[:, None]
     C = torch.from_numpy(np.dot(Ac.T, Ac))
-    E.allreduce_correlation(dist, C, ns, lambda x, d: x.copy_(torch.from_numpy(x.numpy() / d)))
+    r_, c_ = torch.tril_indices(ns, ns)   # CPU stand-ins for pods_pack_lower / pods_unpack_lower
+
+    def pack(M):
+        return M[r_, c_].clone()
+
+    def unpack(packed, M):
+        x = torch.from_numpy(packed.numpy() / ns)
+        M[r_, c_] = x
+        M[c_, r_] = x
+    E.allreduce_correlation(dist, C, ns, pack, unpack)
     s = podsgen.DFSetup(jma=J, kma=K, ns=ns, seed=1)
     full = df.gather_row_slabs(dist, s, np.concatenate([mean[:, None], Ac], axis=1))
     out[rank] = (C.numpy().tobytes(), None if full is None else full.tobytes())
