@@ -94,6 +94,12 @@ int pods_df_snapshots(pods_ctx* ctx, double** a_dev, int64_t* row_len);
  * re-laid out into the K-tiled device layout. */
 int pods_set_snapshots(pods_ctx* ctx, const double* at_host, int ns, int64_t row_len);
 
+/* Snapshots [i0, i1) of the device matrix in the reference's column order, one snapshot per
+ * row: out_dev[(i - i0) * row_len + r] = A[r, i] (A as digitalfilters.py:1397 lays it out,
+ * A[:, i] = the i-th snapshot; SURVEY 8(b) pods_copy_snapshots).  Device output, stream-ordered;
+ * the current contents of A (centred after pods_center). */
+int pods_copy_snapshots(pods_ctx* ctx, int i0, int i1, double* out_dev);
+
 /* Stream-ordered copy between host/device buffers of this context's device
  * (kind: 0 = host->device, 1 = device->host, 2 = device->device).  device->host
  * synchronises the stream before returning. */
@@ -156,6 +162,29 @@ int pods_sytrd_trace(pods_ctx* ctx, const double* C_dev, int n, int wg, int64_t*
 /* 0 if the last pods_syev / pods_sytrd ran to completion, PODS_ERR_INTERNAL if its
  * cross-workgroup wait timed out (results invalid).  Synchronises the stream. */
 int pods_syev_status(pods_ctx* ctx);
+
+/* All n eigenvalues of C alone (the full spectrum POD.eigenvalues.dat and the valid-mode count
+ * consume, PODFS.py:1309-1320, :1339), as a sequence of stream-ordered units that a caller can
+ * spread over several calls: units 0..U-2 are the column ranges of the tridiagonalisation
+ * (512 columns each, U - 1 = (n-1)/512 + 1), unit U-1 the bisection.  Each slot (0..15) has its
+ * own workspace, so several matrices may be in flight at once.  n <= 4096.
+ *   pods_eigvals_begin    starts slot on C_dev (n x n row-major, read by unit 0 only, so C may
+ *                         be reused by work enqueued after this call) and runs unit 0
+ *   pods_eigvals_advance  runs up to max_units more units; *remaining = units still to run
+ *   pods_eigvals_fetch    when none remain: copies the n eigenvalues, descending, to lam_desc_dev
+ *   pods_eigvals_status   synchronises; PODS_ERR_INTERNAL if a hand-off wait timed out */
+int pods_eigvals_begin(pods_ctx* ctx, int slot, const double* C_dev, int n);
+int pods_eigvals_advance(pods_ctx* ctx, int slot, int max_units, int* remaining);
+int pods_eigvals_fetch(pods_ctx* ctx, int slot, double* lam_desc_dev);
+int pods_eigvals_status(pods_ctx* ctx, int slot);
+
+/* One step of the Chebyshev-filtered subspace iteration that finds the nm leading eigenpairs
+ * (podsgen/subspace.py; PODFS.py:1309-1333 consumes only those): out = alpha (C Y) + beta Y +
+ * gamma Z on fp64 MFMA, C_dev n x n row-major, Y_dev / Z_dev / out_dev n x m row-major with m a
+ * multiple of 64, out_dev distinct from Y_dev and Z_dev; Z_dev may be NULL (gamma ignored).
+ * Deterministic (fixed reduction order).  Stream-ordered. */
+int pods_cheb_step(pods_ctx* ctx, const double* C_dev, int n, const double* Y_dev, const double* Z_dev, int m,
+                   double alpha, double beta, double gamma, double* out_dev);
 
 /* Two-stage eigensolver for correlation matrices beyond pods_syev's on-chip limit (BASELINE
  * configs 4/5, PODFS.py:1309-1310 at ns = 8192, 16384): dense -> band (bandwidth 32, fp64 MFMA

@@ -223,6 +223,16 @@ int syrk_kernel_choice() {
 
 }  // namespace
 
+// One eigenvalues-only tridiagonalisation in flight (pods_eigvals_*): its own workspace, so
+// several matrices can be at different column ranges at once.
+struct EigvalSlot {
+  DevBuf wm, x, flags, det, v, cnt, lam;
+  int n = 0, R = 0, klast = 0;
+  int next = 0;       // next unit: ranges 0..klast, then klast + 1 = the bisection
+  bool active = false;
+  pods::TrdArgs args{};
+};
+
 struct pods_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -256,6 +266,7 @@ struct pods_ctx {
   int dft_w_ns = -1;
   double dft_w_period = 0.0;
   std::vector<double> dft_w_t;
+  std::vector<EigvalSlot> eslots;
 };
 
 namespace {
@@ -353,6 +364,8 @@ int pods_destroy(pods_ctx* c) {
                     &c->e2_ipiv, &c->dft_w})
     release(*b);
   c->rng.free_all();
+  for (EigvalSlot& sl : c->eslots)
+    for (DevBuf* b : {&sl.wm, &sl.x, &sl.flags, &sl.det, &sl.v, &sl.cnt, &sl.lam}) release(*b);
   delete c;
   return PODS_OK;
   PODS_CATCH
@@ -670,6 +683,24 @@ int pods_divide_inplace(pods_ctx* c, double* x, int64_t n, double d) {
   return PODS_OK;
 }
 
+int pods_copy_snapshots(pods_ctx* c, int i0, int i1, double* out_dev) {
+  if (int e = check_ctx(c)) return e;
+  if (!c->have_snapshots) return fail(PODS_ERR_STATE, "pods_copy_snapshots: no snapshots");
+  if (!out_dev || i0 < 0 || i1 > c->p.ns || i0 > i1) return fail(PODS_ERR_ARG, "pods_copy_snapshots: bad range");
+  PODS_HIP(hipSetDevice(c->device));
+  PODS_HIP(pods::launch_gather_snapshots(c->A.as<double>(), c->p.ns, c->rowlen, i0, i1, out_dev, c->stream));
+  return PODS_OK;
+}
+
+int pods_cheb_step(pods_ctx* c, const double* C, int n, const double* Y, const double* Z, int m, double alpha,
+                   double beta, double gamma, double* out) {
+  if (int e = check_ctx(c)) return e;
+  if (!C || !Y || !out || n < 1 || m < 64 || m % 64 != 0 || out == Y || (Z && out == Z))
+    return fail(PODS_ERR_ARG, "pods_cheb_step: bad arguments (m must be a multiple of 64, out distinct)");
+  PODS_HIP(pods::launch_cheb_step(C, n, n, Y, Z, m, alpha, beta, gamma, out, c->stream));
+  return PODS_OK;
+}
+
 int pods_pack_lower(pods_ctx* c, const double* C, int n, double* packed) {
   if (int e = check_ctx(c)) return e;
   if (!C || !packed || n < 1) return fail(PODS_ERR_ARG, "pods_pack_lower: bad arguments");
@@ -766,6 +797,118 @@ int run_sytrd(pods_ctx* c, const double* C, int n, int* R_out, int64_t* trace = 
 }
 
 }  // namespace
+
+namespace {
+constexpr int EIGVAL_SLOTS = 16;
+
+int eigval_units(const EigvalSlot& sl) { return sl.klast + 2; }  // trd ranges + the bisection
+
+// launch the slot's units [next, next + count)
+int eigval_run(pods_ctx* c, EigvalSlot& sl, int count) {
+  const int total = eigval_units(sl);
+  const int end = std::min(total, sl.next + count);
+  if (sl.next <= sl.klast && end > sl.next) {
+    const int ke = std::min(end - 1, sl.klast);
+    PODS_HIP(pods::launch_trd_ranges(sl.args, sl.R, sl.next, ke, c->stream));
+  }
+  if (end == total && sl.next < total) {  // the bisection: all n eigenvalues of T
+    double* det = sl.det.as<double>();
+    PODS_HIP(pods::launch_tri_eigvals(det, det + sl.n, sl.n, det + 3 * (int64_t)sl.n, sl.lam.as<double>(),
+                                      sl.cnt.as<int>(), c->stream));
+  }
+  sl.next = end;
+  return PODS_OK;
+}
+}  // namespace
+
+int pods_eigvals_begin(pods_ctx* c, int slot, const double* C, int n) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (slot < 0 || slot >= EIGVAL_SLOTS || !C || n < 1) return fail(PODS_ERR_ARG, "pods_eigvals_begin: bad arguments");
+  int R = 0, G = 0;
+  int64_t slab = 0;
+  if (pods::trd_plan(n, &R, &G, &slab) != 0)
+    return fail(PODS_ERR_UNSUPPORTED, "pods_eigvals_begin: n = " + std::to_string(n) + " > 4096");
+  PODS_HIP(hipSetDevice(c->device));
+  if ((int)c->eslots.size() <= slot) c->eslots.resize(slot + 1);
+  EigvalSlot& sl = c->eslots[slot];
+  if (sl.active && sl.next < eigval_units(sl))
+    return fail(PODS_ERR_STATE, "pods_eigvals_begin: slot " + std::to_string(slot) + " still running");
+  PODS_HIP(ensure(sl.wm, (size_t)slab * sizeof(double)));
+  PODS_HIP(ensure(sl.x, (size_t)32 * n * sizeof(double)));
+  PODS_HIP(ensure(sl.flags, 64));
+  PODS_HIP(ensure(sl.det, ((size_t)4 * n + 8) * sizeof(double)));
+  PODS_HIP(ensure(sl.v, (size_t)std::max(n - 1, 1) * n * sizeof(double)));
+  PODS_HIP(ensure(sl.cnt, pods::tri_grid_bytes()));
+  PODS_HIP(ensure(sl.lam, (size_t)n * sizeof(double)));
+  PODS_HIP(hipMemsetAsync(sl.flags.p, 0, 64, c->stream));
+  PODS_HIP(hipMemsetAsync(sl.x.p, 0, (size_t)32 * n * sizeof(double), c->stream));
+  double* det = sl.det.as<double>();
+  pods::TrdArgs a{};
+  a.C = C;
+  a.ldc = n;
+  a.n = n;
+  a.G = G;
+  a.klast = (n - 1) / 512;
+  a.Wm = sl.wm.as<double>();
+  a.pbuf = sl.x.as<double>();
+  a.rbuf = sl.x.as<double>() + 16 * (int64_t)n;
+  a.flags = sl.flags.as<uint32_t>();
+  a.D = det;
+  a.E = det + n;
+  a.tau = det + 2 * (int64_t)n;
+  a.V = sl.v.as<double>();
+  a.ldv = n;
+  a.nrep = 8;
+  sl.args = a;
+  sl.n = n;
+  sl.R = R;
+  sl.klast = a.klast;
+  sl.next = 0;
+  sl.active = true;
+  return eigval_run(c, sl, 1);  // range 0 is the only one that reads C
+  PODS_CATCH
+}
+
+int pods_eigvals_advance(pods_ctx* c, int slot, int max_units, int* remaining) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (slot < 0 || slot >= (int)c->eslots.size() || !c->eslots[slot].active || max_units < 0)
+    return fail(PODS_ERR_ARG, "pods_eigvals_advance: no such slot");
+  PODS_HIP(hipSetDevice(c->device));
+  EigvalSlot& sl = c->eslots[slot];
+  if (int e = eigval_run(c, sl, max_units)) return e;
+  if (remaining) *remaining = eigval_units(sl) - sl.next;
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_eigvals_fetch(pods_ctx* c, int slot, double* lam_desc_dev) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (slot < 0 || slot >= (int)c->eslots.size() || !c->eslots[slot].active || !lam_desc_dev)
+    return fail(PODS_ERR_ARG, "pods_eigvals_fetch: no such slot");
+  EigvalSlot& sl = c->eslots[slot];
+  if (sl.next < eigval_units(sl)) return fail(PODS_ERR_STATE, "pods_eigvals_fetch: units still to run");
+  PODS_HIP(hipSetDevice(c->device));
+  PODS_HIP(hipMemcpyAsync(lam_desc_dev, sl.lam.p, (size_t)sl.n * sizeof(double), hipMemcpyDeviceToDevice,
+                          c->stream));
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_eigvals_status(pods_ctx* c, int slot) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (slot < 0 || slot >= (int)c->eslots.size() || !c->eslots[slot].active)
+    return fail(PODS_ERR_ARG, "pods_eigvals_status: no such slot");
+  uint32_t abort_word = 0;
+  PODS_HIP(hipMemcpyAsync(&abort_word, c->eslots[slot].flags.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+  PODS_HIP(hipStreamSynchronize(c->stream));
+  if (abort_word) return fail(PODS_ERR_INTERNAL, "pods_eigvals: hand-off wait timed out (aborted)");
+  return PODS_OK;
+  PODS_CATCH
+}
 
 int pods_syev(pods_ctx* c, const double* C, int n, int nvec, double* lam_desc, double* vec) {
   PODS_TRY

@@ -1358,12 +1358,18 @@ int trd_plan(int n, int* R, int* G, int64_t* slab_doubles) {
 // Range 1 (14 rows x 7 slots) keeps all of it in VGPRs + LDS even though the compiler then
 // spills ~100 VGPRs of loop-invariant state: 5.43 ms against 6.25 ms with a slab slot,
 // whose mixed load/store traffic serialises every row group on a full vmcnt drain.
-hipError_t launch_trd(const TrdArgs& a, int R, hipStream_t st) {
+hipError_t launch_trd(const TrdArgs& a, int R, hipStream_t st) { return launch_trd_ranges(a, R, 0, 7, st); }
+
+// Column ranges kb..ke (inclusive, clipped to klast) of the tridiagonalisation: each range is
+// its own launch and leaves the live block parked in a.Wm, so a caller may run the ranges of
+// one matrix in separate calls (with other work on the stream between them) as long as the
+// workspace of TrdArgs is left alone in between.
+hipError_t launch_trd_ranges(const TrdArgs& a, int R, int kb, int ke, hipStream_t st) {
   using namespace eig;
   hipError_t e = hipSuccess;
   if (a.klast != (a.n - 1) / TT) return hipErrorInvalidValue;
 #define PODS_TRD(RR, SS, KK, SGG, SLL) \
-  if (e == hipSuccess && KK <= a.klast) e = launch_trd_t<RR, SS, KK, SGG, SLL>(a, st)
+  if (e == hipSuccess && KK <= a.klast && KK >= kb && KK <= ke) e = launch_trd_t<RR, SS, KK, SGG, SLL>(a, st)
   switch (R) {
     case 1: PODS_TRD(1, 1, 0, 0, 0); break;
     case 2: PODS_TRD(2, 1, 0, 0, 0); break;

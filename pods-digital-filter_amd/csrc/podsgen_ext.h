@@ -14,4 +14,13 @@ int dft_table_rows(int ns);
 hipError_t launch_dft_tab(const double* T, int ldT, int nm, int ns, const double2* W, const int* prog, int nprog,
                           const int* leaves, int nleaf, double inv_n, float2* c, hipStream_t st);
 
+// snapshots [i0, i1) of the K-tiled snapshot matrix as (i1-i0) x rowlen rows (podsgen_pack.hip)
+hipError_t launch_gather_snapshots(const double* AT, int ns, int64_t rowlen, int i0, int i1, double* out,
+                                   hipStream_t st);
+
+// out = alpha (C Y) + beta Y + gamma Z on fp64 MFMA; C n x n (ld ldc), Y/Z/out n x m row-major,
+// m a multiple of 64, out distinct from Y and Z (podsgen_subspace.hip)
+hipError_t launch_cheb_step(const double* C, int64_t ldc, int n, const double* Y, const double* Z, int m,
+                            double alpha, double beta, double gamma, double* out, hipStream_t st);
+
 }  // namespace pods

@@ -81,6 +81,8 @@ struct TrdArgs {
 };
 int trd_plan(int n, int* R, int* G, int64_t* slab_doubles);
 hipError_t launch_trd(const TrdArgs& a, int R, hipStream_t st);
+// ranges kb..ke only (range K = columns [512K - 1, 512(K + 1) - 1)); klast + 1 ranges in all
+hipError_t launch_trd_ranges(const TrdArgs& a, int R, int kb, int ke, hipStream_t st);
 // bounds: 4 doubles {gl, gu, pivmin, atol}; lam_desc: n eigenvalues of T, descending
 // grid_cnt (tri_grid_bytes(), may be null): counts at shared shifts for the first brackets
 // deg: 2n doubles of scratch, needed when n > 10240 ({d, e^2} then live in global memory)

@@ -14,6 +14,7 @@
 #include <cstdint>
 
 #include "podsgen_kernels.h"
+#include "podsgen_ext.h"
 
 namespace pods {
 namespace {
@@ -59,7 +60,27 @@ __global__ __launch_bounds__(256) void k_unpack_lower(const double* __restrict__
   }
 }
 
+// snapshots i0..i1-1 of the K-tiled matrix (element (i, r) at ((r/16) ns + i) 16 + r%16) as
+// rows of a (i1-i0) x rowlen row-major block: out[(i - i0) rowlen + r]
+__global__ __launch_bounds__(256) void k_gather_snapshots(const double* __restrict__ AT, int ns, int64_t rowlen,
+                                                           int i0, int w, double* __restrict__ out) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)w * rowlen) return;
+  const int64_t ii = idx / rowlen, r = idx - ii * rowlen;
+  out[idx] = AT[(((r >> 4) * ns + i0 + ii) << 4) + (r & 15)];
+}
+
 }  // namespace
+
+hipError_t launch_gather_snapshots(const double* AT, int ns, int64_t rowlen, int i0, int i1, double* out,
+                                   hipStream_t st) {
+  const int w = i1 - i0;
+  if (w <= 0) return hipSuccess;
+  const int64_t tot = (int64_t)w * rowlen;
+  hipLaunchKernelGGL(k_gather_snapshots, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, AT, ns, rowlen,
+                     i0, w, out);
+  return hipGetLastError();
+}
 
 hipError_t launch_pack_lower(const double* C, int64_t ldc, int n, double* packed, hipStream_t st) {
   if (n <= 0) return hipSuccess;

@@ -44,6 +44,7 @@ SIGNATURES = {
     "pods_df_generate": (c_int, [c_void_p]),
     "pods_df_snapshots": (c_int, [c_void_p, ctypes.POINTER(c_void_p), ctypes.POINTER(c_i64)]),
     "pods_set_snapshots": (c_int, [c_void_p, c_void_p, c_int, c_i64]),
+    "pods_copy_snapshots": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "pods_copy": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_size_t, c_int]),
     "pods_mean": (c_int, [c_void_p, c_void_p, c_int]),
     "pods_set_mean": (c_int, [c_void_p, c_void_p]),
@@ -57,6 +58,12 @@ SIGNATURES = {
     "pods_syev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "pods_sytrd": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "pods_syev_status": (c_int, [c_void_p]),
+    "pods_cheb_step": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_dbl, c_dbl, c_dbl,
+                               c_void_p]),
+    "pods_eigvals_begin": (c_int, [c_void_p, c_int, c_void_p, c_int]),
+    "pods_eigvals_advance": (c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_int)]),
+    "pods_eigvals_fetch": (c_int, [c_void_p, c_int, c_void_p]),
+    "pods_eigvals_status": (c_int, [c_void_p, c_int]),
     "pods_syev2": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "pods_syev2_status": (c_int, [c_void_p]),
     "pods_syev2_inspect": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_i64]),

@@ -1,0 +1,145 @@
+"""GPU parity at BASELINE config 4's size on one device: 512 x 512 inlet x 8192 snapshots.
+
+The production pipeline runs ONCE (module fixture): generation (6.76 G stream doubles), mean,
+centring, the split-K SYRK at ns = 8192, the two-stage eigensolver pods_syev2 (the path every
+ns > 4096 takes: PODFS.py:1309-1310), temporal scaling and the spatial modes.  Checked against
+the oracle and fp64 torch without ever copying the 51.5 GB snapshot matrix whole:
+
+  (i)   generation: steps 0, 1 and 8191 bit-exact against the oracle (one pass over the
+        reference's draw stream, oracle.generate_steps), every sampled block finite;
+  (ii)  the mean bit-exact against numpy's pairwise np.mean on 2048 sampled rows (the pairwise
+        sum is per row, so a row sample is exact), and the centred rows == raw - mean;
+  (iii) C exactly symmetric; sampled 256 x 256 tiles within 1e-12 max|C| of torch A_c^T A_c/ns;
+  (iv)  all 8192 eigenvalues within 1e-12 lambda_0 of torch.linalg.eigh on the same C, T
+        sign-aligned within 1e-10 of eigh's scaled vectors (modes with relative gap > 1e-6);
+  (v)   Phi within 1e-10 (per mode) of torch's A_c T Lambda^-1 / ns, columns of unit norm.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+from oracle import pods_oracle as O  # noqa: E402
+
+J, K, NS, SEED = 512, 512, 8192, 4242
+STEPS = [0, 1, NS - 1]
+NROWS = 2048
+
+
+def snap_block(gen, i0, i1):
+    """Snapshots [i0, i1) as a (i1-i0, 3P) device tensor (pods_copy_snapshots)."""
+    import podsgen
+    out = torch.empty((i1 - i0, gen.rowlen), dtype=torch.float64, device="cuda")
+    podsgen.check(gen.ctx.lib.pods_copy_snapshots(gen.ctx.h, i0, i1, ctypes.c_void_p(out.data_ptr())),
+                  "pods_copy_snapshots")
+    return out
+
+
+def sample_rows(gen, rows, chunk=512):
+    """A[rows, :] (the reference layout's rows) gathered chunk by chunk: (len(rows), ns) host."""
+    out = np.empty((len(rows), NS))
+    idx = torch.from_numpy(rows).cuda()
+    for i0 in range(0, NS, chunk):
+        b = snap_block(gen, i0, min(NS, i0 + chunk))
+        out[:, i0:i0 + b.shape[0]] = b.index_select(1, idx).T.cpu().numpy()
+        del b
+    return out
+
+
+@pytest.fixture(scope="module")
+def c4():
+    import podsgen
+    from podsgen import engine as E
+    assert torch.cuda.is_available(), "GPU tests need a ROCm device"
+    s = podsgen.DFSetup(jma=J, kma=K, ns=NS, seed=SEED)
+    gen = E.Generator(s, device=0)
+    snap = gen.generate()
+    rows = np.sort(np.random.default_rng(5).choice(gen.rowlen, NROWS, replace=False))
+    cols = {i: snap_block(gen, i, i + 1)[0].cpu().numpy() for i in STEPS}
+    raw_rows = sample_rows(gen, rows)
+    pod = E.run_pod(snap, s.nm, keep_C=True)
+    torch.cuda.synchronize()
+    cen_rows = sample_rows(gen, rows)
+    yield dict(s=s, gen=gen, pod=pod, rows=rows, cols=cols, raw_rows=raw_rows, cen_rows=cen_rows)
+    gen.ctx.close()
+
+
+@pytest.mark.timeout(900)
+def test_c4_generation_sampled_steps_bit_exact(c4):
+    cfg = O.DFConfig(jma=J, kma=K, ns=NS, seed=SEED)
+    ref = O.generate_steps(cfg, STEPS)
+    for i in STEPS:
+        bad = np.nonzero(c4["cols"][i] != ref[i])[0]
+        assert bad.size == 0, (i, bad[:8])
+    assert np.all(np.isfinite(c4["raw_rows"]))
+
+
+@pytest.mark.timeout(600)
+def test_c4_mean_and_centring_rows_bit_exact(c4):
+    rows, raw = c4["rows"], c4["raw_rows"]
+    mean_ref = np.mean(raw, 1)                                  # main() :1492, per row
+    mean = c4["pod"].mean.cpu().numpy()[rows]
+    assert np.array_equal(mean, mean_ref)
+    assert np.array_equal(c4["cen_rows"], raw - mean[:, None])  # :1493-1495
+
+
+@pytest.mark.timeout(600)
+def test_c4_correlation_tiles(c4):
+    C = c4["pod"].C
+    assert torch.equal(C, C.T)
+    cmax = float(C.abs().max())
+    b = 256
+    for bi, bj in [(0, 0), (1, 0), (13, 7), (31, 0), (31, 30), (31, 31)]:
+        X = snap_block(c4["gen"], bi * b, (bi + 1) * b)
+        Y = X if bj == bi else snap_block(c4["gen"], bj * b, (bj + 1) * b)
+        ref = (X @ Y.T) / NS
+        got = C[bi * b:(bi + 1) * b, bj * b:(bj + 1) * b]
+        err = float((got - ref).abs().max())
+        assert err <= 1e-12 * cmax, (bi, bj, err / cmax)
+        del X, Y
+
+
+@pytest.mark.timeout(600)
+def test_c4_eigen_two_stage_vs_eigh(c4):
+    pod, s = c4["pod"], c4["s"]
+    lam_t, V = torch.linalg.eigh(pod.C)
+    lam = torch.flip(lam_t, (0,)).cpu().numpy()
+    assert np.max(np.abs(pod.energy - lam)) <= 1e-12 * lam[0]
+    assert pod.num_valid == O.num_valid_modes(lam, NS) and pod.nm == s.nm
+    nm = pod.nm
+    Vd = torch.flip(V, (1,))[:, :nm].cpu().numpy()
+    T = pod.T.cpu().numpy()[:, :nm]
+    checked = 0
+    for j in range(nm):
+        v = Vd[:, j]
+        Tref = v * np.sqrt(lam[j] / (np.sum(v * v) / NS))
+        gap = min(abs(lam[j] - lam[j - 1]) if j else np.inf, abs(lam[j] - lam[j + 1]))
+        if gap <= 1e-6 * lam[0]:
+            continue
+        sg = np.sign(np.dot(T[:, j], Tref))
+        assert np.max(np.abs(sg * T[:, j] - Tref)) <= 1e-10 * np.max(np.abs(Tref)), j
+        checked += 1
+    assert checked >= nm // 2
+
+
+@pytest.mark.timeout(900)
+def test_c4_spatial_modes(c4):
+    pod, gen = c4["pod"], c4["gen"]
+    nm = pod.nm
+    T = pod.T[:, :nm]
+    lam = torch.from_numpy(np.ascontiguousarray(pod.energy[:nm])).cuda()
+    acc = torch.zeros((gen.rowlen, nm), dtype=torch.float64, device="cuda")
+    for i0 in range(0, NS, 512):                   # A_c T, snapshot block by block
+        b = snap_block(gen, i0, i0 + 512)
+        acc += b.T @ T[i0:i0 + 512]
+        del b
+    ref = acc / lam[None, :] / NS                  # PODFS.py:1330-1333
+    phi = pod.phi
+    for j in range(nm):
+        err = float((phi[:, j] - ref[:, j]).abs().max())
+        assert err <= 1e-10 * float(ref[:, j].abs().max()), j
+    norms = torch.linalg.vector_norm(phi, dim=0).cpu().numpy()
+    assert np.all(np.abs(norms - 1.0) <= 1e-9), norms

@@ -243,7 +243,7 @@ def test_verbose_cli_two_ranks_one_device(tmp_path):
 def test_pack_unpack_lower_kernels():
     """pods_pack_lower / pods_unpack_lower (the all-reduce's packed triangle): the pack is the
     lower triangle row by row, the unpack writes packed / ns to both triangles -- exactly
-    torch's IEEE division, C exactly symmetric -- at sizes with ragged 64 x 64 edge tiles."""
+    numpy's IEEE division, C exactly symmetric -- at sizes with ragged 64 x 64 edge tiles."""
     import podsgen
     from podsgen import engine as E
     ctx = E.Context(0)
@@ -258,9 +258,11 @@ def test_pack_unpack_lower_kernels():
             out = torch.full((n, n), float("nan"), dtype=torch.float64, device="cuda")
             unpack(packed, out)
             torch.cuda.synchronize()
+            # numpy's true division (torch divides by a Python scalar as a multiply by 1/n)
+            q = torch.from_numpy(packed.cpu().numpy() / n).cuda()
             ref = torch.zeros_like(out)
-            ref[r, c] = packed / n
-            ref[c, r] = packed / n
+            ref[r, c] = q
+            ref[c, r] = q
             assert torch.equal(out, ref), n
             assert torch.equal(out, out.T)
         podsgen.check(ctx.lib.pods_synchronize(ctx.h), "sync")

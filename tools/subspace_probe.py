@@ -120,14 +120,45 @@ def main(out):
             C @ Xw
         torch.cuda.synchronize()
         res["gemm_us_w%d" % w] = (time.time() - t) / 20 * 1e6
+    from podsgen.subspace import leading_eigenpairs, Subspace
+    prod = []
+    Vh = Vr[:, :k].cpu().numpy()
+    ws = Subspace(gen.ctx, n, 64)
+    # raw kernel speed: pods_cheb_step at m = 64
+    Y = torch.randn(n, 64, dtype=torch.float64, device="cuda")
+    Z = torch.randn(n, 64, dtype=torch.float64, device="cuda")
+    O_ = torch.empty_like(Y)
+    ws.step(C, Y, Z, 1.0, 0.5, 0.25, O_)
+    ref = (C @ Y) + 0.5 * Y + 0.25 * Z
+    torch.cuda.synchronize()
+    res["cheb_err"] = float((O_ - ref).abs().max() / ref.abs().max())
+    t = time.time()
+    for _ in range(50):
+        ws.step(C, Y, Z, 1.0, 0.5, 0.25, O_)
+    torch.cuda.synchronize()
+    res["cheb_us"] = (time.time() - t) / 50 * 1e6
+    print(json.dumps(dict(cheb_us=res["cheb_us"], cheb_err=res["cheb_err"])), flush=True)
+    for deg, ch in ((12, 4), (12, 5), (10, 5), (16, 3), (8, 6), (14, 4)):
+        for rep in range(2):
+            torch.cuda.synchronize()
+            t = time.time()
+            th, Xk, info = leading_eigenpairs(gen.ctx, C, k, m=64, degree=deg, chunks=ch, tol=3e-14, ws=ws)
+            torch.cuda.synchronize()
+            dt = time.time() - t
+        Xh = Xk.cpu().numpy()
+        err = [float(np.max(np.abs(np.sign(np.dot(Xh[:, j], Vh[:, j])) * Xh[:, j] - Vh[:, j]))) for j in range(k)]
+        prod.append(dict(deg=deg, chunks=ch, s=dt, vec_err=max(err),
+                         lam_err=float(np.max(np.abs(th - lam[:k])) / lam[0]), **info))
+        print(json.dumps(prod[-1]), flush=True)
+    res["product"] = prod
     trials = []
     for init in ("fourier", "random"):
-        for m, deg in ((32, 8), (32, 16), (48, 12), (64, 8), (64, 12), (64, 20), (96, 10), (128, 8)):
+        for m, deg in ((64, 12),):
             X0 = fourier_basis(n, m, "cuda") if init == "fourier" else torch.randn(n, m, dtype=torch.float64,
                                                                                     device="cuda")
             torch.cuda.synchronize()
             t = time.time()
-            Xk, th, its, ngemm, hist = chfsi(C, k, m, deg, X0, tol=1e-14)
+            Xk, th, its, ngemm, hist = chfsi(C, k, m, deg, X0, tol=1e-14, max_outer=15)
             torch.cuda.synchronize()
             dt = time.time() - t
             Xh = Xk.cpu().numpy()
