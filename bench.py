@@ -244,12 +244,20 @@ def main():
     setup = make_setup(podsgen, args.config, args.seed)
     gen = E.Generator(setup, device=device, rank=rank, world=world)
     d = dist if world > 1 else None
+    # several ranks: the nm leading eigenpairs on the critical path (subspace iteration), the
+    # rest of the spectrum spread over the ranks' following steps (engine.SpectrumQueue)
+    split = (world > 1 or os.environ.get("PODS_EIGEN") == "split") and ns >= E.SPLIT_MIN_N
+    spectrum = E.SpectrumQueue(gen.ctx, ns, rank, world) if split else None
 
     def step(timer=None):
-        return E.pipeline(setup, device=device, dist=d, gen=gen, timer=timer)
+        return E.pipeline(setup, device=device, dist=d, gen=gen, timer=timer, spectrum=spectrum)
 
     for _ in range(args.warmup):
         step()
+    if spectrum is not None:
+        spectrum.drain()
+        spectrum.results()
+        spectrum.finished.clear()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -260,6 +268,9 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         _, pod, fo = step(timer=tm_run)
+    if spectrum is not None:   # the last steps' spectra finish inside the timed region
+        with tm_run("eig_full_drain"):
+            spectrum.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -281,6 +292,10 @@ def main():
     # the committed PMC summary is for the one-GPU launch; a rank's launch at N > 1 covers
     # only its row slab, so no measured figure applies there
     traffic = load_traffic(args.config, ns, rank) if world == 1 else None
+    num_valid = pod.num_valid
+    if spectrum is not None:   # from the last full spectrum this rank computed
+        done = spectrum.results()
+        num_valid = E.num_valid_modes(done[max(done)], ns) if done else None
     if world > 1:
         dist.barrier()
     if rank == 0:
@@ -309,7 +324,9 @@ def main():
                          "traffic": traffic, "launch_ms": round(corr_ms, 3),
                          "flops_per_launch": flops},
             "stages_ms": {k: round(v, 3) for k, v in stages.items()},
-            "results": {"nm": int(pod.nm), "num_valid": int(pod.num_valid),
+            "results": {"nm": int(pod.nm), "num_valid": None if num_valid is None else int(num_valid),
+                        "eigensolve": "split: leading pairs by subspace iteration + full spectrum spread over "
+                                      "steps (SpectrumQueue)" if spectrum is not None else "fused (pods_syev)",
                         "N_FC": [int(x) for x in fo.c_count] if fo is not None else None},
         }
         if world == 1 and not args.no_cpu and args.config in ("c1", "c3"):

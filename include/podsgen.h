@@ -180,11 +180,21 @@ int pods_eigvals_status(pods_ctx* ctx, int slot);
 
 /* One step of the Chebyshev-filtered subspace iteration that finds the nm leading eigenpairs
  * (podsgen/subspace.py; PODFS.py:1309-1333 consumes only those): out = alpha (C Y) + beta Y +
- * gamma Z on fp64 MFMA, C_dev n x n row-major, Y_dev / Z_dev / out_dev n x m row-major with m a
- * multiple of 64, out_dev distinct from Y_dev and Z_dev; Z_dev may be NULL (gamma ignored).
+ * gamma Z on fp64 MFMA, C_dev n x n row-major, Y_dev / Z_dev / out_dev n x m row-major with
+ * m = 64, out_dev distinct from Y_dev and Z_dev; Z_dev may be NULL (gamma ignored).
  * Deterministic (fixed reduction order).  Stream-ordered. */
 int pods_cheb_step(pods_ctx* ctx, const double* C_dev, int n, const double* Y_dev, const double* Z_dev, int m,
                    double alpha, double beta, double gamma, double* out_dev);
+
+/* The block operations around pods_cheb_step (n x m row-major device blocks, outputs distinct
+ * from inputs, stream-ordered, deterministic):
+ *   pods_gram       G_dev (m x m) = Y^T Z, m = 64 (row-slice partials summed in order)
+ *   pods_cholqr     one Cholesky-QR pass: X = Y R^{-1} with R^T R = Y^T Y (m = 64); twice in a
+ *                   row gives orthonormal columns to working precision (CholQR2)
+ *   pods_right_mul  out = Y M for an m x m row-major M_dev (the Rayleigh-Ritz rotation) */
+int pods_gram(pods_ctx* ctx, const double* Y_dev, const double* Z_dev, int n, int m, double* G_dev);
+int pods_cholqr(pods_ctx* ctx, const double* Y_dev, int n, int m, double* X_dev);
+int pods_right_mul(pods_ctx* ctx, const double* Y_dev, const double* M_dev, int n, int m, double* out_dev);
 
 /* Two-stage eigensolver for correlation matrices beyond pods_syev's on-chip limit (BASELINE
  * configs 4/5, PODFS.py:1309-1310 at ns = 8192, 16384): dense -> band (bandwidth 32, fp64 MFMA

@@ -267,6 +267,7 @@ struct pods_ctx {
   double dft_w_period = 0.0;
   std::vector<double> dft_w_t;
   std::vector<EigvalSlot> eslots;
+  DevBuf sub_part, sub_R, sub_cheb;  // subspace iteration: Gram partials, G / R^{-1}, split-K partials
 };
 
 namespace {
@@ -364,6 +365,9 @@ int pods_destroy(pods_ctx* c) {
                     &c->e2_ipiv, &c->dft_w})
     release(*b);
   c->rng.free_all();
+  release(c->sub_part);
+  release(c->sub_R);
+  release(c->sub_cheb);
   for (EigvalSlot& sl : c->eslots)
     for (DevBuf* b : {&sl.wm, &sl.x, &sl.flags, &sl.det, &sl.v, &sl.cnt, &sl.lam}) release(*b);
   delete c;
@@ -695,9 +699,38 @@ int pods_copy_snapshots(pods_ctx* c, int i0, int i1, double* out_dev) {
 int pods_cheb_step(pods_ctx* c, const double* C, int n, const double* Y, const double* Z, int m, double alpha,
                    double beta, double gamma, double* out) {
   if (int e = check_ctx(c)) return e;
-  if (!C || !Y || !out || n < 1 || m < 64 || m % 64 != 0 || out == Y || (Z && out == Z))
-    return fail(PODS_ERR_ARG, "pods_cheb_step: bad arguments (m must be a multiple of 64, out distinct)");
-  PODS_HIP(pods::launch_cheb_step(C, n, n, Y, Z, m, alpha, beta, gamma, out, c->stream));
+  if (!C || !Y || !out || n < 1 || m != 64 || out == Y || (Z && out == Z))
+    return fail(PODS_ERR_ARG, "pods_cheb_step: bad arguments (m = 64, out distinct)");
+  PODS_HIP(ensure(c->sub_cheb, (size_t)pods::cheb_splits(n) * n * 64 * sizeof(double)));
+  PODS_HIP(pods::launch_cheb_step(C, n, n, Y, Z, m, alpha, beta, gamma, c->sub_cheb.as<double>(), out, c->stream));
+  return PODS_OK;
+}
+
+int pods_gram(pods_ctx* c, const double* Y, const double* Z, int n, int m, double* G) {
+  if (int e = check_ctx(c)) return e;
+  if (!Y || !Z || !G || n < 1 || m != 64) return fail(PODS_ERR_ARG, "pods_gram: bad arguments (m = 64)");
+  PODS_HIP(ensure(c->sub_part, (size_t)pods::gram_slices(n) * m * m * sizeof(double)));
+  PODS_HIP(pods::launch_gram(Y, Z, n, c->sub_part.as<double>(), G, c->stream));
+  return PODS_OK;
+}
+
+int pods_cholqr(pods_ctx* c, const double* Y, int n, int m, double* X) {
+  if (int e = check_ctx(c)) return e;
+  if (!Y || !X || X == Y || n < m || m != 64) return fail(PODS_ERR_ARG, "pods_cholqr: bad arguments");
+  PODS_HIP(ensure(c->sub_part, (size_t)pods::gram_slices(n) * m * m * sizeof(double)));
+  PODS_HIP(ensure(c->sub_R, (size_t)2 * m * m * sizeof(double)));
+  double* G = c->sub_R.as<double>();
+  double* Rinv = G + m * m;
+  PODS_HIP(pods::launch_gram(Y, Y, n, c->sub_part.as<double>(), G, c->stream));
+  PODS_HIP(pods::launch_chol_inv(G, Rinv, c->stream));
+  PODS_HIP(pods::launch_right_mul(Y, Rinv, n, m, X, c->stream));
+  return PODS_OK;
+}
+
+int pods_right_mul(pods_ctx* c, const double* Y, const double* M, int n, int m, double* out) {
+  if (int e = check_ctx(c)) return e;
+  if (!Y || !M || !out || out == Y || n < 1 || m < 16 || m % 16) return fail(PODS_ERR_ARG, "pods_right_mul: bad arguments");
+  PODS_HIP(pods::launch_right_mul(Y, M, n, m, out, c->stream));
   return PODS_OK;
 }
 

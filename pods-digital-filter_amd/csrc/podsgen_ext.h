@@ -18,9 +18,20 @@ hipError_t launch_dft_tab(const double* T, int ldT, int nm, int ns, const double
 hipError_t launch_gather_snapshots(const double* AT, int ns, int64_t rowlen, int i0, int i1, double* out,
                                    hipStream_t st);
 
-// out = alpha (C Y) + beta Y + gamma Z on fp64 MFMA; C n x n (ld ldc), Y/Z/out n x m row-major,
-// m a multiple of 64, out distinct from Y and Z (podsgen_subspace.hip)
+// out = alpha (C Y) + beta Y + gamma Z on fp64 MFMA; C n x n (ld ldc), Y/Z/out n x 64 row-major,
+// out distinct from Y and Z (podsgen_subspace.hip); part: cheb_splits(n) x n x 64 doubles of
+// split-K partials (unused when cheb_splits(n) == 1)
+int cheb_splits(int n);
 hipError_t launch_cheb_step(const double* C, int64_t ldc, int n, const double* Y, const double* Z, int m,
-                            double alpha, double beta, double gamma, double* out, hipStream_t st);
+                            double alpha, double beta, double gamma, double* part, double* out, hipStream_t st);
+
+// small dense pieces of the subspace iteration, m = 64 (podsgen_subspace.hip):
+// G = Y^T Z (64 x 64) through gram_slices(n) row-slice partials in part (summed in order);
+// Rinv = L^{-T} for G = L L^T (X = Y Rinv orthonormalises Y when G = Y^T Y);
+// out = Y M for an m x m M (m a multiple of 16).  Outputs distinct from inputs.
+int gram_slices(int n);
+hipError_t launch_gram(const double* Y, const double* Z, int n, double* part, double* G, hipStream_t st);
+hipError_t launch_chol_inv(const double* G, double* Rinv, hipStream_t st);
+hipError_t launch_right_mul(const double* Y, const double* M, int n, int m, double* out, hipStream_t st);
 
 }  // namespace pods

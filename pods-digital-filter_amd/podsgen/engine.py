@@ -23,6 +23,7 @@ eigensolve -- nothing else.
 import ctypes
 import os
 import time
+import warnings
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -149,8 +150,8 @@ def load_snapshots(A, ctx: Optional[Context] = None, device=0):
 
 @dataclass
 class PODResult:
-    energy: np.ndarray            # all ns eigenvalues, descending (host)
-    num_valid: int
+    energy: Optional[np.ndarray]  # all ns eigenvalues, descending (host); None when a SpectrumQueue has them
+    num_valid: Optional[int]
     nm: int
     mean: "torch.Tensor"          # (3P_local,)
     T: Optional["torch.Tensor"]   # (ns, ncols) scaled temporal modes (rank 0; others: T[:, :nm])
@@ -197,36 +198,189 @@ def device_triangle_ops(ctx):
 SYEV_MAX_N = 4096   # pods_syev's on-chip limit (trd_plan)
 SYEV2_MAX_N = 16384  # pods_syev2 (two-stage): 64 panel workgroups x 256 rows
 SYEV_MAX_VEC = 64
+SPLIT_MIN_N = 1024   # below this the fused solve is cheaper than a 64-vector subspace iteration
+SPLIT_MAX_VEC = 40   # leading pairs a 64-vector block resolves (nm <= 40; beyond, the fused solve)
 
 
-def eigen_modes(ctx: Context, C, ns, nm, tol_CN, full_temporal, tm=None):
+def _eigen_method(world=1):
+    method = os.environ.get("PODS_EIGEN", "auto")
+    if method not in ("auto", "pods", "pods2", "torch", "split"):
+        raise ValueError("PODS_EIGEN must be auto, pods, pods2, torch or split")
+    return method
+
+
+def _subspace_ws(ctx, n):
+    from .subspace import Subspace
+    ws = getattr(ctx, "_subspace", None)
+    if ws is None or ws.n != n:
+        ws = ctx._subspace = Subspace(ctx, n, 64)
+    return ws
+
+
+def eigvals_full(ctx, C, ns, slot=0):
+    """All ns eigenvalues, descending (device tensor): the eigenvalues-only tridiagonalisation
+    (pods_eigvals_*, ns <= 4096) or the two-stage solver with no vectors (pods_syev2)."""
+    lib = ctx.lib
+    lam = torch.empty(ns, dtype=torch.float64, device=C.device)
+    if ns <= SYEV_MAX_N:
+        check(lib.pods_eigvals_begin(ctx.h, slot, ptr(C), ns), "pods_eigvals_begin")
+        rem = ctypes.c_int(0)
+        check(lib.pods_eigvals_advance(ctx.h, slot, 1 << 20, ctypes.byref(rem)), "pods_eigvals_advance")
+        check(lib.pods_eigvals_fetch(ctx.h, slot, ptr(lam)), "pods_eigvals_fetch")
+        return lam, lambda: check(lib.pods_eigvals_status(ctx.h, slot), "pods_eigvals")
+    check(lib.pods_syev2(ctx.h, ptr(C), ns, 0, ptr(lam), None), "pods_syev2")
+    return lam, lambda: check(lib.pods_syev2_status(ctx.h), "pods_syev2")
+
+
+class SpectrumQueue:
+    """The full spectrum (POD.eigenvalues.dat and the printed valid-mode count: PODFS.py:1309-1320,
+    :1339) of one correlation matrix per step, off the critical path of a multi-step run.
+
+    Nothing in a step consumes eigenvalues past lambda_{nm-1}, so the eigenvalues-only
+    tridiagonalisation of step s runs on rank s % world, spread over that rank's next steps in
+    units of one 512-column range (pods_eigvals_advance): every rank runs about units / world
+    units per step, so no rank carries the whole solve (33 ms at ns = 4096) in one step while
+    the others wait for it at the next all-reduce.  drain() runs what is left (inside a
+    caller's timed region) and results() returns {step: eigenvalues} for the steps this rank
+    owned.  ns <= 4096; beyond that each owner solves its step at once (pods_syev2, no vectors)."""
+
+    def __init__(self, ctx, ns, rank=0, world=1, max_slots=16):
+        self.ctx, self.ns, self.rank, self.world = ctx, ns, rank, world
+        self.units = (ns - 1) // 512 + 2
+        self.per_step = -(-self.units // max(world, 1))
+        self.max_slots = max_slots
+        self.pending = []      # [step, slot, remaining units, lam tensor]
+        self.finished = {}     # step -> (lam tensor, status check)
+        self.step_no = 0
+
+    def _slot(self):
+        used = {p[1] for p in self.pending}
+        for s in range(self.max_slots):
+            if s not in used:
+                return s
+        raise RuntimeError("SpectrumQueue: all %d slots busy" % self.max_slots)
+
+    def submit(self, C, timer=None):
+        tm = timer or (lambda name: _NullCtx())
+        s = self.step_no
+        self.step_no += 1
+        lib = self.ctx.lib
+        with tm("eig_full"):
+            budget = self.per_step
+            if s % self.world == self.rank:
+                if self.ns > SYEV_MAX_N:
+                    self.finished[s] = eigvals_full(self.ctx, C, self.ns)
+                    budget = 0
+                else:
+                    slot = self._slot()
+                    check(lib.pods_eigvals_begin(self.ctx.h, slot, ptr(C), self.ns), "pods_eigvals_begin")
+                    lam = torch.empty(self.ns, dtype=torch.float64, device=C.device)
+                    self.pending.append([s, slot, self.units - 1, lam])
+                    budget -= 1
+            self._advance(budget)
+
+    def _advance(self, budget):
+        lib = self.ctx.lib
+        rem = ctypes.c_int(0)
+        while budget > 0 and self.pending:
+            p = self.pending[0]
+            n = min(budget, p[2])
+            if n > 0:
+                check(lib.pods_eigvals_advance(self.ctx.h, p[1], n, ctypes.byref(rem)), "pods_eigvals_advance")
+                p[2] = rem.value
+                budget -= n
+            if p[2] == 0:
+                check(lib.pods_eigvals_fetch(self.ctx.h, p[1], ptr(p[3])), "pods_eigvals_fetch")
+                slot = p[1]
+                self.finished[p[0]] = (p[3], lambda slot=slot: check(lib.pods_eigvals_status(self.ctx.h, slot),
+                                                                     "pods_eigvals"))
+                self.pending.pop(0)
+
+    def drain(self):
+        self._advance(1 << 30)
+
+    def results(self):
+        """{step: eigenvalues (numpy, descending)} of the finished steps this rank owned."""
+        out = {}
+        for s, (lam, status) in sorted(self.finished.items()):
+            status()
+            out[s] = lam.cpu().numpy()
+        return out
+
+
+def eigen_modes(ctx: Context, C, ns, nm, tol_CN, full_temporal, tm=None, world=1):
+    """Eigensolve + sort + valid-mode count + temporal scaling (PODFS.py:1309-1325):
+    (lambda descending (numpy), num_valid, nm_trunc, T (ns x ncols device tensor))."""
+    return eigen_solve(ctx, C, ns, nm, tol_CN, full_temporal, tm, world)[:4]
+
+
+def eigen_solve(ctx: Context, C, ns, nm, tol_CN, full_temporal, tm=None, world=1, defer_full=False):
     """Eigensolve + sort + valid-mode count + temporal scaling (PODFS.py:1309-1325).
 
-    Returns (lambda descending (numpy), num_valid, nm_trunc, T (ns x ncols device tensor,
-    ncols = ns if full_temporal else max(nm_trunc, 1)))."""
+    Returns (lambda descending (numpy; None when defer_full), num_valid (None when deferred),
+    nm_trunc, T (ns x ncols device tensor, ncols = ns if full_temporal else max(nm_trunc, 1)),
+    the eigenvalues of T's columns (numpy, descending) that scale the modes).
+
+    Paths (PODS_EIGEN=auto):
+      fused  (one device, ns <= 4096): pods_syev -- the on-chip tridiagonalisation, all
+             eigenvalues, the nm leading vectors by twisted factorisation + back-transformation;
+      split  (several ranks, or PODS_EIGEN=split): the nm leading pairs by Chebyshev-filtered
+             subspace iteration on fp64 MFMA (podsgen.subspace, stage "eigh"), which is all the
+             step consumes; the full spectrum is computed apart (stage "eig_full": now, or by a
+             SpectrumQueue when defer_full);
+      pods2  (4096 < ns <= 16384 on one device): the two-stage pods_syev2."""
+    from .subspace import leading_eigenpairs
     tm = tm or (lambda name: _NullCtx())
     lib, dev = ctx.lib, C.device
-    method = os.environ.get("PODS_EIGEN", "auto")
-    if method not in ("auto", "pods", "pods2", "torch"):
-        raise ValueError("PODS_EIGEN must be auto, pods, pods2 or torch")
+    method = _eigen_method(world)
     nvec = max(min(nm, ns), 1) if nm >= 0 else ns
     fits = not full_temporal and nvec <= SYEV_MAX_VEC
-    use_pods = method in ("auto", "pods") and fits and ns <= SYEV_MAX_N
-    use_pods2 = fits and 3 <= ns <= SYEV2_MAX_N and (method == "pods2" or (method == "auto" and not use_pods))
+    split = (fits and nvec <= SPLIT_MAX_VEC and ns >= SPLIT_MIN_N and
+             (method == "split" or (method == "auto" and (world > 1 or defer_full))))
+    use_pods = not split and method in ("auto", "pods") and fits and ns <= SYEV_MAX_N
+    use_pods2 = not split and fits and 3 <= ns <= SYEV2_MAX_N and (method == "pods2" or
+                                                                     (method == "auto" and not use_pods))
     if method in ("pods", "pods2") and not (use_pods or use_pods2):
         raise ValueError("PODS_EIGEN=%s needs ns <= %d, nm <= %d and truncated temporal modes"
                          % (method, SYEV_MAX_N if method == "pods" else SYEV2_MAX_N, SYEV_MAX_VEC))
+    if split:
+        with tm("eigh"):
+            th, X, _info = leading_eigenpairs(ctx, C, nvec, m=64, ws=_subspace_ws(ctx, ns))
+        nv_top = num_valid_modes(th, ns, tol_CN)   # exact when < nvec, else a lower bound
+        nmt = nm if (0 <= nm <= nv_top) else nv_top
+        ncols = max(min(nmt, nvec), 1)
+        T = torch.empty((ns, ncols), dtype=torch.float64, device=dev)
+        v0 = ctypes.c_void_p(X.data_ptr() + (ns - 1) * 8)   # descending columns, see below
+        with tm("temporal"):
+            check(lib.pods_temporal_modes(ctx.h, v0, X.shape[1], -1, ptr(np.ascontiguousarray(th)),
+                                          min(nv_top, ncols), ncols, ptr(T)), "pods_temporal_modes")
+        if defer_full:
+            return None, None, nmt, T, th
+        with tm("eig_full"):
+            lam_t, status = eigvals_full(ctx, C, ns)
+            lam_desc = lam_t.cpu().numpy()
+            status()
+        return lam_desc, num_valid_modes(lam_desc, ns, tol_CN), nmt, T, th
     if use_pods or use_pods2:
         lam_t = torch.empty(ns, dtype=torch.float64, device=dev)
         Y = torch.empty((ns, nvec), dtype=torch.float64, device=dev)
         with tm("eigh"):
-            if use_pods:
-                check(lib.pods_syev(ctx.h, ptr(C), ns, nvec, ptr(lam_t), ptr(Y)), "pods_syev")
-                check(lib.pods_syev_status(ctx.h), "pods_syev")
-            else:  # two-stage (band reduction + bulge chasing) beyond the on-chip limit
-                check(lib.pods_syev2(ctx.h, ptr(C), ns, nvec, ptr(lam_t), ptr(Y)), "pods_syev2")
-                check(lib.pods_syev2_status(ctx.h), "pods_syev2")
-            lam_desc = lam_t.cpu().numpy()
+            try:
+                if use_pods:
+                    check(lib.pods_syev(ctx.h, ptr(C), ns, nvec, ptr(lam_t), ptr(Y)), "pods_syev")
+                    check(lib.pods_syev_status(ctx.h), "pods_syev")
+                else:  # two-stage (band reduction + bulge chasing) beyond the on-chip limit
+                    check(lib.pods_syev2(ctx.h, ptr(C), ns, nvec, ptr(lam_t), ptr(Y)), "pods_syev2")
+                    check(lib.pods_syev2_status(ctx.h), "pods_syev2")
+            except RuntimeError as exc:
+                # a persistent solver whose workgroups could not all be resident (another
+                # process on the device) refuses to launch or aborts its hand-off wait: solve
+                # with rocSOLVER on the same device instead of failing the POD
+                warnings.warn("podsgen: %s; falling back to torch.linalg.eigh" % exc)
+                use_pods = use_pods2 = False
+            else:
+                lam_desc = lam_t.cpu().numpy()
+    if use_pods or use_pods2:
         nvalid = num_valid_modes(lam_desc, ns, tol_CN)
         nmt = nm if (0 <= nm <= nvalid) else nvalid
         ncols = max(min(nmt, nvec), 1)
@@ -237,7 +391,7 @@ def eigen_modes(ctx: Context, C, ns, nm, tol_CN, full_temporal, tm=None):
         with tm("temporal"):
             check(lib.pods_temporal_modes(ctx.h, v0, nvec, -1, ptr(lam_desc), min(nvalid, ncols), ncols,
                                           ptr(T)), "pods_temporal_modes")
-        return lam_desc, nvalid, nmt, T
+        return lam_desc, nvalid, nmt, T, lam_desc[:ncols]
     with tm("eigh"):
         lam, V = torch.linalg.eigh(C)
         lam_desc = torch.flip(lam, dims=(0,)).cpu().numpy()
@@ -248,12 +402,16 @@ def eigen_modes(ctx: Context, C, ns, nm, tol_CN, full_temporal, tm=None):
     with tm("temporal"):
         check(lib.pods_temporal_modes(ctx.h, ptr(V), V.stride(0), V.stride(1), ptr(lam_desc),
                                       min(nvalid, ncols), ncols, ptr(T)), "pods_temporal_modes")
-    return lam_desc, nvalid, nmt, T
+    return lam_desc, nvalid, nmt, T, lam_desc[:ncols]
 
 
 def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=False,
-            keep_C=False, timer=None, on_temporal=None):
+            keep_C=False, timer=None, on_temporal=None, spectrum=None):
     """PODFS.POD (PODFS.py:1294-1393) with correct_for_cell_volumes='false'.
+
+    spectrum: a SpectrumQueue -- the eigenvalues past the nm leading ones are then computed by
+    it (spread over the following steps, energy/num_valid of the result are None); without one
+    the whole spectrum is computed in this call.
 
     on_temporal(T, nm_trunc), if given, is called on rank 0 as soon as the scaled temporal
     modes exist, before the spatial modes are enqueued (pipeline() starts the Fourier
@@ -275,19 +433,31 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
         with tm("allreduce"):
             allreduce_correlation(dist, C, ns, *device_triangle_ops(ctx))
     meta = torch.zeros(4, dtype=torch.int64, device=dev)
-    lam_desc_t = torch.empty(ns, dtype=torch.float64, device=dev)
-    T = None
+    T = lam_desc = nvalid = None
+    defer = spectrum is not None
     if rank == 0:
-        lam_desc, nvalid, nmt, T = eigen_modes(ctx, C, ns, nm, tol_CN, full_temporal, tm)
+        lam_desc, nvalid, nmt, T, lam_modes = eigen_solve(ctx, C, ns, nm, tol_CN, full_temporal, tm, world,
+                                                          defer_full=defer)
         if on_temporal is not None:
             on_temporal(T, nmt)
-        lam_desc_t.copy_(torch.from_numpy(lam_desc).to(dev))
-        meta[0], meta[1] = nvalid, nmt
+        meta[0] = -1 if nvalid is None else nvalid
+        meta[1] = nmt
+        meta[2] = 0 if lam_desc is None else 1
     if world > 1:
         dist.broadcast(meta, 0)
-        dist.broadcast(lam_desc_t, 0)
-        nvalid, nmt = int(meta[0]), int(meta[1])
-        lam_desc = lam_desc_t.cpu().numpy()
+        nv, nmt, have_full = int(meta[0]), int(meta[1]), bool(meta[2])
+        nvalid = None if nv < 0 else nv
+        lm = torch.empty(max(nmt, 1), dtype=torch.float64, device=dev)
+        if rank == 0:
+            lm.copy_(torch.from_numpy(np.ascontiguousarray(lam_modes[:max(nmt, 1)])).to(dev))
+        dist.broadcast(lm, 0)
+        lam_modes = lm.cpu().numpy()
+        if have_full:   # the drop-in path: every rank gets the spectrum (32 KB at ns = 4096)
+            lt = torch.empty(ns, dtype=torch.float64, device=dev)
+            if rank == 0:
+                lt.copy_(torch.from_numpy(lam_desc).to(dev))
+            dist.broadcast(lt, 0)
+            lam_desc = lt.cpu().numpy()
         Tn = torch.empty((ns, max(nmt, 1)), dtype=torch.float64, device=dev)
         if rank == 0:
             Tn.copy_(T[:, :max(nmt, 1)])
@@ -300,8 +470,10 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
     phi = torch.empty((snap.rowlen, max(nmt, 1)), dtype=torch.float64, device=dev)
     if nmt > 0:
         with tm("spatial"):
-            check(lib.pods_spatial_modes(ctx.h, ptr(Tsel), ldT, ptr(np.ascontiguousarray(lam_desc[:nmt])),
+            check(lib.pods_spatial_modes(ctx.h, ptr(Tsel), ldT, ptr(np.ascontiguousarray(lam_modes[:nmt])),
                                          nmt, ptr(phi)), "pods_spatial_modes")
+    if defer:  # the full spectrum, spread over this and the following steps (SpectrumQueue)
+        spectrum.submit(C, timer)
     return PODResult(energy=lam_desc, num_valid=nvalid, nm=nmt, mean=mean, T=T, phi=phi[:, :nmt],
                      C=C if keep_C else None)
 
@@ -466,8 +638,9 @@ class StageTimer:
         return out
 
 
-def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=None, gen=None):
-    """The whole hot path; returns (Generator, PODResult, FourierResult | None)."""
+def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=None, gen=None, spectrum=None):
+    """The whole hot path; returns (Generator, PODResult, FourierResult | None).
+    spectrum: a SpectrumQueue for multi-step runs (see run_pod)."""
     dist_, rank, world = _dist_info(dist)
     tm = timer or (lambda name: _NullCtx())
     gen = gen or Generator(setup, device=device, rank=rank, world=world)
@@ -479,7 +652,7 @@ def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=Non
         pending.append(launch_fourier(gen.ctx, T, nmt, setup.ns, setup.dt_eff, setup.et, timer=timer,
                                       side=True))
     pod = run_pod(snap, setup.nm, dist=dist_, full_temporal=full_temporal, timer=timer,
-                  on_temporal=start_fourier)
+                  on_temporal=start_fourier, spectrum=spectrum)
     fo = pending[0]() if pending else None
     return gen, pod, fo
 

@@ -136,3 +136,115 @@ def test_eigen_modes_paths_agree(ctx, monkeypatch):
     for k in range(nm):
         s = np.sign(np.dot(Ta[:, k], Tb[:, k]))
         assert np.max(np.abs(s * Ta[:, k] - Tb[:, k])) <= 1e-9 * np.max(np.abs(Tb[:, k])), k
+
+
+@pytest.mark.parametrize("n,m", [(1000, 64), (4096, 64), (777, 64), (16, 64), (8192, 64)])
+def test_cheb_step_kernel(ctx, n, m):
+    """pods_cheb_step: out = alpha C Y + beta Y + gamma Z on fp64 MFMA against torch, ragged n
+    included (k-chunks and row tiles past n read zeros)."""
+    from podsgen.subspace import Subspace
+    if m > n or n > 4096:
+        C = torch.randn(n, n, dtype=torch.float64, device="cuda")
+    else:
+        C = pod_like(n, seed=n)
+    Y = torch.randn(n, m, dtype=torch.float64, device="cuda")
+    Z = torch.randn(n, m, dtype=torch.float64, device="cuda")
+    out = torch.empty_like(Y)
+    ws = Subspace.__new__(Subspace)   # the kernel call only
+    ws.ctx, ws.lib, ws.n, ws.m = ctx, ctx.lib, n, m
+    ws.step(C, Y, Z, 0.75, -0.5, 0.25, out)
+    ref = 0.75 * (C @ Y) - 0.5 * Y + 0.25 * Z
+    assert float((out - ref).abs().max()) <= 1e-13 * float(ref.abs().max())
+    ws.step(C, Y, None, 1.0, 0.0, 0.0, out)
+    assert float((out - C @ Y).abs().max()) <= 1e-13 * float((C @ Y).abs().max())
+    a = out.clone()
+    ws.step(C, Y, None, 1.0, 0.0, 0.0, out)
+    assert torch.equal(a, out)   # deterministic reduction order
+
+
+@pytest.mark.parametrize("n,k", [(1024, 20), (2049, 20), (4096, 20), (3000, 40)])
+def test_leading_eigenpairs_vs_eigh(ctx, n, k):
+    """The subspace solver's k leading pairs: eigenvalues within 1e-12 lambda_0, residuals and
+    orthonormality within 1e-12, sign-aligned vectors within 1e-10 (gap rule)."""
+    from podsgen.subspace import leading_eigenpairs
+    C = pod_like(n, seed=n + 1)
+    th, X, info = leading_eigenpairs(ctx, C, k, m=64)
+    lr, Vr = torch.linalg.eigh(C)
+    lr = torch.flip(lr, (0,)).cpu().numpy()
+    Vr = torch.flip(Vr, (1,)).cpu().numpy()
+    assert np.max(np.abs(th - lr[:k])) <= 1e-12 * lr[0], info
+    Xh = X.cpu().numpy()
+    Ch = C.cpu().numpy()
+    assert np.max(np.linalg.norm(Ch @ Xh - Xh * th, axis=0)) <= 1e-12 * lr[0]
+    assert np.max(np.abs(Xh.T @ Xh - np.eye(k))) <= 1e-12
+    gl = np.abs(np.diff(lr)) / lr[0]
+    for j in range(k):
+        if min(gl[j], gl[j - 1] if j else np.inf) <= 1e-6:
+            continue
+        s = np.sign(np.dot(Xh[:, j], Vr[:, j]))
+        assert np.max(np.abs(s * Xh[:, j] - Vr[:, j])) <= 1e-10, (j, info)
+
+
+def test_eigen_split_path_matches_fused(ctx, monkeypatch):
+    """eigen_modes with PODS_EIGEN=split (leading pairs by subspace iteration + eigenvalues-only
+    tridiagonalisation) == the fused pods_syev: the same eigenvalues bit for bit (same
+    tridiagonalisation and bisection kernels), nm and num_valid, T within 1e-10."""
+    n, nm = 2500, 20
+    C = pod_like(n, seed=12)
+    E.load_snapshots(np.random.default_rng(0).standard_normal((48, n)), ctx=ctx)  # sets ns
+    monkeypatch.setenv("PODS_EIGEN", "pods")
+    la, nva, nma, Ta = E.eigen_modes(ctx, C, n, nm, 1e-15, False)
+    monkeypatch.setenv("PODS_EIGEN", "split")
+    lb, nvb, nmb, Tb = E.eigen_modes(ctx, C, n, nm, 1e-15, False)
+    assert np.array_equal(la, lb)
+    assert (nva, nma) == (nvb, nmb)
+    Ta, Tb = Ta.cpu().numpy(), Tb.cpu().numpy()
+    gl = np.abs(np.diff(la)) / la[0]
+    for j in range(nm):
+        if min(gl[j], gl[j - 1] if j else np.inf) <= 1e-6:
+            continue
+        s = np.sign(np.dot(Ta[:, j], Tb[:, j]))
+        assert np.max(np.abs(s * Ta[:, j] - Tb[:, j])) <= 1e-10 * np.max(np.abs(Ta[:, j])), j
+
+
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_spectrum_queue_spreads_and_matches(ctx, world):
+    """SpectrumQueue (rank 0's view of a `world`-rank run): the steps it owns are solved in
+    units spread over later steps and drained at the end; each spectrum equals pods_syev's
+    eigenvalues of the same matrix bit for bit."""
+    n = 2100
+    mats = [pod_like(n, seed=40 + i) for i in range(7)]
+    q = E.SpectrumQueue(ctx, n, rank=0, world=world)
+    for C in mats:
+        q.submit(C)
+    q.drain()
+    got = q.results()
+    assert sorted(got) == [s for s in range(len(mats)) if s % world == 0]
+    for s, lam in got.items():
+        ref, _ = solve(ctx, mats[s], 0)
+        assert np.array_equal(lam, ref), s
+
+
+@pytest.mark.parametrize("n", [64, 1000, 4096])
+def test_block_kernels(ctx, n):
+    """pods_gram, pods_cholqr (twice = orthonormal), pods_right_mul against torch."""
+    import ctypes
+    m = 64
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    g = torch.Generator(device="cpu").manual_seed(n)
+    Y = torch.randn(n, m, generator=g, dtype=torch.float64).cuda()
+    Z = torch.randn(n, m, generator=g, dtype=torch.float64).cuda()
+    G = torch.empty((m, m), dtype=torch.float64, device="cuda")
+    podsgen.check(ctx.lib.pods_gram(ctx.h, P(Y), P(Z), n, m, P(G)), "pods_gram")
+    ref = Y.T @ Z
+    assert float((G - ref).abs().max()) <= 1e-12 * float(ref.abs().max())
+    Q0, Q1 = torch.empty_like(Y), torch.empty_like(Y)
+    podsgen.check(ctx.lib.pods_cholqr(ctx.h, P(Y), n, m, P(Q0)), "pods_cholqr")
+    podsgen.check(ctx.lib.pods_cholqr(ctx.h, P(Q0), n, m, P(Q1)), "pods_cholqr")
+    assert float((Q1.T @ Q1 - torch.eye(m, dtype=torch.float64, device="cuda")).abs().max()) <= 1e-13
+    # same span: the projection of Y onto Q1 recovers Y
+    assert float((Q1 @ (Q1.T @ Y) - Y).abs().max()) <= 1e-11 * float(Y.abs().max())
+    M = torch.randn(m, m, generator=g, dtype=torch.float64).cuda()
+    out = torch.empty_like(Y)
+    podsgen.check(ctx.lib.pods_right_mul(ctx.h, P(Y), P(M), n, m, P(out)), "pods_right_mul")
+    assert float((out - Y @ M).abs().max()) <= 1e-13 * float((Y @ M).abs().max())

@@ -151,3 +151,29 @@ def test_c3_fourier_and_ranking(c3):
     # and the GPU ranking kernel equals the host restatement on the same c
     c_ind, c_count, FC = E.host_rank_and_count(fo.c, s.et)
     assert np.array_equal(fo.c_count, c_count) and np.array_equal(fo.c_ind, c_ind)
+
+
+@pytest.mark.timeout(600)
+def test_c3_split_eigensolve(c3, monkeypatch):
+    """The multi-rank eigensolve on the real C3 matrix: the 20 leading pairs by Chebyshev-filtered
+    subspace iteration (pods_cheb_step) and the eigenvalues-only tridiagonalisation -- the
+    eigenvalues are pods_syev's bit for bit, T within 1e-10 of eigh's scaled vectors (gap rule),
+    nm / num_valid the same."""
+    from podsgen import engine as E
+    pod, s = c3["pod"], c3["s"]
+    monkeypatch.setenv("PODS_EIGEN", "split")
+    lam, nvalid, nmt, T = E.eigen_modes(c3["gen"].ctx, pod.C, NS, s.nm, 1e-15, False)
+    assert np.array_equal(lam, pod.energy)
+    assert (nvalid, nmt) == (pod.num_valid, pod.nm)
+    lam_t, V = torch.linalg.eigh(pod.C)
+    lr = torch.flip(lam_t, (0,)).cpu().numpy()
+    Vd = torch.flip(V, (1,))[:, :nmt].cpu().numpy()
+    T = T.cpu().numpy()
+    for j in range(nmt):
+        v = Vd[:, j]
+        Tref = v * np.sqrt(lr[j] / (np.sum(v * v) / NS))
+        gap = min(abs(lr[j] - lr[j - 1]) if j else np.inf, abs(lr[j] - lr[j + 1]))
+        if gap <= 1e-6 * lr[0]:
+            continue
+        sg = np.sign(np.dot(T[:, j], Tref))
+        assert np.max(np.abs(sg * T[:, j] - Tref)) <= 1e-10 * np.max(np.abs(Tref)), j
