@@ -178,6 +178,10 @@ int pods_eigvals_advance(pods_ctx* ctx, int slot, int max_units, int* remaining)
 int pods_eigvals_fetch(pods_ctx* ctx, int slot, double* lam_desc_dev);
 int pods_eigvals_status(pods_ctx* ctx, int slot);
 
+/* Prepares C_dev (n x n row-major) for pods_cheb_step: a 64 x 64-tiled copy in the context
+ * (each tile contiguous, so the step streams C at the MFMA rate).  Call again whenever C_dev
+ * or its contents change; pods_cheb_step refuses a C it was not prepared for. */
+int pods_cheb_prepare(pods_ctx* ctx, const double* C_dev, int n);
 /* One step of the Chebyshev-filtered subspace iteration that finds the nm leading eigenpairs
  * (podsgen/subspace.py; PODFS.py:1309-1333 consumes only those): out = alpha (C Y) + beta Y +
  * gamma Z on fp64 MFMA, C_dev n x n row-major, Y_dev / Z_dev / out_dev n x m row-major with

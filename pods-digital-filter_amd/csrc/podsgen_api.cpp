@@ -267,7 +267,10 @@ struct pods_ctx {
   double dft_w_period = 0.0;
   std::vector<double> dft_w_t;
   std::vector<EigvalSlot> eslots;
-  DevBuf sub_part, sub_R, sub_cheb;  // subspace iteration: Gram partials, G / R^{-1}, split-K partials
+  DevBuf sub_part, sub_R, sub_cheb, sub_ct;  // subspace iteration: Gram partials, G / R^{-1}, split-K
+                                             // partials, the tiled copy of C
+  const double* sub_ct_src = nullptr;        // the C that sub_ct holds (pods_cheb_prepare)
+  int sub_ct_n = 0;
 };
 
 namespace {
@@ -368,6 +371,7 @@ int pods_destroy(pods_ctx* c) {
   release(c->sub_part);
   release(c->sub_R);
   release(c->sub_cheb);
+  release(c->sub_ct);
   for (EigvalSlot& sl : c->eslots)
     for (DevBuf* b : {&sl.wm, &sl.x, &sl.flags, &sl.det, &sl.v, &sl.cnt, &sl.lam}) release(*b);
   delete c;
@@ -696,13 +700,27 @@ int pods_copy_snapshots(pods_ctx* c, int i0, int i1, double* out_dev) {
   return PODS_OK;
 }
 
+int pods_cheb_prepare(pods_ctx* c, const double* C, int n) {
+  if (int e = check_ctx(c)) return e;
+  if (!C || n < 1) return fail(PODS_ERR_ARG, "pods_cheb_prepare: bad arguments");
+  PODS_HIP(hipSetDevice(c->device));
+  PODS_HIP(ensure(c->sub_ct, pods::cheb_tiled_doubles(n) * sizeof(double)));
+  PODS_HIP(pods::launch_tile_c(C, n, n, c->sub_ct.as<double>(), c->stream));
+  c->sub_ct_src = C;
+  c->sub_ct_n = n;
+  return PODS_OK;
+}
+
 int pods_cheb_step(pods_ctx* c, const double* C, int n, const double* Y, const double* Z, int m, double alpha,
                    double beta, double gamma, double* out) {
   if (int e = check_ctx(c)) return e;
   if (!C || !Y || !out || n < 1 || m != 64 || out == Y || (Z && out == Z))
     return fail(PODS_ERR_ARG, "pods_cheb_step: bad arguments (m = 64, out distinct)");
+  if (C != c->sub_ct_src || n != c->sub_ct_n)
+    return fail(PODS_ERR_STATE, "pods_cheb_step: C was not prepared (pods_cheb_prepare)");
   PODS_HIP(ensure(c->sub_cheb, (size_t)pods::cheb_splits(n) * n * 64 * sizeof(double)));
-  PODS_HIP(pods::launch_cheb_step(C, n, n, Y, Z, m, alpha, beta, gamma, c->sub_cheb.as<double>(), out, c->stream));
+  PODS_HIP(pods::launch_cheb_step(c->sub_ct.as<double>(), n, Y, Z, m, alpha, beta, gamma, c->sub_cheb.as<double>(),
+                                  out, c->stream));
   return PODS_OK;
 }
 

@@ -1006,33 +1006,45 @@ __global__ __launch_bounds__(256) void k_orth(const double* __restrict__ lam_des
   const int t = threadIdx.x;
   const double tnorm = fmax(fabs(bounds[0]), fabs(bounds[1]));
   int rk = 0;
-  for (int k = 1; k < nvec; ++k) {
+  auto dot = [&](int a, int b) {
+    double d = 0.0;
+    for (int i = t; i < n; i += 256) d = __builtin_fma(Z[(int64_t)i * ldz + a], Z[(int64_t)i * ldz + b], d);
+    d = wave_sum(d);
+    double* rb = red[rk++ & 1];
+    if ((t & 63) == 0) rb[t >> 6] = d;
+    __syncthreads();
+    return rb[0] + rb[1] + rb[2] + rb[3];
+  };
+  auto project_out = [&](int k) {  // MGS of column k against its cluster's earlier columns
     bool touched = false;
     for (int jj = 0; jj < k; ++jj) {
       if (fabs(lam_desc[jj] - lam_desc[k]) > 1e-3 * tnorm) continue;
-      double d = 0.0;
-      for (int i = t; i < n; i += 256) d = __builtin_fma(Z[(int64_t)i * ldz + jj], Z[(int64_t)i * ldz + k], d);
-      d = wave_sum(d);
-      double* rb = red[rk++ & 1];
-      if ((t & 63) == 0) rb[t >> 6] = d;
-      __syncthreads();
-      d = rb[0] + rb[1] + rb[2] + rb[3];
+      const double d = dot(jj, k);
       for (int i = t; i < n; i += 256)
         Z[(int64_t)i * ldz + k] = __builtin_fma(-d, Z[(int64_t)i * ldz + jj], Z[(int64_t)i * ldz + k]);
       __syncthreads();
       touched = true;
     }
-    if (touched) {
-      double s = 0.0;
-      for (int i = t; i < n; i += 256) s = __builtin_fma(Z[(int64_t)i * ldz + k], Z[(int64_t)i * ldz + k], s);
-      s = wave_sum(s);
-      double* rb = red[rk++ & 1];
-      if ((t & 63) == 0) rb[t >> 6] = s;
+    return touched;
+  };
+  for (int k = 1; k < nvec; ++k) {
+    if (!project_out(k)) continue;
+    double s = dot(k, k);
+    // A vector that (nearly) lies in the span of the cluster's earlier ones -- identical
+    // inverse-iteration results inside a degenerate cluster, e.g. a zero or diagonal block --
+    // is replaced by a unit vector orthogonalised against them (dstein's restart, as a
+    // deterministic choice), so the columns stay orthonormal instead of turning into NaN.
+    for (int attempt = 0; s < 1e-16 && attempt < n; ++attempt) {
+      const int p = (int)(((int64_t)k * 7919 + attempt * 104729) % n);
+      for (int i = t; i < n; i += 256) Z[(int64_t)i * ldz + k] = i == p ? 1.0 : 0.0;
       __syncthreads();
-      const double inv = 1.0 / sqrt(rb[0] + rb[1] + rb[2] + rb[3]);
-      for (int i = t; i < n; i += 256) Z[(int64_t)i * ldz + k] = Z[(int64_t)i * ldz + k] * inv;
-      __syncthreads();
+      project_out(k);
+      project_out(k);
+      s = dot(k, k);
     }
+    const double inv = 1.0 / sqrt(s);
+    for (int i = t; i < n; i += 256) Z[(int64_t)i * ldz + k] = Z[(int64_t)i * ldz + k] * inv;
+    __syncthreads();
   }
 }
 

@@ -18,12 +18,15 @@ hipError_t launch_dft_tab(const double* T, int ldT, int nm, int ns, const double
 hipError_t launch_gather_snapshots(const double* AT, int ns, int64_t rowlen, int i0, int i1, double* out,
                                    hipStream_t st);
 
-// out = alpha (C Y) + beta Y + gamma Z on fp64 MFMA; C n x n (ld ldc), Y/Z/out n x 64 row-major,
-// out distinct from Y and Z (podsgen_subspace.hip); part: cheb_splits(n) x n x 64 doubles of
+// out = alpha (C Y) + beta Y + gamma Z on fp64 MFMA from the tiled copy Ct of C (launch_tile_c:
+// cheb_tiled_doubles(n) doubles, 64 x 64 tiles, each contiguous); Y/Z/out n x 64 row-major, out
+// distinct from Y and Z (podsgen_subspace.hip); part: cheb_splits(n) x n x 64 doubles of
 // split-K partials (unused when cheb_splits(n) == 1)
 int cheb_splits(int n);
-hipError_t launch_cheb_step(const double* C, int64_t ldc, int n, const double* Y, const double* Z, int m,
-                            double alpha, double beta, double gamma, double* part, double* out, hipStream_t st);
+size_t cheb_tiled_doubles(int n);
+hipError_t launch_tile_c(const double* C, int64_t ldc, int n, double* Ct, hipStream_t st);
+hipError_t launch_cheb_step(const double* Ct, int n, const double* Y, const double* Z, int m, double alpha,
+                            double beta, double gamma, double* part, double* out, hipStream_t st);
 
 // small dense pieces of the subspace iteration, m = 64 (podsgen_subspace.hip):
 // G = Y^T Z (64 x 64) through gram_slices(n) row-slice partials in part (summed in order);

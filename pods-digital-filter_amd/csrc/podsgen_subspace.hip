@@ -1,23 +1,22 @@
-// One step of the Chebyshev-filtered subspace iteration for the leading POD modes
+// Kernels of the Chebyshev-filtered subspace iteration for the leading POD modes
 // (podsgen/subspace.py; the eigenpairs PODFS.py:1309-1333 consumes):
 //
-//   out = alpha * (C Y) + beta * Y + gamma * Z        C: n x n, Y, Z, out: n x m (row-major)
+//   k_cheb / k_cheb_sum   out = alpha (C Y) + beta Y + gamma Z on fp64 MFMA (v_mfma_f64_16x16x4),
+//                         C from a 64 x 64-tiled copy (k_tile_c), split-K partials summed in
+//                         order (deterministic), the filter's three-term recurrence fused into
+//                         the epilogue
+//   k_gram_mfma / _reduce 64 x 64 Gram matrices Y^T Z on fp64 MFMA
+//   k_chol_inv            one wave: Cholesky of the Gram and R^{-1} (Cholesky QR)
+//   k_right_mul           Y M for a 64 x 64 M (CholQR's Y R^{-1}, Rayleigh-Ritz rotations)
 //
-// on fp64 MFMA (v_mfma_f64_16x16x4_f64).  A workgroup owns 16 rows x 64 columns of out; its
-// 8 waves split the reduction over k into 8 contiguous ranges and their partial 16 x 64 tiles
-// are summed through LDS in wave order (deterministic), the epilogue fusing the three-term
-// recurrence.  Operand loads are 32-B vectors with no lane exchange: in MFMA sub-step s of a
-// 16-k chunk, lane group g = lane / 16 contributes k = 16 kc + 4 g + s (A and B use the same
-// k permutation, so the sum over the chunk is unchanged), and output column tile t holds the
-// columns 4 (lane % 16) + t -- so a lane's A operands are one double4 of its C row and its B
-// operands for all four tiles one double4 of a Y row.  The product is bandwidth/MFMA balanced
-// at m = 64 (16 flop per byte of C); C (134 MB at ns = 4096) stays in the Infinity Cache across
-// the filter's steps.
+// MFMA operand mapping (f64 16x16x4: A[l%16][l/16], B[l/16][l%16], D[l/16 + 4 r][l%16]): in
+// sub-step s of a 16-k block, lane group g = l/16 contributes k = 16 kb + 4 g + s (A and B use
+// the same k permutation, so a block's sum is unchanged), and column tile q holds columns
+// 4 (l%16) + q -- so a lane's operands are whole 32-B pairs of LDS slots, no lane exchange.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdint>
-#include <cstdlib>
 
 #include "podsgen_ext.h"
 
@@ -50,69 +49,121 @@ __device__ __forceinline__ f64x4 ld4(const double* p, int64_t base, int64_t off,
 // is loaded into registers while the current one is multiplied.
 // With KS > 1 each workgroup writes its partial tile and k_cheb_sum adds the KS partials in
 // order (deterministic) and applies the recurrence; with KS = 1 the epilogue is applied here.
-constexpr int CB_ROWS = 64;
-constexpr int CB_K = 64;                 // k per chunk
-constexpr int CB_CLD = CB_K + 4;         // LDS row stride of the C tile (doubles)
-__global__ __launch_bounds__(256) void k_cheb(const double* __restrict__ C, int64_t ldc, int n,
+constexpr int CB_ROWS = 64;  // rows per workgroup = tile edge
+constexpr int CB_K = 64;     // k per chunk = tile edge
+// LDS images in 16-byte slots, bank-conflict-free for the MFMA operand reads (ds_read_b128 lane
+// groups, checked exhaustively): C tile row r, k pair kk at r * 36 + r / 8 + kk; Y chunk row kr,
+// column pair cc at kr * 32 + kr / 4 + cc.  (Unpadded, the B reads of lane groups g and g + 1
+// hit the same banks: 2-way conflicts on every operand fetch.)
+__device__ __forceinline__ int cs_slot(int r, int kk) { return r * 36 + (r >> 3) + kk; }
+__device__ __forceinline__ int ys_slot(int kr, int cc) { return kr * 32 + (kr >> 2) + cc; }
+constexpr int CS_SLOTS = 64 * 36 + 8;
+constexpr int YS_SLOTS = 64 * 32 + 16;
+
+// C re-laid out once per matrix into 64 x 64 tiles, tile (rb, kb) contiguous (32 KB, rows of
+// 512 B), zero-padded to whole tiles: a workgroup's operand stream is then one contiguous
+// range.  In row-major C the same stream is 64 rows x 512 B per chunk, 32 KB apart: every
+// variant of the kernel on that layout ran at ~2 TB/s (65 us per step at ns = 4096).
+__global__ __launch_bounds__(256) void k_tile_c(const double* __restrict__ C, int64_t ldc, int n, int nt,
+                                                double* __restrict__ Ct) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;  // quad index in the tiled copy
+  const int64_t tile = q >> 10, w = q & 1023;
+  if (tile >= (int64_t)nt * nt) return;
+  const int rb = (int)(tile / nt), kb = (int)(tile % nt);
+  const int r = rb * 64 + (int)(w >> 4), k = kb * 64 + (int)(w & 15) * 4;
+  const f64x4 v = r < n ? ld4(C, (int64_t)r * ldc, k, n) : f64x4{0.0, 0.0, 0.0, 0.0};
+  reinterpret_cast<f64x4*>(Ct)[q] = v;
+}
+
+// Workgroup (256 threads) = 64 rows x 64 columns of out over one of KS ranges of k; wave w owns
+// rows 16 w .. 16 w + 15.  Each C element feeds exactly one MFMA k-step of 4 column tiles
+// (16 flop per byte of C): the kernel streams C at the fp64 MFMA rate, one 32 KB tile per
+// chunk staged through LDS with the 64 x 64 chunk of Y that all four waves share; the next
+// chunk is loaded into registers while the current one is multiplied.
+// With KS > 1 each workgroup writes its partial tile and k_cheb_sum adds the KS partials in
+// order (deterministic) and applies the recurrence; with KS = 1 the epilogue is applied here.
+__global__ __launch_bounds__(256) void k_cheb(const double* __restrict__ Ct, int nt, int n,
                                               const double* __restrict__ Y, const double* __restrict__ Z,
                                               double alpha, double beta, double gamma, int kper,
                                               double* __restrict__ part, double* __restrict__ out) {
-  __shared__ __attribute__((aligned(32))) double cs[CB_ROWS * CB_CLD];  // [row][k]
-  __shared__ f64x4 ys[CB_K * 16];                                        // [k][column quad]
+  __shared__ double2 cs[CS_SLOTS];  // C tile [row][k]
+  __shared__ double2 ys[YS_SLOTS];  // Y chunk [k][column]
   const int t = threadIdx.x, wave = t >> 6, l = t & 63;
   const int g = l >> 4, li = l & 15;
-  const int rb0 = blockIdx.x * CB_ROWS;
+  const int rb = blockIdx.x;
   const int ks = blockIdx.y;
-  const int nch = (n + CB_K - 1) / CB_K;
-  const int kc0 = ks * kper, kc1 = min(nch, kc0 + kper);
+  const int kc0 = ks * kper, kc1 = min(nt, kc0 + kper);
   const f64x4 zero4{0.0, 0.0, 0.0, 0.0};
-  // loader mapping: C tile 64 x 64 = 1024 quads, thread t loads quads t + 256 p (p < 4):
-  // row (t + 256 p) / 16, k quad (t % 16) -> 16 threads x 32 B = 512 B per row
-  // Y chunk 64 x 64 = 1024 quads, thread t loads quads t + 256 p: k row (t + 256 p) / 16, quad t % 16
+  const f64x4* Cq = reinterpret_cast<const f64x4*>(Ct) + (int64_t)rb * nt * 1024;
+  // loader: tile quad q = t + 256 p -> row q / 16, k quad q % 16; Y chunk quad q -> k row q / 16
   f64x4 cr[4], yr[4];
   auto load = [&](int kc) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int q = t + 256 * p;
-      const int rr = q >> 4, kq = (q & 15) * 4;
-      const int r = rb0 + rr, k = kc * CB_K + kq;
-      cr[p] = (kc < kc1 && r < n) ? ld4(C, (int64_t)r * ldc, k, n) : zero4;
-      const int kr = kc * CB_K + rr;
-      yr[p] = (kc < kc1 && kr < n) ? *reinterpret_cast<const f64x4*>(Y + (int64_t)kr * 64 + kq) : zero4;
+      cr[p] = kc < kc1 ? Cq[(int64_t)kc * 1024 + q] : zero4;
+      const int kr = kc * CB_K + (q >> 4);
+      yr[p] = (kc < kc1 && kr < n) ? *reinterpret_cast<const f64x4*>(Y + (int64_t)kr * 64 + (q & 15) * 4) : zero4;
     }
   };
   auto stage = [&]() {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int q = t + 256 * p;
-      const int rr = q >> 4, kq = (q & 15) * 4;
-      *reinterpret_cast<f64x4*>(&cs[rr * CB_CLD + kq]) = cr[p];
-      ys[q] = yr[p];
+      const int sc = cs_slot(q >> 4, (q & 15) * 2), sy = ys_slot(q >> 4, (q & 15) * 2);
+      cs[sc] = double2{cr[p][0], cr[p][1]};
+      cs[sc + 1] = double2{cr[p][2], cr[p][3]};
+      ys[sy] = double2{yr[p][0], yr[p][1]};
+      ys[sy + 1] = double2{yr[p][2], yr[p][3]};
     }
   };
   f64x4 acc[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q] = zero4;
-  const int arow = (wave * 16 + li) * CB_CLD;
+  const int arow = wave * 16 + li;
   load(kc0);
   for (int kc = kc0; kc < kc1; ++kc) {
     __syncthreads();  // the previous chunk's operands have been read
     stage();
     __syncthreads();
     load(kc + 1);     // in flight during this chunk's MFMAs
+    // operands of a 16-k block (A: 4 doubles, B: 4 x 4) are read from LDS one block ahead, so
+    // the 16 MFMAs of a block issue back to back in accumulator-rotating order (each
+    // accumulator every 4th MFMA: dependent f64 MFMAs two apart ran the loop at half rate)
+    {
+      double a[4], b[4][4], an[4], bn[4][4];
+      auto rd = [&](int kb, double* aa, double (*bb)[4]) {
+        const int sa = cs_slot(arow, (kb + 4 * g) / 2);
+        const double2 a0 = cs[sa], a1 = cs[sa + 1];
+        aa[0] = a0.x; aa[1] = a0.y; aa[2] = a1.x; aa[3] = a1.y;
 #pragma unroll
-    for (int kb = 0; kb < CB_K; kb += 16) {
-      const f64x4 a = *reinterpret_cast<const f64x4*>(&cs[arow + kb + 4 * g]);
+        for (int s = 0; s < 4; ++s) {
+          const int sb = ys_slot(kb + 4 * g + s, 2 * li);
+          const double2 b0 = ys[sb], b1 = ys[sb + 1];
+          bb[s][0] = b0.x; bb[s][1] = b0.y; bb[s][2] = b1.x; bb[s][3] = b1.y;
+        }
+      };
+      rd(0, a, b);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const f64x4 b = ys[(kb + 4 * g + s) * 16 + li];
+      for (int kb = 0; kb < CB_K; kb += 16) {
+        if (kb + 16 < CB_K) rd(kb + 16, an, bn);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[q], acc[q], 0, 0, 0);
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s][q], acc[q], 0, 0, 0);
+        if (kb + 16 < CB_K) {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            a[s] = an[s];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) b[s][q] = bn[s][q];
+          }
+        }
       }
     }
   }
   // D of column tile q: row g + 4 reg, column 4 li + q -> one double4 per (lane, reg)
-  const int r0 = rb0 + wave * 16;
+  const int r0 = rb * CB_ROWS + wave * 16;
 #pragma unroll
   for (int rg = 0; rg < 4; ++rg) {
     const int r = r0 + g + 4 * rg;
@@ -317,31 +368,42 @@ hipError_t launch_right_mul(const double* Y, const double* M, int n, int m, doub
 }
 
 int cheb_splits(int n) {
-  const int rb = (n + CB_ROWS - 1) / CB_ROWS;
-  const int nch = (n + CB_K - 1) / CB_K;
-  static const int target = std::getenv("PODS_CHEB_WG") ? std::atoi(std::getenv("PODS_CHEB_WG")) : 512;
-  int ks = std::max(1, std::min(32, (target + rb / 2) / rb));  // ~2 workgroups per CU
-  return std::max(1, std::min(ks, nch / 2));                 // >= 2 chunks per split
+  const int nt = (n + 63) / 64;
+  const int ks = std::max(1, std::min(32, (512 + nt / 2) / nt));  // ~2 workgroups per CU
+  return std::max(1, std::min(ks, nt / 2));                          // >= 2 chunks per split
 }
 
-hipError_t launch_cheb_step(const double* C, int64_t ldc, int n, const double* Y, const double* Z, int m,
-                            double alpha, double beta, double gamma, double* part, double* out, hipStream_t st) {
+size_t cheb_tiled_doubles(int n) {
+  const size_t nt = (size_t)(n + 63) / 64;
+  return nt * nt * 64 * 64;
+}
+
+hipError_t launch_tile_c(const double* C, int64_t ldc, int n, double* Ct, hipStream_t st) {
+  const int nt = (n + 63) / 64;
+  const int64_t quads = (int64_t)nt * nt * 1024;
+  hipLaunchKernelGGL(k_tile_c, dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, st, C, ldc, n, nt, Ct);
+  return hipGetLastError();
+}
+
+hipError_t launch_cheb_step(const double* Ct, int n, const double* Y, const double* Z, int m, double alpha,
+                            double beta, double gamma, double* part, double* out, hipStream_t st) {
   if (n <= 0 || m != 64) return hipErrorInvalidValue;
   if (!Z) {
     Z = Y;
     gamma = 0.0;
   }
+  const int nt = (n + 63) / 64;
   const int ks = cheb_splits(n);
-  const int nch = (n + CB_K - 1) / CB_K;
-  const int kper = (nch + ks - 1) / ks;
-  const int ksn = (nch + kper - 1) / kper;
-  const dim3 grid((unsigned)((n + CB_ROWS - 1) / CB_ROWS), (unsigned)ksn);
+  const int kper = (nt + ks - 1) / ks;
+  const int ksn = (nt + kper - 1) / kper;
+  const dim3 grid((unsigned)nt, (unsigned)ksn);
+  auto kern = k_cheb;
   if (ksn == 1) {
-    hipLaunchKernelGGL(k_cheb, grid, dim3(256), 0, st, C, ldc, n, Y, Z, alpha, beta, gamma, kper,
-                       (double*)nullptr, out);
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, Ct, nt, n, Y, Z, alpha, beta, gamma, kper, (double*)nullptr,
+                       out);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(k_cheb, grid, dim3(256), 0, st, C, ldc, n, Y, Z, alpha, beta, gamma, kper, part, out);
+  hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, Ct, nt, n, Y, Z, alpha, beta, gamma, kper, part, out);
   const int64_t nq = (int64_t)n * 16;
   hipLaunchKernelGGL(k_cheb_sum, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, part, ksn, nq, Y, Z, alpha,
                      beta, gamma, out);

@@ -1299,8 +1299,11 @@ __global__ __launch_bounds__(256) void k_band_invit(const double* __restrict__ b
     __syncthreads();
   }
   // ---- two solves from a pseudo-random start (dlarnv-like), one wave, register windows ---
+  // The start depends on k as well: members of an exactly degenerate cluster (a zero block,
+  // I + u u^T) then reach different vectors of the eigenspace, which k_orth orthonormalises
+  // (one start for all k gave identical vectors there, and the cluster collapsed).
   for (int e = t; e < n; e += 256) {
-    uint32_t hh = (uint32_t)e * 2654435761u ^ 0x9e3779b9u;
+    uint32_t hh = (uint32_t)e * 2654435761u ^ (0x9e3779b9u + (uint32_t)k * 0x85ebca6bu);
     hh ^= hh >> 15; hh *= 2246822519u; hh ^= hh >> 13; hh *= 3266489917u; hh ^= hh >> 16;
     x[e] = (double)hh * (2.0 / 4294967296.0) - 1.0;
   }

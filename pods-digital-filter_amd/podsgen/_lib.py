@@ -58,6 +58,7 @@ SIGNATURES = {
     "pods_syev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "pods_sytrd": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "pods_syev_status": (c_int, [c_void_p]),
+    "pods_cheb_prepare": (c_int, [c_void_p, c_void_p, c_int]),
     "pods_cheb_step": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_dbl, c_dbl, c_dbl,
                                c_void_p]),
     "pods_gram": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),

@@ -63,6 +63,10 @@ class Subspace:
         self._start = None
 
     # -- kernels (C-ABI) --------------------------------------------------------------------
+    def prepare(self, C):
+        """Tiled copy of C for the Chebyshev steps (once per matrix)."""
+        check(self.lib.pods_cheb_prepare(self.ctx.h, _p(C), self.n), "pods_cheb_prepare")
+
     def step(self, C, Y, Z, alpha, beta, gamma, out):
         check(self.lib.pods_cheb_step(self.ctx.h, _p(C), self.n, _p(Y), None if Z is None else _p(Z), self.m,
                                       float(alpha), float(beta), float(gamma), _p(out)), "pods_cheb_step")
@@ -122,6 +126,7 @@ def leading_eigenpairs(ctx, C, k, m=64, degree=12, chunks=3, warm=8, tol=3e-14, 
     if m != 64 or m > n or k > m:
         raise ValueError("leading_eigenpairs: m = 64 with k <= m <= n")
     ws = ws or Subspace(ctx, n, m)
+    ws.prepare(C)
     th, X, CX = ws.rayleigh_ritz(C, ws.start())
     gemms = 1
     if warm:

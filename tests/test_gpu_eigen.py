@@ -152,6 +152,7 @@ def test_cheb_step_kernel(ctx, n, m):
     out = torch.empty_like(Y)
     ws = Subspace.__new__(Subspace)   # the kernel call only
     ws.ctx, ws.lib, ws.n, ws.m = ctx, ctx.lib, n, m
+    ws.prepare(C)
     ws.step(C, Y, Z, 0.75, -0.5, 0.25, out)
     ref = 0.75 * (C @ Y) - 0.5 * Y + 0.25 * Z
     assert float((out - ref).abs().max()) <= 1e-13 * float(ref.abs().max())
@@ -160,6 +161,9 @@ def test_cheb_step_kernel(ctx, n, m):
     a = out.clone()
     ws.step(C, Y, None, 1.0, 0.0, 0.0, out)
     assert torch.equal(a, out)   # deterministic reduction order
+    C2 = C.clone()
+    with pytest.raises(RuntimeError):   # a matrix that was not prepared is refused
+        ws.step(C2, Y, None, 1.0, 0.0, 0.0, out)
 
 
 @pytest.mark.parametrize("n,k", [(1024, 20), (2049, 20), (4096, 20), (3000, 40)])

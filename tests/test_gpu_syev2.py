@@ -97,7 +97,7 @@ def test_syev2_structured(ctx, kind, n, nvec):
     C = _structured(kind, n, seed=n + nvec)
     lam, Y = solve2(ctx, C, min(nvec, n))
     if kind == "zero":
-        assert np.all(lam == 0.0)
+        assert np.all(np.abs(lam) <= 1e-290)   # bisection of T = 0 (the bracket floor)
         if nvec:
             assert np.max(np.abs(Y.T @ Y - np.eye(Y.shape[1]))) <= 1e-12
         return

@@ -19,6 +19,7 @@ def main(reps):
     C = torch.randn(n, n, dtype=torch.float64, device="cuda")
     C = (C + C.T).contiguous()
     ws = Subspace(ctx, n, 64)
+    ws.prepare(C)
     Y = torch.randn(n, 64, dtype=torch.float64, device="cuda")
     Z = torch.randn(n, 64, dtype=torch.float64, device="cuda")
     out = torch.empty_like(Y)
