@@ -85,8 +85,8 @@ FP64_MFMA_PEAK_TFLOPS = 78.6  # MI355X dense FP64 matrix (spec); measured 70-76 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--seed", type=int, default=12345)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -293,9 +293,17 @@ def main():
     # only its row slab, so no measured figure applies there
     traffic = load_traffic(args.config, ns, rank) if world == 1 else None
     num_valid = pod.num_valid
-    if spectrum is not None:   # from the last full spectrum this rank computed
+    if spectrum is not None:   # from the last full spectrum (whichever rank owned it)
         done = spectrum.results()
-        num_valid = E.num_valid_modes(done[max(done)], ns) if done else None
+        last = torch.zeros(2 * world, dtype=torch.float64, device="cuda")
+        if done:
+            last[2 * rank] = max(done) + 1
+            last[2 * rank + 1] = E.num_valid_modes(done[max(done)], ns)
+        if world > 1:
+            dist.all_reduce(last)
+        last = last.view(world, 2).cpu().numpy()
+        r = int(np.argmax(last[:, 0]))
+        num_valid = int(last[r, 1]) if last[r, 0] > 0 else None
     if world > 1:
         dist.barrier()
     if rank == 0:

@@ -237,21 +237,35 @@ class SpectrumQueue:
     :1339) of one correlation matrix per step, off the critical path of a multi-step run.
 
     Nothing in a step consumes eigenvalues past lambda_{nm-1}, so the eigenvalues-only
-    tridiagonalisation of step s runs on rank s % world, spread over that rank's next steps in
-    units of one 512-column range (pods_eigvals_advance): every rank runs about units / world
-    units per step, so no rank carries the whole solve (33 ms at ns = 4096) in one step while
-    the others wait for it at the next all-reduce.  drain() runs what is left (inside a
-    caller's timed region) and results() returns {step: eigenvalues} for the steps this rank
-    owned.  ns <= 4096; beyond that each owner solves its step at once (pods_syev2, no vectors)."""
+    tridiagonalisation of step s (pods_eigvals_*, 33 ms at ns = 4096) runs on an owner rank,
+    spread over that rank's following steps in units of one 512-column range (the bisection is
+    the last unit).  Owners rotate over ranks 1..world-1 from world 3 on (rank 0 carries the
+    leading-pair solve and the DFT), over all ranks below that.  Each owner runs units while it
+    has time credit: every step adds (total cost / owners), every unit spends its estimated
+    cost (UNIT_MS, measured at ns = 4096), so the per-step load evens out at the average.
+    drain() runs what is left (inside a caller's timed region); results() returns {step:
+    eigenvalues} for the steps this rank owned.  ns <= 4096; beyond that each owner solves its
+    step at once (pods_syev2, no vectors)."""
+
+    # per-unit time (ms) of k_trd column ranges 0..7 and the bisection at ns = 4096
+    # (profiles/r3/c3_kernel_stats.csv); used only to even out the per-step load
+    UNIT_MS = [7.8, 5.5, 4.6, 4.0, 3.0, 2.9, 2.5, 2.2, 1.6]
 
     def __init__(self, ctx, ns, rank=0, world=1, max_slots=16):
         self.ctx, self.ns, self.rank, self.world = ctx, ns, rank, world
         self.units = (ns - 1) // 512 + 2
-        self.per_step = -(-self.units // max(world, 1))
+        self.cost = (self.UNIT_MS if self.units == len(self.UNIT_MS)
+                     else [1.0] * self.units)
+        self.owners = list(range(1, world)) if world >= 3 else list(range(world))
+        self.budget = sum(self.cost) / len(self.owners)
+        self.credit = 0.0
         self.max_slots = max_slots
-        self.pending = []      # [step, slot, remaining units, lam tensor]
+        self.pending = []      # [step, slot, next unit, lam tensor]
         self.finished = {}     # step -> (lam tensor, status check)
         self.step_no = 0
+
+    def owner(self, step):
+        return self.owners[step % len(self.owners)]
 
     def _slot(self):
         used = {p[1] for p in self.pending}
@@ -266,38 +280,40 @@ class SpectrumQueue:
         self.step_no += 1
         lib = self.ctx.lib
         with tm("eig_full"):
-            budget = self.per_step
-            if s % self.world == self.rank:
+            if self.rank in self.owners:
+                self.credit += self.budget
+            if self.owner(s) == self.rank:
                 if self.ns > SYEV_MAX_N:
                     self.finished[s] = eigvals_full(self.ctx, C, self.ns)
-                    budget = 0
+                    self.credit = 0.0
                 else:
                     slot = self._slot()
                     check(lib.pods_eigvals_begin(self.ctx.h, slot, ptr(C), self.ns), "pods_eigvals_begin")
                     lam = torch.empty(self.ns, dtype=torch.float64, device=C.device)
-                    self.pending.append([s, slot, self.units - 1, lam])
-                    budget -= 1
-            self._advance(budget)
+                    self.pending.append([s, slot, 1, lam])
+                    self.credit -= self.cost[0]
+            self._advance()
 
-    def _advance(self, budget):
+    def _advance(self, drain=False):
         lib = self.ctx.lib
         rem = ctypes.c_int(0)
-        while budget > 0 and self.pending:
+        while self.pending and (drain or self.credit > 0.0):
             p = self.pending[0]
-            n = min(budget, p[2])
-            if n > 0:
-                check(lib.pods_eigvals_advance(self.ctx.h, p[1], n, ctypes.byref(rem)), "pods_eigvals_advance")
-                p[2] = rem.value
-                budget -= n
-            if p[2] == 0:
+            check(lib.pods_eigvals_advance(self.ctx.h, p[1], 1, ctypes.byref(rem)), "pods_eigvals_advance")
+            self.credit -= self.cost[min(p[2], len(self.cost) - 1)]
+            p[2] += 1
+            if rem.value == 0:
                 check(lib.pods_eigvals_fetch(self.ctx.h, p[1], ptr(p[3])), "pods_eigvals_fetch")
                 slot = p[1]
                 self.finished[p[0]] = (p[3], lambda slot=slot: check(lib.pods_eigvals_status(self.ctx.h, slot),
                                                                      "pods_eigvals"))
                 self.pending.pop(0)
+        if not self.pending:
+            self.credit = min(self.credit, self.budget)  # no banking of idle time
 
     def drain(self):
-        self._advance(1 << 30)
+        self._advance(drain=True)
+        self.credit = 0.0
 
     def results(self):
         """{step: eigenvalues (numpy, descending)} of the finished steps this rank owned."""
