@@ -195,10 +195,15 @@ int pods_cheb_step(pods_ctx* ctx, const double* C_dev, int n, const double* Y_de
  *   pods_gram       G_dev (m x m) = Y^T Z, m = 64 (row-slice partials summed in order)
  *   pods_cholqr     one Cholesky-QR pass: X = Y R^{-1} with R^T R = Y^T Y (m = 64); twice in a
  *                   row gives orthonormal columns to working precision (CholQR2)
- *   pods_right_mul  out = Y M for an m x m row-major M_dev (the Rayleigh-Ritz rotation) */
+ *   pods_right_mul  out = Y M for an m x m row-major M_dev (the Rayleigh-Ritz rotation)
+ *   pods_ritz_residual  E = CX - X H (H = X^T C X): the residual block of the Rayleigh-Ritz
+ *                   step, whose Gram E^T E gives every Ritz pair's residual norm
+ *                   ||C X v - theta X v|| = ||E v|| without cancellation */
 int pods_gram(pods_ctx* ctx, const double* Y_dev, const double* Z_dev, int n, int m, double* G_dev);
 int pods_cholqr(pods_ctx* ctx, const double* Y_dev, int n, int m, double* X_dev);
 int pods_right_mul(pods_ctx* ctx, const double* Y_dev, const double* M_dev, int n, int m, double* out_dev);
+int pods_ritz_residual(pods_ctx* ctx, const double* X_dev, const double* CX_dev, const double* H_dev, int n, int m,
+                       double* E_dev);
 
 /* Two-stage eigensolver for correlation matrices beyond pods_syev's on-chip limit (BASELINE
  * configs 4/5, PODFS.py:1309-1310 at ns = 8192, 16384): dense -> band (bandwidth 32, fp64 MFMA

@@ -741,14 +741,22 @@ int pods_cholqr(pods_ctx* c, const double* Y, int n, int m, double* X) {
   double* Rinv = G + m * m;
   PODS_HIP(pods::launch_gram(Y, Y, n, c->sub_part.as<double>(), G, c->stream));
   PODS_HIP(pods::launch_chol_inv(G, Rinv, c->stream));
-  PODS_HIP(pods::launch_right_mul(Y, Rinv, n, m, X, c->stream));
+  PODS_HIP(pods::launch_right_mul(Y, Rinv, nullptr, n, m, X, c->stream));
   return PODS_OK;
 }
 
 int pods_right_mul(pods_ctx* c, const double* Y, const double* M, int n, int m, double* out) {
   if (int e = check_ctx(c)) return e;
   if (!Y || !M || !out || out == Y || n < 1 || m < 16 || m % 16) return fail(PODS_ERR_ARG, "pods_right_mul: bad arguments");
-  PODS_HIP(pods::launch_right_mul(Y, M, n, m, out, c->stream));
+  PODS_HIP(pods::launch_right_mul(Y, M, nullptr, n, m, out, c->stream));
+  return PODS_OK;
+}
+
+int pods_ritz_residual(pods_ctx* c, const double* X, const double* CX, const double* H, int n, int m, double* E) {
+  if (int e = check_ctx(c)) return e;
+  if (!X || !CX || !H || !E || E == X || E == CX || n < 1 || m < 16 || m % 16)
+    return fail(PODS_ERR_ARG, "pods_ritz_residual: bad arguments");
+  PODS_HIP(pods::launch_right_mul(X, H, CX, n, m, E, c->stream));
   return PODS_OK;
 }
 

@@ -35,6 +35,8 @@ hipError_t launch_cheb_step(const double* Ct, int n, const double* Y, const doub
 int gram_slices(int n);
 hipError_t launch_gram(const double* Y, const double* Z, int n, double* part, double* G, hipStream_t st);
 hipError_t launch_chol_inv(const double* G, double* Rinv, hipStream_t st);
-hipError_t launch_right_mul(const double* Y, const double* M, int n, int m, double* out, hipStream_t st);
+// out = Y M, or Z - Y M when Z is not null
+hipError_t launch_right_mul(const double* Y, const double* M, const double* Z, int n, int m, double* out,
+                            hipStream_t st);
 
 }  // namespace pods

@@ -7,7 +7,8 @@
 //                         the epilogue
 //   k_gram_mfma / _reduce 64 x 64 Gram matrices Y^T Z on fp64 MFMA
 //   k_chol_inv            one wave: Cholesky of the Gram and R^{-1} (Cholesky QR)
-//   k_right_mul           Y M for a 64 x 64 M (CholQR's Y R^{-1}, Rayleigh-Ritz rotations)
+//   k_right_mul           Y M or Z - Y M for a 64 x 64 M (CholQR's Y R^{-1}, Rayleigh-Ritz
+//                         rotations and residual blocks)
 //
 // MFMA operand mapping (f64 16x16x4: A[l%16][l/16], B[l/16][l%16], D[l/16 + 4 r][l%16]): in
 // sub-step s of a 16-k block, lane group g = l/16 contributes k = 16 kb + 4 g + s (A and B use
@@ -82,6 +83,8 @@ __global__ __launch_bounds__(256) void k_tile_c(const double* __restrict__ C, in
 // chunk is loaded into registers while the current one is multiplied.
 // With KS > 1 each workgroup writes its partial tile and k_cheb_sum adds the KS partials in
 // order (deterministic) and applies the recurrence; with KS = 1 the epilogue is applied here.
+// (Loading the C operand straight into the MFMA registers from a copy laid out in operand
+// order -- only Y through LDS -- measured the same: 57.8 vs 56.2 us per step with the sum.)
 __global__ __launch_bounds__(256) void k_cheb(const double* __restrict__ Ct, int nt, int n,
                                               const double* __restrict__ Y, const double* __restrict__ Z,
                                               double alpha, double beta, double gamma, int kper,
@@ -261,63 +264,80 @@ __global__ __launch_bounds__(256) void k_gram_mfma(const double* __restrict__ Y,
   }
 }
 
-// G = the partials summed in workgroup order (deterministic)
-__global__ __launch_bounds__(256) void k_gram_reduce(const double* __restrict__ part, int np, int m,
+// G = the partials summed in workgroup order (deterministic); all NP loads of a thread are
+// issued before the first add (a rolled load-add loop waited one L2 round trip per partial)
+template <int NP>
+__global__ __launch_bounds__(256) void k_gram_reduce(const double* __restrict__ part, int m,
                                                      double* __restrict__ G) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= m * m) return;
+  double v[NP];
+#pragma unroll
+  for (int w = 0; w < NP; ++w) v[w] = part[(int64_t)w * m * m + e];
   double s = 0.0;
-  for (int w = 0; w < np; ++w) s += part[(int64_t)w * m * m + e];
+#pragma unroll
+  for (int w = 0; w < NP; ++w) s += v[w];
   G[e] = s;
 }
 
+__device__ __forceinline__ double rdlane(double x, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(x), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), lane);
+  return __hiloint2double(hi, lo);
+}
+
 // One wave: G (64 x 64, symmetrised) = L L^T; Rinv = L^{-T} (upper triangular, row-major),
-// so that X = Y Rinv has X^T X = I for G = Y^T Y.  Lane i holds row i of G / L in registers;
-// the column of L just formed is broadcast through LDS.  A non-positive pivot gives NaN.
+// so that X = Y Rinv has X^T X = I for G = Y^T Y.  A non-positive pivot gives NaN.
+// Lane i holds row i of G (the factorisation's trailing rows) and column i of Z = L^{-1}
+// (forward substitution) in registers.  Step j takes the pivot from lane j (readlane), forms
+// column j of L, broadcasts it through LDS, and applies it to BOTH: the trailing update
+// g_ik -= l_ij l_kj and the substitution s_k -= l_kj z_j (k > j), whose z_j = s_j / l_jj is
+// final at step j.  (Factorisation, then a separate back substitution: 74 us; fused: the
+// substitution rides on the factorisation's column loads, tools/chol_bench.hip.)
 __global__ __launch_bounds__(64) void k_chol_inv(const double* __restrict__ G, double* __restrict__ Rinv) {
-  __shared__ double col[64];
-  __shared__ double Ls[64][65];
+  __shared__ double col[2][64];
+  __shared__ double Zs[64][65];   // Zs[t][c] = Z[c][t] = Rinv[t][c]
   const int i = threadIdx.x;
-  double gr[64];
+  double gr[64], sv[64];
 #pragma unroll
-  for (int k = 0; k < 64; ++k) gr[k] = 0.5 * (G[i * 64 + k] + G[k * 64 + i]);
+  for (int k = 0; k < 64; ++k) {
+    gr[k] = 0.5 * (G[i * 64 + k] + G[k * 64 + i]);
+    sv[k] = k == i ? 1.0 : 0.0;
+  }
 #pragma unroll
   for (int j = 0; j < 64; ++j) {
-    const double d = __shfl(gr[j], j);
+    const double d = rdlane(gr[j], j);
     const double ljj = d > 0.0 ? sqrt(d) : __builtin_nan("");
-    const double lij = i == j ? ljj : gr[j] / ljj;
-    gr[j] = i >= j ? lij : 0.0;
-    col[i] = i > j ? lij : 0.0;
+    const double r = 1.0 / ljj;
+    const double lij = gr[j] * r;   // lanes i > j: L[i][j] (other lanes' values are never read)
+    const double zj = sv[j] * r;    // Z[j][i]
+    Zs[i][j] = zj;
+    col[j & 1][i] = lij;
+    // the fences keep each step's column reads after its column write (and out of the
+    // previous steps: hoisted, they take the kernel past 256 VGPRs)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-    for (int k = j + 1; k < 64; ++k) gr[k] = fma(-lij, col[k], gr[k]);
+    for (int k = j + 1; k < 64; ++k) {
+      const double lk = col[j & 1][k];
+      gr[k] = fma(-lij, lk, gr[k]);
+      sv[k] = fma(-zj, lk, sv[k]);
+    }
     __builtin_amdgcn_wave_barrier();
   }
-#pragma unroll
-  for (int k = 0; k < 64; ++k) Ls[i][k] = gr[k];
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // lane c: column c of L^{-T} = R^{-1} (R = L^T): back substitution x_t for t = c .. 0,
-  // x_c = 1 / R[c][c], x_t = -(sum_{k = t+1..c} R[t][k] x_k) / R[t][t], R[t][k] = L[k][t]
-  const int c = i;
-  double x[64];
 #pragma unroll
-  for (int t = 63; t >= 0; --t) {
-    double s = t == c ? 1.0 : 0.0;
-#pragma unroll
-    for (int k = t + 1; k < 64; ++k) s = k <= c ? fma(-Ls[k][t], x[k], s) : s;
-    x[t] = t <= c ? s / Ls[t][t] : 0.0;
-  }
-#pragma unroll
-  for (int t = 0; t < 64; ++t) Rinv[t * 64 + c] = x[t];
+  for (int t = 0; t < 64; ++t) Rinv[t * 64 + i] = Zs[t][i];
 }
 
-// out = Y M (M m x m row-major); 16 rows per workgroup, a thread per (row, m/16 columns)
+// out = Y M (M m x m row-major), or Z - Y M with Z; 16 rows per workgroup, a thread per
+// (row, m/16 columns)
 __global__ __launch_bounds__(256) void k_right_mul(const double* __restrict__ Y, const double* __restrict__ Mx,
-                                                   int n, int m, double* __restrict__ out) {
+                                                   const double* __restrict__ Z, int n, int m,
+                                                   double* __restrict__ out) {
   extern __shared__ double sh[];
   double* Ms = sh;          // m x m
   double* ys = sh + m * m;  // 16 x m
@@ -337,7 +357,8 @@ __global__ __launch_bounds__(256) void k_right_mul(const double* __restrict__ Y,
       s0 = fma(ys[rr * m + k], Ms[k * m + c], s0);
       s1 = fma(ys[rr * m + k + 1], Ms[(k + 1) * m + c], s1);
     }
-    out[(int64_t)r * m + c] = s0 + s1;
+    const int64_t o = (int64_t)r * m + c;
+    out[o] = Z ? Z[o] - (s0 + s1) : s0 + s1;
   }
 }
 
@@ -348,7 +369,7 @@ int gram_slices(int n) { return GR_WG; }
 hipError_t launch_gram(const double* Y, const double* Z, int n, double* part, double* G, hipStream_t st) {
   const int rows_per = ((n + GR_WG - 1) / GR_WG + 15) / 16 * 16;
   hipLaunchKernelGGL(k_gram_mfma, dim3(GR_WG), dim3(256), 0, st, Y, Z, n, rows_per, part);
-  hipLaunchKernelGGL(k_gram_reduce, dim3(16), dim3(256), 0, st, part, GR_WG, 64, G);
+  hipLaunchKernelGGL(k_gram_reduce<GR_WG>, dim3(16), dim3(256), 0, st, part, 64, G);
   return hipGetLastError();
 }
 
@@ -357,13 +378,14 @@ hipError_t launch_chol_inv(const double* G, double* Rinv, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_right_mul(const double* Y, const double* M, int n, int m, double* out, hipStream_t st) {
+hipError_t launch_right_mul(const double* Y, const double* M, const double* Z, int n, int m, double* out,
+                            hipStream_t st) {
   if (m % 16) return hipErrorInvalidValue;
   const size_t lds = (size_t)(m * m + 16 * m) * sizeof(double);
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_right_mul),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_right_mul, dim3((unsigned)((n + 15) / 16)), dim3(256), lds, st, Y, M, n, m, out);
+  hipLaunchKernelGGL(k_right_mul, dim3((unsigned)((n + 15) / 16)), dim3(256), lds, st, Y, M, Z, n, m, out);
   return hipGetLastError();
 }
 

@@ -64,6 +64,7 @@ SIGNATURES = {
     "pods_gram": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "pods_cholqr": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "pods_right_mul": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
+    "pods_ritz_residual": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "pods_eigvals_begin": (c_int, [c_void_p, c_int, c_void_p, c_int]),
     "pods_eigvals_advance": (c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_int)]),
     "pods_eigvals_fetch": (c_int, [c_void_p, c_int, c_void_p]),

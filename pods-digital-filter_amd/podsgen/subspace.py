@@ -5,18 +5,25 @@ PODFS.py:1309-1333 consumes only lambda_0..lambda_{nm-1} and the nm leading eige
 count only (:1312-1320, :1339), and are computed apart (pods_eigvals_*).  This module finds the
 leading block by Chebyshev-filtered subspace iteration (Zhou & Saad) on C itself.  Every filter
 step is one call of pods_cheb_step: out = alpha (C Y) + beta Y + gamma Z on fp64 MFMA (the
-three-term recurrence fused into the GEMM's epilogue).  Between filter chunks the block is
-re-orthonormalised by Cholesky QR (twice); a Rayleigh-Ritz step, whose m x m eigenproblem is
-solved on the host, closes each round and measures the residuals.
+three-term recurrence fused into the GEMM's epilogue).  The block is re-conditioned by one
+Cholesky-QR pass between filter chunks and orthonormalised by two before a Rayleigh-Ritz step.
 
-    X0   = the m lowest-frequency Fourier vectors, orthonormalised
-    round: repeat `chunks` times: Y = T_d((C - c I) / e) X (damps [lo, cut]); X = orth(Y)
-           H = X^T C X; H V = V Theta; X = X V;  stop when max_j ||C x_j - theta_j x_j||
-           <= tol * theta_0 over the k wanted pairs
+    X0   = cos / sin of the m/2 lowest non-zero frequencies, orthonormalised
+    RR   : H = X^T C X, E = C X - X H, F = E^T E (device); eigh(H) = V Theta (host, 64 x 64);
+           residual of pair j = sqrt(v_j^T F v_j) / theta_0 (no cancellation: E is the
+           residual block itself) -- one host round trip per Rayleigh-Ritz step
+    warm : a degree-20 filter on the interval the start's Rayleigh quotients give (no
+           eigensolve), then RR (places the damped interval's edge near lambda_{m-5})
+    round: d = the filter degree that takes the largest residual of the k wanted pairs to
+           tol at the convergence rate per degree (first planned round: 0.8 x the Chebyshev
+           rate of theta_{k-1} against the damped interval [lo, theta_{m-1}]; later: the rate
+           the previous round achieved), in chunks whose condition growth stays below ~1e6;
+           then RR and the residual check
+    end  : X V[:, :k]
 
 At ns = 4096 (BASELINE config 3) the top of the POD spectrum is flat (lambda_19 / lambda_63
-= 1.10) and one filter degree gains a factor ~1.85 on mode 19 with a 64-vector block; ~70
-degrees take the residual to ~1e-14 lambda_0 (tools/subspace_probe.py, profiles/r3/).
+= 1.10) and one filter degree gains ~0.5 nat on mode 19 with a 64-vector block; ~60 degrees
+take the residual to ~1e-14 lambda_0 (tools/topk_probe.py, profiles/r3/).
 """
 import ctypes
 
@@ -31,8 +38,11 @@ except Exception:  # pragma: no cover
 
 
 def fourier_start(n, m, device):
+    """cos / sin of the m/2 lowest non-zero frequencies over the n snapshots.  No constant
+    vector: the snapshots are centred (main :1492-1495), so C 1 = 0 and it would only place
+    the damped interval's edge at 0."""
     t = torch.arange(n, dtype=torch.float64, device=device) * (2.0 * np.pi / n)
-    cols = [torch.ones(n, dtype=torch.float64, device=device)]
+    cols = []
     f = 1
     while len(cols) < m:
         cols.append(torch.cos(f * t))
@@ -48,7 +58,7 @@ def _p(t):
 
 class Subspace:
     """Workspace of the iteration on one context: named n x m blocks (F*: the filter's three
-    rotating terms, Q*: Cholesky QR, R*: Rayleigh-Ritz) and the m x m Gram / rotation."""
+    rotating terms, Q*: Cholesky QR, R*: Rayleigh-Ritz) and the m x m Gram matrices."""
 
     def __init__(self, ctx, n, m=64):
         if m != 64:
@@ -58,7 +68,7 @@ class Subspace:
         mk = lambda: torch.empty((n, m), dtype=torch.float64, device=dev)  # noqa: E731
         self.F = [mk(), mk(), mk()]
         self.Q0, self.Q1, self.R0, self.R1, self.R2 = mk(), mk(), mk(), mk(), mk()
-        self.G = torch.empty((m, m), dtype=torch.float64, device=dev)
+        self.HF = torch.empty((2, m, m), dtype=torch.float64, device=dev)   # H and F of one RR
         self.V = torch.empty((m, m), dtype=torch.float64, device=dev)
         self._start = None
 
@@ -72,16 +82,20 @@ class Subspace:
                                       float(alpha), float(beta), float(gamma), _p(out)), "pods_cheb_step")
         return out
 
+    def cholqr(self, Y, out):
+        """One Cholesky-QR pass: out = Y R^{-1}, R^T R = Y^T Y."""
+        check(self.lib.pods_cholqr(self.ctx.h, _p(Y), self.n, self.m, _p(out)), "pods_cholqr")
+        return out
+
     def cholqr2(self, Y):
         """Orthonormal basis of span(Y) by two Cholesky-QR passes: Y -> Q0 -> Q1."""
-        check(self.lib.pods_cholqr(self.ctx.h, _p(Y), self.n, self.m, _p(self.Q0)), "pods_cholqr")
-        check(self.lib.pods_cholqr(self.ctx.h, _p(self.Q0), self.n, self.m, _p(self.Q1)), "pods_cholqr")
-        return self.Q1
+        return self.cholqr(self.cholqr(Y, self.Q0), self.Q1)
 
     def start(self):
-        """The m lowest-frequency Fourier vectors, orthonormalised (cached per workspace)."""
+        """The m lowest-frequency Fourier vectors, orthonormalised (a constant basis, cached per
+        workspace)."""
         if self._start is None:
-            X = fourier_start(self.n, self.m, self.G.device)
+            X = fourier_start(self.n, self.m, self.HF.device)
             self._start = self.cholqr2(X).clone()
         return self._start
 
@@ -100,54 +114,108 @@ class Subspace:
             sigma = sn
         return Y
 
-    def rayleigh_ritz(self, C, X):
-        """Ritz values (host, descending), Ritz vectors R1 and C R1 = R2 of span(X)."""
+    def ritz(self, C, X, k):
+        """Rayleigh-Ritz on span(X), X orthonormal and not R0/R1: Ritz values (descending), the
+        rotation V (host, m x m) and the residual norms / theta_0 of the k leading pairs."""
+        lib, h, n, m = self.lib, self.ctx.h, self.n, self.m
         CX = self.step(C, X, None, 1.0, 0.0, 0.0, self.R0)
-        check(self.lib.pods_gram(self.ctx.h, _p(X), _p(CX), self.n, self.m, _p(self.G)), "pods_gram")
-        H = self.G.cpu().numpy()
-        th, V = np.linalg.eigh(0.5 * (H + H.T))
+        H, F = self.HF[0], self.HF[1]
+        check(lib.pods_gram(h, _p(X), _p(CX), n, m, _p(H)), "pods_gram")
+        check(lib.pods_ritz_residual(h, _p(X), _p(CX), _p(H), n, m, _p(self.R1)), "pods_ritz_residual")
+        check(lib.pods_gram(h, _p(self.R1), _p(self.R1), n, m, _p(F)), "pods_gram")
+        HF = self.HF.cpu().numpy()
+        Hh, Fh = HF[0], HF[1]
+        th, V = np.linalg.eigh(0.5 * (Hh + Hh.T))
         th, V = th[::-1].copy(), np.ascontiguousarray(V[:, ::-1])
+        Vk = V[:, :k]
+        r2 = np.einsum("ij,ij->j", Vk, (0.5 * (Fh + Fh.T)) @ Vk)
+        res = np.sqrt(np.maximum(r2, 0.0)) / th[0]
+        return th, V, res
+
+    def quotients(self, C, X):
+        """Rayleigh quotients x_j^T C x_j of the columns of an orthonormal X (host, descending):
+        the damped interval of the first filter, without an eigensolve."""
+        CX = self.step(C, X, None, 1.0, 0.0, 0.0, self.R0)
+        H = self.HF[0]
+        check(self.lib.pods_gram(self.ctx.h, _p(X), _p(CX), self.n, self.m, _p(H)), "pods_gram")
+        return np.sort(torch.diagonal(H).cpu().numpy())[::-1].copy()
+
+    def rotate(self, X, V):
+        """X V (device), V a host m x m rotation; the result lives in R2."""
         self.V.copy_(torch.from_numpy(V))
-        check(self.lib.pods_right_mul(self.ctx.h, _p(X), _p(self.V), self.n, self.m, _p(self.R1)), "pods_right_mul")
-        check(self.lib.pods_right_mul(self.ctx.h, _p(CX), _p(self.V), self.n, self.m, _p(self.R2)),
+        check(self.lib.pods_right_mul(self.ctx.h, _p(X), _p(self.V), self.n, self.m, _p(self.R2)),
               "pods_right_mul")
-        return th, self.R1, self.R2
+        return self.R2
 
 
-def leading_eigenpairs(ctx, C, k, m=64, degree=12, chunks=3, warm=8, tol=3e-14, max_rounds=4, ws=None):
+def _chebyshev_rate(x):
+    """Growth per degree of T_d at x >= 1 (0 inside the damped interval)."""
+    return float(np.arccosh(x)) if x > 1.0 else 0.0
+
+
+def leading_eigenpairs(ctx, C, k, m=64, tol=3e-14, max_degree=400, warm=20, rate_factor=0.85, margin=1.05,
+                      cut_index=None, schedule=None, ws=None):
     """The k largest eigenpairs of the symmetric positive semi-definite device matrix C.
 
-    A Rayleigh-Ritz step on the Fourier start, one `warm`-degree filter and a second
-    Rayleigh-Ritz place the damping interval's upper edge (cut = the smallest Ritz value of
-    the block, near lambda_m); then rounds of `chunks` filters of `degree` (CholQR2 between
-    them, no host round trip) each closed by a Rayleigh-Ritz step and the residual check.
-    Returns (theta (k,) numpy descending, X (n, k) device tensor, orthonormal columns, info)."""
+    The first round is a fixed `warm`-degree filter: the Fourier start's Ritz values sit far
+    below the spectrum's (theta_59 ~ lambda_263 at C3), so the damped interval they give is too
+    short to plan with.
+
+    Returns (theta (k,) numpy descending, X (n, k) device tensor with orthonormal columns,
+    info: rounds, gemms, filter degree, final max residual / theta_0, the residual history)."""
     n = C.shape[0]
-    if m != 64 or m > n or k > m:
-        raise ValueError("leading_eigenpairs: m = 64 with k <= m <= n")
+    if m != 64 or m > n or k > m or k < 1:
+        raise ValueError("leading_eigenpairs: m = 64 with 1 <= k <= m <= n")
     ws = ws or Subspace(ctx, n, m)
     ws.prepare(C)
-    th, X, CX = ws.rayleigh_ritz(C, ws.start())
-    gemms = 1
-    if warm:
-        cut, top = float(th[-1]), float(th[0])
-        X = ws.cholqr2(ws.filter(C, X, warm, -1e-3 * cut, cut, top))
-        th, X, CX = ws.rayleigh_ritz(C, X)
-        gemms += warm + 1
-    res, r, hist = np.inf, 0, []
-    for r in range(1, max_rounds + 1):
-        cut, top = float(th[-1]), float(th[0])
-        lo = -1e-3 * cut              # C is a PSD correlation: nothing meaningful below 0
-        for _ in range(chunks):
-            X = ws.cholqr2(ws.filter(C, X, degree, lo, cut, top))
-            gemms += degree
-        th, X, CX = ws.rayleigh_ritz(C, X)
-        gemms += 1
-        thd = torch.from_numpy(th[:k].copy()).to(C.device)
-        res = float(torch.linalg.vector_norm(CX[:, :k] - X[:, :k] * thd, dim=0).max()) / float(th[0])
-        hist.append(res)
-        if res <= tol:
-            break
-        chunks = 1                    # top-up rounds
-    return th[:k].copy(), X[:, :k].contiguous(), dict(rounds=r, gemms=gemms, residual=res, block=m,
-                                                        degree=degree, hist=hist)
+    X = ws.start()
+    if warm and schedule is None:
+        th = ws.quotients(C, X)             # enough for the warm filter's interval
+        worst = np.inf
+    else:
+        th, V, res = ws.ritz(C, X, k)
+        worst = float(res.max())
+    gemms, degrees, rounds, rate = 1, 0, 0, None
+    hist = [worst]
+    cuts = [] if schedule is not None else None
+    while worst > tol and degrees < max_degree:
+        rounds += 1
+        # damped interval [lo, theta_{m-5}]: its edge converges (to ~lambda_{m-4}) within two
+        # rounds, where theta_{m-1} is still far below lambda_{m-1} (profiles/r3/topk_*.json)
+        top, cut = float(th[0]), float(th[m - 5 if cut_index is None else cut_index])
+        lo = -1e-3 * cut                    # C is a PSD correlation: nothing meaningful below 0
+        if schedule is not None:            # diagnostics: fixed degrees per round
+            if rounds > len(schedule):
+                break
+            need = schedule[rounds - 1]
+        elif rounds == 1 and warm:
+            need = warm
+        else:
+            if rate is None:
+                rate = rate_factor * _chebyshev_rate(2.0 * float(th[k - 1]) / cut - 1.0)
+            rate = max(rate, 0.05)
+            need = int(np.ceil(margin * np.log(worst / tol) / rate))
+        need = max(2, min(need, max_degree - degrees))
+        # condition growth of the block over one chunk ~ T_d(x_0): keep it below ~2e6
+        grow = max(_chebyshev_rate(2.0 * top / cut - 1.0), 1e-3)
+        chunk = int(min(20, max(2, np.floor(np.log(2e6) / grow))))
+        nchunks = -(-need // chunk)
+        per = -(-need // nchunks)
+        for _ in range(nchunks):
+            X = ws.cholqr(ws.filter(C, X, per, lo, cut, top), ws.Q0)
+        X = ws.cholqr(X, ws.Q1)
+        degrees += per * nchunks
+        gemms += per * nchunks + 1
+        th, V, res = ws.ritz(C, X, k)
+        new = float(res.max())
+        hist.append(new)
+        if cuts is not None:
+            cuts.append((per * nchunks, cut))
+        if rounds > 1 or not warm:          # the warm round's rate says nothing about the next
+            rate = np.log(worst / new) / (per * nchunks) if 0.0 < new < worst else 0.5 * rate
+        worst = new
+    Xk = ws.rotate(X, V)[:, :k].contiguous()
+    info = dict(rounds=rounds, gemms=gemms, degrees=degrees, residual=worst, block=m, hist=hist)
+    if cuts is not None:
+        info["cuts"] = cuts
+    return th[:k].copy(), Xk, info

@@ -181,6 +181,7 @@ def test_leading_eigenpairs_vs_eigh(ctx, n, k):
     Ch = C.cpu().numpy()
     assert np.max(np.linalg.norm(Ch @ Xh - Xh * th, axis=0)) <= 1e-12 * lr[0]
     assert np.max(np.abs(Xh.T @ Xh - np.eye(k))) <= 1e-12
+    assert info["residual"] <= 3e-14 and info["hist"][-1] == info["residual"]
     gl = np.abs(np.diff(lr)) / lr[0]
     for j in range(k):
         if min(gl[j], gl[j - 1] if j else np.inf) <= 1e-6:
@@ -233,7 +234,8 @@ def test_spectrum_queue_spreads_and_matches(ctx, world):
 
 @pytest.mark.parametrize("n", [64, 1000, 4096])
 def test_block_kernels(ctx, n):
-    """pods_gram, pods_cholqr (twice = orthonormal), pods_right_mul against torch."""
+    """pods_gram, pods_cholqr (twice = orthonormal), pods_right_mul, pods_ritz_residual against
+    torch."""
     import ctypes
     m = 64
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
@@ -254,3 +256,8 @@ def test_block_kernels(ctx, n):
     out = torch.empty_like(Y)
     podsgen.check(ctx.lib.pods_right_mul(ctx.h, P(Y), P(M), n, m, P(out)), "pods_right_mul")
     assert float((out - Y @ M).abs().max()) <= 1e-13 * float((Y @ M).abs().max())
+    # Rayleigh-Ritz residual block E = CX - X H
+    E_ = torch.empty_like(Y)
+    podsgen.check(ctx.lib.pods_ritz_residual(ctx.h, P(Y), P(Z), P(M), n, m, P(E_)), "pods_ritz_residual")
+    ref = Z - Y @ M
+    assert float((E_ - ref).abs().max()) <= 1e-13 * float((Y @ M).abs().max())

@@ -23,9 +23,13 @@ def main(reps):
     Y = torch.randn(n, 64, dtype=torch.float64, device="cuda")
     Z = torch.randn(n, 64, dtype=torch.float64, device="cuda")
     out = torch.empty_like(Y)
+    ws.step(C, Y, Z, 1.0, 0.5, 0.25, out)
+    ref = C @ Y + 0.5 * Y + 0.25 * Z
+    torch.cuda.synchronize()
+    print("cheb rel err %.3e" % float((out - ref).abs().max() / ref.abs().max()), flush=True)
     for name, fn in (("cheb", lambda: ws.step(C, Y, Z, 1.0, 0.5, 0.25, out)),
                      ("cholqr", lambda: ctx.lib.pods_cholqr(ctx.h, _p(Y), n, 64, _p(out))),
-                     ("gram", lambda: ctx.lib.pods_gram(ctx.h, _p(Y), _p(Z), n, 64, _p(ws.G)))):
+                     ("gram", lambda: ctx.lib.pods_gram(ctx.h, _p(Y), _p(Z), n, 64, _p(ws.HF[0])))):
         for _ in range(3):
             fn()
         torch.cuda.synchronize()

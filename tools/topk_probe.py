@@ -28,17 +28,28 @@ def main(out, reps):
     Vh = torch.flip(Vr, (1,))[:, :k].cpu().numpy()
     ws = Subspace(gen.ctx, n, 64)
     rows = []
-    for warm, deg, ch in ((8, 12, 3), (8, 12, 4), (8, 16, 3), (10, 20, 2), (8, 10, 5), (6, 24, 2)):
+    configs = ((0.85, 1.05, 20), (0.9, 1.05, 16))
+    if len(sys.argv) > 3:   # e.g. "0.8,1.1,8;0.7,1.2,8" (rate_factor, margin, warm)
+        configs = [tuple(float(v) for v in c.split(",")) for c in sys.argv[3].split(";")]
+        configs = [(a, b, int(c)) for a, b, c in configs]
+    for rf, mg, wm in configs:
         for rep in range(reps):
             torch.cuda.synchronize()
             t = time.time()
-            th, X, info = leading_eigenpairs(gen.ctx, C, k, m=64, degree=deg, chunks=ch, warm=warm, ws=ws)
+            th, X, info = leading_eigenpairs(gen.ctx, C, k, m=64, rate_factor=rf, margin=mg, warm=wm, ws=ws)
             torch.cuda.synchronize()
             dt = time.time() - t
         Xh = X.cpu().numpy()
         err = max(float(np.max(np.abs(np.sign(np.dot(Xh[:, j], Vh[:, j])) * Xh[:, j] - Vh[:, j]))) for j in range(k))
-        rows.append(dict(warm=warm, deg=deg, chunks=ch, ms=dt * 1e3, vec_err=err,
+        rows.append(dict(rate_factor=rf, margin=mg, warm=wm, ms=dt * 1e3, vec_err=err,
                          lam_err=float(np.max(np.abs(th - lam[:k])) / lam[0]), **info))
+        print(json.dumps(rows[-1]), flush=True)
+    # convergence per round for a fixed schedule and several damped-interval edges
+    for ci, sched in ((63, [16] * 6), (59, [16] * 6), (55, [16] * 6), (59, [8] + [16] * 5), (59, [24] * 4),
+                      (59, [12] * 8)):
+        th, X, info = leading_eigenpairs(gen.ctx, C, k, m=64, cut_index=ci, schedule=sched, tol=1e-300, ws=ws)
+        cuts = [(d, c / lam[0], int(np.searchsorted(-lam, -c))) for d, c in info["cuts"]]
+        rows.append(dict(cut_index=ci, schedule=sched, hist=info["hist"], cuts=cuts))
         print(json.dumps(rows[-1]), flush=True)
     with open(os.path.join(out, "topk_probe.json"), "w") as f:
         json.dump(rows, f)
