@@ -179,10 +179,10 @@ struct RngBuffers {
 };
 
 // SYRK work items {bi, bj, split, 0}: split-major, then 8x8 super-blocks of 128x128 tiles
-// in the lower triangle, tiles row-major inside a super-block (kernels 1 and 3).  Consecutive
-// items go to one XCD, so the 64 workgroups an XCD holds at once (two per CU) cover one
-// super-block: 16 panels, one K range.
-std::vector<int> syrk_items(int kernel, int ns, int nsplit) {
+// in the lower triangle, tiles row-major inside a super-block.  Consecutive items go to one
+// XCD, so the 64 workgroups an XCD holds at once (two per CU) cover one super-block: 16
+// panels, one K range.
+std::vector<int> syrk_items(int ns, int nsplit) {
   std::vector<int> it;
   auto push = [&](int bi, int bj, int s) {
     it.push_back(bi);
@@ -190,16 +190,6 @@ std::vector<int> syrk_items(int kernel, int ns, int nsplit) {
     it.push_back(s);
     it.push_back(0);
   };
-  if (kernel == 2) {  // 256 x 128 tiles, super-blocks of 4 x 8 tiles (32 = one XCD's CUs)
-    const int nbi = (ns + 255) / 256, nbj = (ns + 127) / 128;
-    for (int s = 0; s < nsplit; ++s)
-      for (int BI = 0; BI < nbi; BI += 4)
-        for (int BJ = 0; BJ < nbj; BJ += 8)
-          for (int bi = BI; bi < std::min(nbi, BI + 4); ++bi)
-            for (int bj = BJ; bj < std::min(nbj, BJ + 8); ++bj)
-              if (bj < 2 * bi + 2) push(bi, bj, s);
-    return it;
-  }
   const int T = 128, SB = 8;
   const int nb = (ns + T - 1) / T;
   const int nsb = (nb + SB - 1) / SB;
@@ -210,15 +200,6 @@ std::vector<int> syrk_items(int kernel, int ns, int nsplit) {
           for (int bj = Jb * SB; bj < std::min(nb, (Jb + 1) * SB); ++bj)
             if (bj <= bi) push(bi, bj, s);
   return it;
-}
-
-// 3 (default): 128 x 128 tiles, two workgroups per CU; 2: 256 x 128 tiles, one per CU
-// (1.9 ms slower at C3); 1: the register-staged v1.
-int syrk_kernel_choice() {
-  const char* e = std::getenv("PODS_SYRK_KERNEL");
-  if (e && e[0] == '1') return 1;
-  if (e && e[0] == '2') return 2;
-  return 3;
 }
 
 }  // namespace
@@ -254,7 +235,6 @@ struct pods_ctx {
   int nprog_mean = 0;
   bool mean_valid = false;
   bool have_snapshots = false;  // A holds ns x rowlen snapshots (generated or loaded)
-  bool gen_fused = false;       // pods_df_generate runs k_filter_xyz (no T1 planes)
   bool centered = false;        // A holds A - mean (pods_center); consumers subtract zero
   DevBuf zero;                  // rowpad zeros: the mean operand once A is centred
   std::vector<double> stage;  // host staging for small uploads
@@ -435,11 +415,7 @@ int pods_df_configure(pods_ctx* c, const pods_df_params* prm, const double* bx, 
   const int64_t ntot = nplanes * c->S;  // doubles of the stream that reach A
   c->layout = make_layout(ntot);
   PODS_HIP(ensure(c->R, (size_t)nplanes * c->Sl * sizeof(double)));
-  // PODS_GEN_FUSED=1 selects the fused x+y+z pass (k_filter_xyz: no x-filtered planes, bit
-  // identical); the default two-pass path (k_filter_x2 + k_filter_yz) is faster
-  const char* fz = std::getenv("PODS_GEN_FUSED");
-  c->gen_fused = pods::filter_xyz_supported(c->NX, c->NY, c->NZ) && fz && std::atoi(fz) == 1;
-  if (!c->gen_fused) PODS_HIP(ensure(c->T1, (size_t)3 * p.ns * c->Sl * sizeof(double)));
+  PODS_HIP(ensure(c->T1, (size_t)3 * p.ns * c->Sl * sizeof(double)));
   PODS_HIP(ensure(c->A, (size_t)p.ns * c->rowpad * sizeof(double)));
   PODS_HIP(ensure(c->mean, (size_t)c->rowpad * sizeof(double)));
   // padded K columns of the K-tiled snapshot matrix (and of the mean) stay zero
@@ -490,17 +466,6 @@ int pods_df_generate(pods_ctx* c) {
                                     p.j1 + 2 * p.nfy, c->Sl, p.rng_low, p.rng_range, c->R.as<double>(),
                                     c->stream));
   const double* taps = c->taps.as<double>();
-  if (c->gen_fused) {
-    int cus = 256;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
-    PODS_HIP(pods::launch_filter_xyz(c->NX, c->NY, c->NZ, c->R.as<double>(), taps, p.ns, c->jl, p.kma, c->Kp,
-                                     c->Sl, c->lund.as<double>(), c->lund_sj, p.lund_mode, c->rot.as<double>(),
-                                     p.rotate, c->A.as<double>(), cus, c->stream));
-    c->have_snapshots = true;
-    c->mean_valid = false;
-    c->centered = false;
-    return PODS_OK;
-  }
   // x pass: enough (component, point, step-chunk) threads to fill the chip
   const int64_t pts = 3 * c->Sl;
   int64_t nch = (256LL * 2048 + pts - 1) / pts;
@@ -600,18 +565,17 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
   PODS_HIP(hipSetDevice(c->device));
   int64_t ksplit = 0;
   const int ns = c->p.ns;
-  const int kern = syrk_kernel_choice();
-  const int nsplit = pods::syrk_plan(kern, ns, c->rowpad, &ksplit);
-  if (nsplit > 1 || kern >= 2) PODS_HIP(ensure(c->cwork, (size_t)nsplit * ns * ns * sizeof(double)));
-  const int64_t key = ((int64_t)kern << 40) | ((int64_t)ns << 20) | nsplit;
+  const int nsplit = pods::syrk_plan(ns, c->rowpad, &ksplit);
+  PODS_HIP(ensure(c->cwork, (size_t)nsplit * ns * ns * sizeof(double)));
+  const int64_t key = ((int64_t)ns << 20) | nsplit;
   if (c->items_key != key) {
-    std::vector<int> items = syrk_items(kern, ns, nsplit);
+    std::vector<int> items = syrk_items(ns, nsplit);
     PODS_HIP(ensure(c->items, items.size() * sizeof(int)));
     PODS_HIP(hipMemcpy(c->items.p, items.data(), items.size() * sizeof(int), hipMemcpyHostToDevice));
     c->nitems = (int)items.size() / 4;
     c->items_key = key;
   }
-  PODS_HIP(pods::launch_syrk(kern, c->A.as<double>(), c->rowpad, ns, c->rowpad,
+  PODS_HIP(pods::launch_syrk(c->A.as<double>(), ns, c->rowpad,
                              c->centered ? c->zero.as<double>() : c->mean.as<double>(),
                              c->items.as<int>(), c->nitems, nsplit, ksplit, C_dev, ns, divide,
                              c->cwork.as<double>(), c->centered ? 1 : 0, c->stream));
@@ -982,14 +946,14 @@ int pods_syev(pods_ctx* c, const double* C, int n, int nvec, double* lam_desc, d
   double* tau = det + 2 * (int64_t)n;
   double* bounds = det + 3 * (int64_t)n;
   // All n eigenvalues start from brackets given by Sturm counts at 64 Ki shared shifts
-  // (k_sturm_grid, 0.16 ms): k_bisect 2.09 -> 1.41 ms.  PODS_BISECT_PLAIN=1 starts every
-  // eigenvalue from the Gershgorin interval instead.
+  // (k_sturm_grid, 0.16 ms): k_bisect 2.09 -> 1.41 ms against every eigenvalue from the
+  // Gershgorin interval.
   // (Bisecting the nvec wanted eigenvalues first and the rest on a side stream was measured
   // slower: each eigenvalue's bisection is latency bound (13 sequential n-step Sturm
   // passes), so the top nvec alone cost as much as all n, and the side launch slowed the
   // back-transformation kernels it shared CUs with.)
   PODS_HIP(ensure(c->e_cnt, pods::tri_grid_bytes()));
-  int* gcnt = std::getenv("PODS_BISECT_PLAIN") ? nullptr : c->e_cnt.as<int>();
+  int* gcnt = c->e_cnt.as<int>();
   PODS_HIP(pods::launch_tri_eigvals(D, E, n, bounds, lam_desc, gcnt, c->stream));
   if (nvec > 0) {
     const int nblk = std::max((n - 1 + 63) / 64, 1);

@@ -21,10 +21,6 @@ hipError_t launch_mt_generate(const uint32_t* states, int G, int64_t Bs, int64_t
 hipError_t launch_filter_x(int NX, const double* R, const double* bx, int ns, int64_t Sl, int ncomp,
                            int chunk, double* T1, hipStream_t st);
 // lund_sj: j-stride of the 9 x Pl Lund table (0 = the same row of parameters for every j)
-bool filter_xyz_supported(int NX, int NY, int NZ);
-hipError_t launch_filter_xyz(int NX, int NY, int NZ, const double* R, const double* taps, int ns, int jl, int K,
-                             int Kp, int64_t Sl, const double* lund, int64_t lund_sj, int lund_mode,
-                             const double* rot, int rotate, double* AT, int cus, hipStream_t st);
 hipError_t launch_filter_yz(int NY, const double* T1, const double* by, const double* bz, int NZ,
                             int ns, int jl, int K, int Kp, int64_t Sl, int ncomp,
                             const double* lund, int64_t lund_sj, int lund_mode, const double* rot,
@@ -34,13 +30,13 @@ hipError_t launch_lund_apply(double* yu, double* yv, double* yw, int64_t P, cons
                              int lund_mode, const double* rot, int rotate, hipStream_t st);
 hipError_t launch_mean(const double* AT, int64_t rowlen, int ns, const int* prog, int nprog,
                        double* mean, hipStream_t st);
-// SYRK kernels: 1 = 128x128 register-staged (k_syrk_split), 2 = 256x128 LDS-DMA (k_syrk_glds).
-// Split-K plan: returns the number of K splits (work slabs of ns*ns doubles needed when > 1).
-int syrk_plan(int kernel, int ns, int64_t Kdim, int64_t* ksplit);
+// Split-K SYRK (k_syrk_g128 + k_syrk_reduce).  Plan: returns the number of K splits (work
+// slabs of ns*ns doubles).
+int syrk_plan(int ns, int64_t Kdim, int64_t* ksplit);
 // items: nitems x int4 {bi, bj, split, 0} in launch order (see podsgen_api.cpp syrk_items)
-hipError_t launch_syrk(int kernel, const double* AT, int64_t ld, int ns, int64_t Kdim,
-                       const double* mean, const int* items, int nitems, int nsplit, int64_t ksplit,
-                       double* C, int64_t ldc, int divide, double* work, int centred, hipStream_t st);
+hipError_t launch_syrk(const double* AT, int ns, int64_t Kdim, const double* mean, const int* items, int nitems,
+                       int nsplit, int64_t ksplit, double* C, int64_t ldc, int divide, double* work, int centred,
+                       hipStream_t st);
 // A <- A - mean in place (K-tiled layout, rowpad rows x ns snapshots)
 hipError_t launch_center(double* AT, int64_t rowpad, int ns, const double* mean, hipStream_t st);
 hipError_t launch_divide(double* x, int64_t n, double d, hipStream_t st);

@@ -113,74 +113,14 @@ __device__ void twist_wave(uint32_t* st, int lane) {
   wave_sync();
 }
 
-// Jump-ahead: dst = g(F) src by block Horner over 32 blocks of 624 coefficients:
-//   acc <- twist(acc) ^ sum_r c_{624q+r} window_r(x),  x = (src, twist(src)).
-__global__ __launch_bounds__(256) void k_mt_jump(const uint32_t* __restrict__ src_base,
-                                                 const int* __restrict__ src_idx,
-                                                 const uint32_t* __restrict__ polys,
-                                                 const int* __restrict__ poly_idx,
-                                                 uint32_t* __restrict__ dst_base,
-                                                 const int* __restrict__ dst_idx, int njobs) {
-  // x[0, 2N): the window source; x[2N, 3N): zeros, read by the padding slots of a 4-bit batch
-  constexpr int ZR = 2 * MTN;
-  __shared__ uint32_t x[3 * MTN];
-  __shared__ uint32_t acc[MTN];
-  __shared__ uint32_t g[MTN];  // the jump polynomial's coefficient bits (read wave-uniformly)
-  const int job = blockIdx.x;
-  if (job >= njobs) return;
-  const uint32_t* s = src_base + (size_t)src_idx[job] * MTN;
-  const uint32_t* gsrc = polys + (size_t)poly_idx[job] * MTN;
-  for (int i = threadIdx.x; i < MTN; i += 256) {
-    const uint32_t v = s[i];
-    x[i] = v;
-    x[MTN + i] = v;
-    x[ZR + i] = 0u;
-    acc[i] = 0u;
-    g[i] = gsrc[i];
-  }
-  __syncthreads();
-  twist_block256(x + MTN);
-  const int w0 = threadIdx.x, w1 = threadIdx.x + 256, w2 = threadIdx.x + 512;
-  const bool has2 = w2 < MTN;
-  for (int q = 31; q >= 0; --q) {
-    if (q != 31) twist_block256(acc);
-    uint32_t v0 = 0, v1 = 0, v2 = 0;
-    for (int rb = 0; rb < MTN; rb += 32) {
-      const int off = q * MTN + rb;
-      const int wi = off >> 5, sh = off & 31;
-      uint32_t bits = g[wi] >> sh;
-      if (sh && wi + 1 < MTN) bits |= g[wi + 1] << (32 - sh);
-      if (rb + 32 > MTN) bits &= (1u << (MTN - rb)) - 1u;
-      bits = __builtin_amdgcn_readfirstlane(bits);
-      // four set bits per iteration (missing ones read the zero block): 12 independent LDS
-      // loads in flight instead of a load-use chain per bit; XOR order does not matter
-      while (bits) {
-        int r[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          r[u] = bits ? rb + __builtin_ctz(bits) : ZR;
-          bits &= bits - 1u;
-        }
-        v0 ^= (x[r[0] + w0] ^ x[r[1] + w0]) ^ (x[r[2] + w0] ^ x[r[3] + w0]);
-        v1 ^= (x[r[0] + w1] ^ x[r[1] + w1]) ^ (x[r[2] + w1] ^ x[r[3] + w1]);
-        if (has2) v2 ^= (x[r[0] + w2] ^ x[r[1] + w2]) ^ (x[r[2] + w2] ^ x[r[3] + w2]);
-      }
-    }
-    acc[w0] ^= v0;
-    acc[w1] ^= v1;
-    if (has2) acc[w2] ^= v2;
-    __syncthreads();
-  }
-  uint32_t* d = dst_base + (size_t)dst_idx[job] * MTN;
-  for (int i = threadIdx.x; i < MTN; i += 256) d[i] = acc[i];
-}
-
-// The same jump with the coefficients taken three at a time (a sliding-window table): for
-// each 3-bit pattern p, Y_p[k] = XOR_{i in p} x[k + i] is built once per job, so the three
-// windows of coefficients r, r+1, r+2 cost ONE LDS read (Y_p[r + w]) instead of one per set
-// bit (1.5 on average).  Pattern 0 is a row of zeros, so every group reads unconditionally
-// and the 24 reads of an 8-group chunk are independent.  XOR is exact and order-free: the
-// result is bit-identical to k_mt_jump.  LDS 47 KB: three workgroups per CU.
+// Jump-ahead: dst = g(F) src by block Horner over 32 blocks of 624 coefficients,
+//   acc <- twist(acc) ^ sum_r c_{624q+r} window_r(x),  x = (src, twist(src)),
+// with the coefficients taken three at a time (a sliding-window table): for each 3-bit
+// pattern p, Y_p[k] = XOR_{i in p} x[k + i] is built once per job, so the three windows of
+// coefficients r, r+1, r+2 cost ONE LDS read (Y_p[r + w]) instead of one per set bit (a
+// per-bit version took 1.19 against 0.89 ms at C3).  Pattern 0 is a row of zeros, so every
+// group reads unconditionally and the 24 reads of an 8-group chunk are independent.  XOR is
+// exact and order-free.  LDS 47 KB: three workgroups per CU.
 __global__ __launch_bounds__(256) void k_mt_jump3(const uint32_t* __restrict__ src_base,
                                                   const int* __restrict__ src_idx,
                                                   const uint32_t* __restrict__ polys,
@@ -528,24 +468,16 @@ __global__ __launch_bounds__(NT) void k_filter_yz(
     const double* __restrict__ T1, const double* __restrict__ by, const double* __restrict__ bz,
     int NZr, int ns, int jl, int K, int Kp, int64_t Sl, int ncomp,
     const double* __restrict__ lund, int64_t lund_sj, int lund_mode, const double* __restrict__ rot,
-    int rotate, double* __restrict__ AT, int nsb, int xcd_remap) {
+    int rotate, double* __restrict__ AT, int nsb) {
   extern __shared__ __attribute__((aligned(16))) double t2[];  // TJ x ldt
   constexpr int YR = TJ < 16 ? TJ : 16;  // rows per y-pass item
   constexpr int NZMAX = NZC > 0 ? NZC : 25;
   const int NZ = NZC > 0 ? NZC : NZr;
   constexpr int WIN = 16 + NZMAX - 1;
   const int ldt = kpad(Kp + 16) + 1;
-  // XCD-aware block order: blocks are dealt round-robin over the 8 XCDs (b and b+8 share one),
-  // so the row tiles of one step group -- whose y halos are each other's rows -- would land on
-  // 8 different L2s.  Renumber so each XCD walks consecutive (step group, tile) pairs: the
-  // neighbouring tiles of a step group run together on one XCD and the halo rows hit its L2.
-  // Any map is correct (blocks are independent); this one is only for speed.
-  int lin = blockIdx.y * gridDim.x + blockIdx.x;
-  if (xcd_remap) {
-    const int nfull = (int)(gridDim.x * gridDim.y) & ~7;
-    if (lin < nfull) lin = (lin & 7) * (nfull >> 3) + (lin >> 3);
-  }
-  const int tile_x = lin % gridDim.x, group_y = lin / gridDim.x;
+  // (An XCD-aware renumbering of the blocks, so the row tiles of one step group share an L2,
+  // cut the HBM traffic 18.4 -> 14.5 GB at C3 at the same time and made C4 ~4 ms slower.)
+  const int tile_x = blockIdx.x, group_y = blockIdx.y;
   const int jt = tile_x * TJ;
   const int tid0 = threadIdx.x;
   const int rows = min(TJ, jl - jt);
@@ -825,244 +757,24 @@ __global__ __launch_bounds__(256) void k_center(double* __restrict__ AT, int64_t
 // -----------------------------------------------------------------------------------------
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
-// Split-K SYRK, 128x128 tiles.  Work item = (lower-triangle tile, K split), dealt so that the
-// items one XCD runs back to back are neighbouring tiles of one split (T1 remap, bijective).
-// 4 waves as 2x2, each wave 64x64 = 4x4 MFMA 16x16 blocks; next K-tile prefetched into
-// registers while the current one is on the matrix cores.  Partials go to slab `s` of Cout
-// (deterministic: the sum over splits is done by k_syrk_reduce in split order).
-template <int BT, int KT>
-__global__ __launch_bounds__(256, 2) void k_syrk_split(const double* __restrict__ AT, int64_t ld,
-                                                       int ns, int64_t Kdim,
-                                                       const double* __restrict__ mean,
-                                                       const int4* __restrict__ items, int nitems,
-                                                       int64_t ksplit, double* __restrict__ Cout,
-                                                       int64_t ldc, int64_t slab, int final_write,
-                                                       int divide) {
-  constexpr int MB = BT / 32;            // 16x16 blocks per wave per dim
-  constexpr int PAIRS = BT * KT / 2;     // double2 per operand per K-tile
-  constexpr int PPT = PAIRS / 256;       // per thread
-  __shared__ __attribute__((aligned(16))) double Xs[BT][KT + 1];
-  __shared__ __attribute__((aligned(16))) double Ys[BT][KT + 1];
-  // items[] is host-ordered (split, super-block, tile); the bijective XCD remap hands each
-  // XCD a contiguous run of it (T1), so co-resident workgroups share panels and K position.
-  const int b = blockIdx.x;
-  const int xcd = b & 7, qq = nitems >> 3, rr = nitems & 7;
-  const int logical = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
-  const int4 it = items[logical];
-  const int bi = it.x, bj = it.y, sp = it.z;
-  const int64_t kb = (int64_t)sp * ksplit;
-  const int64_t ke = min(Kdim, kb + ksplit);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int i0 = bi * BT, j0 = bj * BT;
-  f64x4 acc[MB][MB];
-#pragma unroll
-  for (int m = 0; m < MB; ++m)
-#pragma unroll
-    for (int n = 0; n < MB; ++n) acc[m][n] = (f64x4){0.0, 0.0, 0.0, 0.0};
-  double2 xr[PPT], yr[PPT];
-  // K-tiled layout: the (panel, K-tile) operand is a contiguous BT x KT block; padded K
-  // columns are zero in both A and the mean, so no K guard is needed.
-  auto load = [&](int64_t k0) {
-    const double* xb = AT + (((k0 >> 4) * ns + i0) << 4);
-    const double* yb = AT + (((k0 >> 4) * ns + j0) << 4);
-#pragma unroll
-    for (int e = 0; e < PPT; ++e) {
-      const int pidx = tid + e * 256;
-      const int row = pidx / (KT / 2), kk = (pidx % (KT / 2)) * 2;
-      const double2 m2 = *reinterpret_cast<const double2*>(mean + k0 + kk);
-      double2 xv = make_double2(0.0, 0.0), yv = make_double2(0.0, 0.0);
-      if (i0 + row < ns) {
-        const double2 a = *reinterpret_cast<const double2*>(xb + row * KT + kk);
-        xv = make_double2(a.x - m2.x, a.y - m2.y);
-      }
-      if (j0 + row < ns) {
-        const double2 a = *reinterpret_cast<const double2*>(yb + row * KT + kk);
-        yv = make_double2(a.x - m2.x, a.y - m2.y);
-      }
-      xr[e] = xv;
-      yr[e] = yv;
-    }
-  };
-  load(kb);
-  for (int64_t k0 = kb; k0 < ke; k0 += KT) {
-#pragma unroll
-    for (int e = 0; e < PPT; ++e) {
-      const int pidx = tid + e * 256;
-      const int row = pidx / (KT / 2), kk = (pidx % (KT / 2)) * 2;
-      Xs[row][kk] = xr[e].x;
-      Xs[row][kk + 1] = xr[e].y;
-      Ys[row][kk] = yr[e].x;
-      Ys[row][kk + 1] = yr[e].y;
-    }
-    __syncthreads();
-    if (k0 + KT < ke) load(k0 + KT);
-#pragma unroll
-    for (int kk = 0; kk < KT; kk += 4) {
-      double a[MB], bv[MB];
-#pragma unroll
-      for (int m = 0; m < MB; ++m) a[m] = Xs[wr * (BT / 2) + m * 16 + (lane & 15)][kk + (lane >> 4)];
-#pragma unroll
-      for (int n = 0; n < MB; ++n) bv[n] = Ys[wc * (BT / 2) + n * 16 + (lane & 15)][kk + (lane >> 4)];
-#pragma unroll
-      for (int m = 0; m < MB; ++m)
-#pragma unroll
-        for (int n = 0; n < MB; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], bv[n], acc[m][n], 0, 0, 0);
-    }
-    __syncthreads();
-  }
-  double* dst = final_write ? Cout : Cout + (int64_t)sp * slab;
-  const double dn = (double)ns;
-#pragma unroll
-  for (int m = 0; m < MB; ++m)
-#pragma unroll
-    for (int n = 0; n < MB; ++n)
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int gi = i0 + wr * (BT / 2) + m * 16 + (lane >> 4) + 4 * reg;
-        const int gj = j0 + wc * (BT / 2) + n * 16 + (lane & 15);
-        if (gi < ns && gj < ns) {
-          double v = acc[m][n][reg];
-          if (final_write) {
-            if (divide) v = v / dn;
-            dst[(int64_t)gi * ldc + gj] = v;
-            if (bi != bj) dst[(int64_t)gj * ldc + gi] = v;
-          } else if (gi >= gj) {
-            dst[(int64_t)gi * ldc + gj] = v;
-          }
-        }
-      }
-}
-
-// SYRK v2: one 256 x 128 tile per workgroup (one 512-thread workgroup per CU), operands
-// streamed by LDS-DMA (global_load_lds_dwordx4) into a 3-stage ring; counted vmcnt + raw
-// s_barrier keep two K-tiles in flight across barriers.  The K-tiled A makes each (panel,
-// K-tile) operand one contiguous block; rows are XOR-swizzled on the SOURCE address (double2
-// slot j of row R holds logical slot j ^ ((R>>1)&7)) so the MFMA fragment reads are
-// bank-conflict free.  The mean is subtracted while fragments are read (A stays uncentred).
-// 8 waves as 4 x 2, each 64 x 64 = 4 x 4 blocks of v_mfma_f64_16x16x4_f64.  Partial tiles
-// (lower triangle only) go to slab `split`; k_syrk_reduce sums the slabs in split order.
-namespace syrk2 {
-constexpr int BM = 256, BN = 128, KT = 16, NST = 3, NW = 8;
-constexpr int XB = BM * KT * 8;            // 32 KB
-constexpr int YB = BN * KT * 8;            // 16 KB
-constexpr int MBYTES = NW * 128;           // one 16-double mean slot per wave
-constexpr int STAGE = XB + YB + MBYTES;    // 49 KB
-constexpr int XP = XB / 1024 / NW;         // LDS-DMA pieces per wave per stage: 4
-constexpr int YP = YB / 1024 / NW;         //                                    2
-}  // namespace syrk2
-
 __device__ __forceinline__ void glds16(const void* src, uint32_t lds_byte_addr) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(uintptr_t)lds_byte_addr,
                                    16, 0, 0);
 }
 
-// CENTRED = 1: A was centred in place (k_center), so the fragments go to the MFMAs as
-// read; the in-loop subtraction costs 8 v_add_f64 per 16 MFMAs (57.0 -> 52.9 ms measured).
-template <int CENTRED>
-__global__ __launch_bounds__(512, 1) void k_syrk_glds(const double* __restrict__ AT, int ns,
-                                                      int64_t Kdim, const double* __restrict__ mean,
-                                                      const int4* __restrict__ items, int nitems,
-                                                      int64_t ksplit, double* __restrict__ work,
-                                                      int64_t ldc, int64_t slab) {
-  using namespace syrk2;
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  const int b = blockIdx.x;
-  const int xcd = b & 7, qq = nitems >> 3, rr = nitems & 7;
-  const int logical = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
-  const int4 it = items[logical];
-  const int bi = it.x, bj = it.y, sp = it.z;
-  const int i0 = bi * BM, j0 = bj * BN;
-  const int64_t kt0 = (int64_t)sp * (ksplit / KT);
-  const int64_t kt1 = min(Kdim, (int64_t)(sp + 1) * ksplit) / KT;
-  const int nt = (int)(kt1 - kt0);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wr = wave >> 1, wc = wave & 1;
-  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
-  // LDS-DMA piece q of this wave covers 8 rows of 128 B; lane -> (row R, 16-B slot)
-  const int lrow = lane >> 3, lslot = lane & 7;
-  int64_t xsrc[XP], ysrc[YP];  // per-lane source offsets (doubles) inside one K-tile block
-#pragma unroll
-  for (int q = 0; q < XP; ++q) {
-    const int R = (wave * XP + q) * 8 + lrow;
-    xsrc[q] = ((int64_t)min(i0 + R, ns - 1) << 4) + ((lslot ^ ((R >> 1) & 7)) << 1);
-  }
-#pragma unroll
-  for (int q = 0; q < YP; ++q) {
-    const int R = (wave * YP + q) * 8 + lrow;
-    ysrc[q] = ((int64_t)min(j0 + R, ns - 1) << 4) + ((lslot ^ ((R >> 1) & 7)) << 1);
-  }
-  const int64_t blk = (int64_t)ns << 4;  // doubles per K-tile block
-  auto issue = [&](int t) {
-    const int64_t kt = kt0 + t;
-    const uint32_t base = lds0 + (uint32_t)((t % NST) * STAGE);
-    const double* g = AT + kt * blk;
-#pragma unroll
-    for (int q = 0; q < XP; ++q) glds16(g + xsrc[q], base + (wave * XP + q) * 1024);
-#pragma unroll
-    for (int q = 0; q < YP; ++q) glds16(g + ysrc[q], base + XB + (wave * YP + q) * 1024);
-    // mean K-tile: 16 doubles = lanes 0..7 x 16 B (an LDS-DMA writes base + 16*lane for each
-    // active lane, so the other lanes must be masked off)
-    if (lane < 8) glds16(mean + kt * KT + (lane << 1), base + XB + YB + wave * 128);
-  };
-  f64x4 acc[4][4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = (f64x4){0.0, 0.0, 0.0, 0.0};
-  if (nt > 0) issue(0);
-  if (nt > 1) issue(1);
-  // fragment offsets: row R = base + 16*m + fr, swizzle (R>>1)&7 = (fr>>1)&7 for every m
-  const int fr = lane & 15, fk = lane >> 4, fs = (fr >> 1) & 7;
-  const int xrow = (wr * 64 + fr) << 4, yrow = (wc * 64 + fr) << 4;
-  for (int t = 0; t < nt; ++t) {
-    if (t + 1 < nt)
-      asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (t + 2 < nt) issue(t + 2);
-    const char* st = smem + (t % NST) * STAGE;
-    const double* Xs = reinterpret_cast<const double*>(st);
-    const double* Ys = reinterpret_cast<const double*>(st + XB);
-    const double* Ms = reinterpret_cast<const double*>(st + XB + YB + wave * 128);
-#pragma unroll
-    for (int kk = 0; kk < KT; kk += 4) {
-      const int k = kk + fk;
-      const int koff = ((((k >> 1) ^ fs)) << 1) + (k & 1);
-      const double mk = Ms[k];
-      double a[4], bv[4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) a[m] = CENTRED ? Xs[xrow + koff + m * 256] : Xs[xrow + koff + m * 256] - mk;
-#pragma unroll
-      for (int n = 0; n < 4; ++n) bv[n] = CENTRED ? Ys[yrow + koff + n * 256] : Ys[yrow + koff + n * 256] - mk;
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], bv[n], acc[m][n], 0, 0, 0);
-    }
-  }
-  double* dst = work + (int64_t)sp * slab;
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int gi = i0 + wr * 64 + m * 16 + fk + 4 * reg;
-        const int gj = j0 + wc * 64 + n * 16 + fr;
-        if (gi < ns && gj <= gi) dst[(int64_t)gi * ldc + gj] = acc[m][n][reg];
-      }
-}
-
-// SYRK v3: one 128 x 128 tile per 256-thread workgroup, TWO workgroups per CU (2-stage
-// LDS-DMA ring, 66.5 KB each): the two workgroups' K-tile barriers are independent, so one
-// keeps the fp64 MFMA pipe fed while the other waits at its barrier (v2 stalls all 8 waves of
-// its single workgroup at every barrier).  Same operand layout, swizzle, mean slot and
-// lower-triangle partial output as v2; 4 waves as 2 x 2, each 64 x 64.
+// Split-K SYRK: one 128 x 128 tile of the lower triangle per 256-thread workgroup, TWO
+// workgroups per CU.  Operands are streamed by LDS-DMA (global_load_lds_dwordx4) into a
+// 2-stage ring (66.5 KB per workgroup); counted vmcnt + raw s_barrier keep the next K-tile in
+// flight across the barrier.  The two workgroups' K-tile barriers are independent, so one keeps
+// the fp64 MFMA pipe fed while the other waits at its barrier (one 512-thread 256 x 128
+// workgroup per CU stalled all 8 waves at every barrier: 53.0 against 50.8 ms at C3).  The
+// K-tiled A makes each (panel, K-tile) operand one contiguous block; rows are XOR-swizzled on
+// the SOURCE address (double2 slot j of row R holds logical slot j ^ ((R>>1)&7)) so the MFMA
+// fragment reads are bank-conflict free.  CENTRED = 1: A was centred in place (k_center), so
+// the fragments go to the MFMAs as read; CENTRED = 0 subtracts the mean slot at fragment read
+// (57.0 against 52.9 ms).  4 waves as 2 x 2, each 64 x 64 = 4 x 4 blocks of
+// v_mfma_f64_16x16x4_f64.  Partial tiles go to slab `split`; k_syrk_reduce sums the slabs in
+// split order (deterministic).
 namespace syrk3 {
 constexpr int BM = 128, BN = 128, KT = 16, NST = 2, NW = 4;
 constexpr int XB = BM * KT * 8;            // 16 KB
@@ -1378,12 +1090,8 @@ hipError_t launch_mt_jump(const uint32_t* src, const int* src_idx, const uint32_
                           const int* poly_idx, uint32_t* dst, const int* dst_idx, int njobs,
                           hipStream_t st) {
   if (njobs <= 0) return hipSuccess;
-  if (std::getenv("PODS_MT_JUMP_BITS") == nullptr)  // default: the 3-bit window table
-    hipLaunchKernelGGL(k_mt_jump3, dim3(njobs), dim3(256), 0, st, src, src_idx, polys, poly_idx, dst,
-                       dst_idx, njobs);
-  else
-    hipLaunchKernelGGL(k_mt_jump, dim3(njobs), dim3(256), 0, st, src, src_idx, polys, poly_idx, dst,
-                       dst_idx, njobs);
+  hipLaunchKernelGGL(k_mt_jump3, dim3(njobs), dim3(256), 0, st, src, src_idx, polys, poly_idx, dst,
+                     dst_idx, njobs);
   return hipGetLastError();
 }
 
@@ -1396,7 +1104,7 @@ hipError_t launch_mt_generate(const uint32_t* states, int G, int64_t Bs, int64_t
     hipLaunchKernelGGL(k_mt_generate_full, dim3(G), dim3(256), 0, st, states, G, Bs, ntot, low, range, out);
     return hipGetLastError();
   }
-  if (S >= 312 && std::getenv("PODS_MT_GENERIC") == nullptr) {
+  if (S >= 312) {
     hipLaunchKernelGGL(k_mt_generate_slab, dim3(G), dim3(256), 0, st, states, G, Bs, ntot, S, Kp, rlo, rhi,
                        Sl, low, range, out);
     return hipGetLastError();
@@ -1409,16 +1117,14 @@ hipError_t launch_mt_generate(const uint32_t* states, int G, int64_t Bs, int64_t
 template <int NX>
 static hipError_t launch_fx(const double* R, const double* bx, int ns, int64_t Sl, int ncomp,
                             int chunk, double* T1, hipStream_t st) {
-  if (Sl % 2 == 0 && ((uintptr_t)R & 15) == 0 && ((uintptr_t)T1 & 15) == 0 &&
-      std::getenv("PODS_FX_SCALAR") == nullptr) {
+  if (Sl % 2 == 0 && ((uintptr_t)R & 15) == 0 && ((uintptr_t)T1 & 15) == 0) {
     // point pairs: half the threads, so twice the step chunks keep the same parallelism
     // with PD loads in flight per wave, about four resident workgroups per CU suffice: step
     // chunks so the grid is one round of ~1024 workgroups (a partial second round of a
     // longer grid left most CUs idle at the end)
     (void)chunk;
     const int64_t bx_ = (Sl / 2 + 255) / 256;
-    const char* env = std::getenv("PODS_FX_WG");
-    const int64_t want = env ? std::max(1, std::atoi(env)) : 1024;
+    const int64_t want = 1024;
     const int64_t nch0 = std::max<int64_t>(1, std::min<int64_t>(ns, want / std::max<int64_t>(1, bx_ * ncomp)));
     const int chunk2 = (int)((ns + nch0 - 1) / nch0);
     const int nch = (ns + chunk2 - 1) / chunk2;
@@ -1453,12 +1159,10 @@ hipError_t launch_filter_x(int NX, const double* R, const double* bx, int ns, in
 // fit (K <= 256): two workgroups per CU (LDS ~58 KB each), so one block's loads overlap the
 // other's filter arithmetic -- worth more than the 32-row tile's smaller halo (1.375 vs
 // 1.75 reads per output row), whose 97 KB of LDS allowed one block per CU.
-// PODS_YZ_TILE=32 selects the 32 x 512 tile.
+// (The 32 x 512 tile for K <= 256 measured 12.2 against 11.2 ms of generation at C3.)
 static int yz_tj(int K) {
   const int kch = (K + 15) / 16;
-  const char* env = std::getenv("PODS_YZ_TILE");
-  const bool force32 = env && env[0] == '3';
-  if (!force32 && 16 * kch <= 256) return 16256;
+  if (16 * kch <= 256) return 16256;
   if (32 * kch <= 512) return 32;
   if (16 * kch <= 512) return 16;
   if (8 * kch <= 512) return 8;
@@ -1480,12 +1184,8 @@ static hipError_t launch_fyz_t(const double* T1, const double* by, const double*
   const int tiles = (jl + TJ - 1) / TJ;
   const int nsb = (int)std::max<int64_t>(1, std::min<int64_t>(16, (int64_t)tiles * ns / 512));
   const dim3 grid((unsigned)tiles, (unsigned)((ns + nsb - 1) / nsb));
-  // opt-in (PODS_YZ_REMAP=1): at C3 it cuts the kernel's HBM traffic 18.4 -> 14.5 GB at the same
-  // time, at C4 (32 tiles per step group, 512-thread blocks) generation measured ~4 ms slower
-  const char* remap_env = std::getenv("PODS_YZ_REMAP");
-  const int xcd_remap = remap_env != nullptr && remap_env[0] == '1';
   hipLaunchKernelGGL((k_filter_yz<TJ, NY, NZC, NT>), grid, dim3(NT), lds, st, T1, by, bz, NZ, ns, jl, K,
-                     Kp, Sl, ncomp, lund, lund_sj, lund_mode, rot, rotate, AT, nsb, xcd_remap);
+                     Kp, Sl, ncomp, lund, lund_sj, lund_mode, rot, rotate, AT, nsb);
   return hipGetLastError();
 }
 
@@ -1554,21 +1254,13 @@ hipError_t launch_center(double* AT, int64_t rowpad, int ns, const double* mean,
   return hipGetLastError();
 }
 
-// Number of K splits for `tiles` work tiles on `slots` concurrent workgroups: ~8+ rounds,
-// chosen to minimise the partial last round, >= 64 K-tiles of 16 per item.
-int syrk_plan(int kernel, int ns, int64_t Kdim, int64_t* ksplit) {
+// Number of K splits for the 128 x 128 lower-triangle tiles on 512 concurrent workgroups
+// (two per CU): ~8+ rounds, chosen to minimise the partial last round, >= 64 K-tiles of 16
+// per item.
+int syrk_plan(int ns, int64_t Kdim, int64_t* ksplit) {
   constexpr int KT = 16;
-  int tiles, slots;
-  if (kernel == 2) {
-    const int nbi = (ns + 255) / 256, nbj = (ns + 127) / 128;
-    tiles = 0;
-    for (int bi = 0; bi < nbi; ++bi) tiles += std::min(2 * bi + 2, nbj);
-    slots = 256;
-  } else {
-    const int nb = (ns + 127) / 128;
-    tiles = nb * (nb + 1) / 2;
-    slots = 512;
-  }
+  const int nb = (ns + 127) / 128;
+  const int tiles = nb * (nb + 1) / 2, slots = 512;
   const int64_t kts = Kdim / KT;
   const int64_t maxsplit = std::max<int64_t>(1, kts / 64);
   int64_t best = 1;
@@ -1589,55 +1281,22 @@ int syrk_plan(int kernel, int ns, int64_t Kdim, int64_t* ksplit) {
   return (int)std::max<int64_t>(1, nsplit);
 }
 
-
-hipError_t launch_syrk(int kernel, const double* AT, int64_t ld, int ns, int64_t Kdim,
-                       const double* mean, const int* items, int nitems, int nsplit, int64_t ksplit,
-                       double* C, int64_t ldc, int divide, double* work, int centred, hipStream_t st) {
+hipError_t launch_syrk(const double* AT, int ns, int64_t Kdim, const double* mean, const int* items, int nitems,
+                       int nsplit, int64_t ksplit, double* C, int64_t ldc, int divide, double* work, int centred,
+                       hipStream_t st) {
   const int64_t slab = (int64_t)ns * ldc;
-  const int final_write = nsplit == 1;
-  if (kernel == 3) {
-    auto launch = [&](auto kern) -> hipError_t {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         syrk3::NST * syrk3::STAGE);
-      if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(kern, dim3(nitems), dim3(256), syrk3::NST * syrk3::STAGE, st, AT, ns, Kdim,
-                         mean, reinterpret_cast<const int4*>(items), nitems, ksplit, work, ldc, slab);
-      return hipGetLastError();
-    };
-    hipError_t le = centred ? launch(k_syrk_g128<1>) : launch(k_syrk_g128<0>);
-    if (le != hipSuccess) return le;
-    hipLaunchKernelGGL(k_syrk_reduce, dim3(((ns + 63) / 64) * ((ns + 63) / 64 + 1) / 2), dim3(256), 0, st, work, nsplit, slab,
-                       ns, ldc, C, divide);
-    return hipGetLastError();
-  }
-  if (kernel == 2) {
-    auto launch = [&](auto kern) -> hipError_t {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         syrk2::NST * syrk2::STAGE);
-      if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(kern, dim3(nitems), dim3(512), syrk2::NST * syrk2::STAGE, st, AT, ns, Kdim,
-                         mean, reinterpret_cast<const int4*>(items), nitems, ksplit, work, ldc, slab);
-      return hipGetLastError();
-    };
-    hipError_t le = centred ? launch(k_syrk_glds<1>) : launch(k_syrk_glds<0>);
-    if (le != hipSuccess) return le;
-    hipError_t e = hipGetLastError();
+  auto launch = [&](auto kern) -> hipError_t {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, syrk3::NST * syrk3::STAGE);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_syrk_reduce, dim3(((ns + 63) / 64) * ((ns + 63) / 64 + 1) / 2), dim3(256), 0, st, work, nsplit, slab,
-                       ns, ldc, C, divide);
+    hipLaunchKernelGGL(kern, dim3(nitems), dim3(256), syrk3::NST * syrk3::STAGE, st, AT, ns, Kdim, mean,
+                       reinterpret_cast<const int4*>(items), nitems, ksplit, work, ldc, slab);
     return hipGetLastError();
-  } else {
-    constexpr int BT = 128, KT = 16;
-    hipLaunchKernelGGL((k_syrk_split<BT, KT>), dim3(nitems), dim3(256), 0, st, AT, ld, ns, Kdim, mean,
-                       reinterpret_cast<const int4*>(items), nitems, ksplit, final_write ? C : work, ldc,
-                       slab, final_write, divide);
-  }
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || final_write) return e;
-  hipLaunchKernelGGL(k_syrk_reduce, dim3(((ns + 63) / 64) * ((ns + 63) / 64 + 1) / 2), dim3(256), 0, st, work, nsplit, slab,
-                     ns, ldc, C, divide);
+  };
+  hipError_t le = centred ? launch(k_syrk_g128<1>) : launch(k_syrk_g128<0>);
+  if (le != hipSuccess) return le;
+  hipLaunchKernelGGL(k_syrk_reduce, dim3(((ns + 63) / 64) * ((ns + 63) / 64 + 1) / 2), dim3(256), 0, st, work,
+                     nsplit, slab, ns, ldc, C, divide);
   return hipGetLastError();
 }
 

@@ -659,192 +659,16 @@ __global__ void k_band(const double* __restrict__ A, int64_t lda, int n, double*
 }
 
 // ---------------------------------------------------------------------------------------
-// Stage 2: k_sbtrd<B>.  One wave per workgroup; workgroup g runs sweeps g, g + NG, ...
+// Stage 2, windowed: k_sbtrd_win<B, G>.  Bulge chasing in tasks (s, k):
 // Task (s, k): rows R_k = [r0, r1), r0 = s+1+k*B (k = 0: the column s itself is the target);
 // the Householder annihilates A[r0+1:r1, col] (col = s for k = 0, else the first column of
 // the previous bulge, s+1+(k-1)*B) and is applied to A[R_k, col:r0] (left), A[R_k, R_k]
-// (both sides) and A[r1:r1+B, R_k] (right; the new bulge).  prog[s] counts finished tasks of
-// sweep s (0x7fffffff when done); task (s, k) waits for prog[s-1] >= k + 3.
-// Band entries are read and written with agent-scope (L2-bypassing) accesses: the tasks of
-// one region run on different CUs one after another.
-// ---------------------------------------------------------------------------------------
-template <int B>
-__global__ __launch_bounds__(64, 1) void k_sbtrd(double* __restrict__ band, int n, int NG,
-                                                 uint32_t* __restrict__ prog, uint32_t* __restrict__ abortw,
-                                                 int64_t* __restrict__ trace, int trace_s) {
-  static_assert(B == 32, "k_sbtrd maps a 32 x 32 block onto one wave (lane = column, half of the rows)");
-  constexpr int LDB = 2 * B, H = B / 2;
-  constexpr uint32_t DONE = 0x7fffffffu;
-  __shared__ double Ds[B][B + 1];  // the diagonal block, both triangles
-  __shared__ double vs[B];
-  const int lane = threadIdx.x, c = lane & (B - 1), h = lane >> 5;
-  auto idx = [&](int r, int cc) -> int { return cc * LDB + (r - cc); };
-  const __amdgpu_buffer_rsrc_t rb = rsrc(band, (int64_t)n * LDB);
-  // lane (c, h) holds rows [16h, 16h+16) of column c of each block:
-  //   L[i][c] (rows R_k, column col + c), D[i][c] (column r0 + c), R[c][j] (row r1 + c, j in its half)
-  // operand loads batch (no volatile bit: the flag poll above them ends in a compiler barrier);
-  // sc1 stores write through, so the next sweep's workgroup on another XCD sees them
-  auto ld = [&](int idx) -> double {
-    const auto q = __builtin_amdgcn_raw_buffer_load_b64(rb, idx * 8, 0, 16u);
-    return __builtin_bit_cast(double, q);
-  };
-  auto st = [&](int idx, double v) {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(rb, 0, 0, 0)), v),
-                                          rb, idx * 8, 0, 16u);
-  };
-  for (int s = blockIdx.x; s < n - 2; s += NG) {
-    for (int k = 0;; ++k) {
-      const int r0 = s + 1 + k * B;
-      if (r0 >= n - 1) break;
-      const int r1 = min(r0 + B, n), len = r1 - r0;
-      const int col = k == 0 ? s : s + 1 + (k - 1) * B;
-      const int nl = r0 - col;
-      const int r2 = min(r1 + B, n), nr = r2 - r1;
-      int64_t* tr = (trace && s == trace_s && lane == 0 && k < 256) ? trace + k * 6 : nullptr;
-      if (tr) tr[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
-      if (s > 0 && lane == 0) {
-        int spin = 0;
-        for (;;) {
-          const uint32_t p = ld_f(prog + s - 1);
-          if (p == DONE || p >= (uint32_t)(k + 3)) break;
-          if (++spin > SPIN_LIMIT) {
-            st_f(abortw, 1u);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-      asm volatile("" ::: "memory");  // the operand loads stay behind the poll
-      if (tr) tr[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
-      // ---- loads (all issued, one wait) -------------------------------------------------
-      double L[H], D[H], R[H];
-#pragma unroll
-      for (int q = 0; q < H; ++q) {
-        const int i = H * h + q;
-        L[q] = (c < nl && i < len) ? ld(idx(r0 + i, col + c)) : 0.0;
-        D[q] = (c < len && i < len && i >= c) ? ld(idx(r0 + i, r0 + c)) : 0.0;
-        R[q] = (c < nr && i < len) ? ld(idx(r1 + c, r0 + i)) : 0.0;  // R[c][j = i]
-      }
-#pragma unroll
-      for (int q = 0; q < H; ++q) {  // the upper triangle of D from the lower one
-        const int i = H * h + q;
-        if (i >= c) Ds[i][c] = D[q];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int q = 0; q < H; ++q) {
-        const int i = H * h + q;
-        if (i < c && c < len) D[q] = Ds[c][i];
-      }
-      if (tr) {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        tr[2] = (int64_t)__builtin_amdgcn_s_memrealtime();
-      }
-      // ---- Householder of x = L[:, 0] (column col) --------------------------------------
-      const double x0 = __shfl(L[0], 0);  // lane 0 = (c 0, h 0): row 0
-      double sq = 0.0;
-      if (c == 0) {
-#pragma unroll
-        for (int q = 0; q < H; ++q) {
-          const int i = H * h + q;
-          if (i >= 1) sq = fma(L[q], L[q], sq);
-        }
-      }
-      sq += __shfl_xor(sq, 32);
-      sq = __shfl(sq, 0);
-      double beta = x0, tau = 0.0, scal = 0.0;
-      if (sq != 0.0) {
-        beta = -copysign(sqrt(fma(x0, x0, sq)), x0);
-        tau = (beta - x0) / beta;
-        scal = 1.0 / (x0 - beta);
-      }
-      if (c == 0) {
-#pragma unroll
-        for (int q = 0; q < H; ++q) {
-          const int i = H * h + q;
-          if (i < len) vs[i] = i == 0 ? 1.0 : L[q] * scal;
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      double v[H];
-#pragma unroll
-      for (int q = 0; q < H; ++q) {
-        const int i = H * h + q;
-        v[q] = i < len ? vs[i] : 0.0;
-      }
-      // ---- left: column c of rows R_k -----------------------------------------------------
-      {
-        double d = 0.0;
-#pragma unroll
-        for (int q = 0; q < H; ++q) d = fma(v[q], L[q], d);
-        d += __shfl_xor(d, 32);
-        const double f = tau * d;
-#pragma unroll
-        for (int q = 0; q < H; ++q) {
-          const int i = H * h + q;
-          L[q] = c == 0 ? (i == 0 ? beta : 0.0) : fma(-f, v[q], L[q]);
-        }
-      }
-      // ---- both sides on D: p = tau D v, w = p - 1/2 tau (p.v) v, D -= v w^T + w v^T -------
-      {
-        // p_c = tau sum_i D[i][c] v_i (D symmetric: column c = row c)
-        double pc = 0.0;
-#pragma unroll
-        for (int q = 0; q < H; ++q) pc = fma(D[q], v[q], pc);
-        pc += __shfl_xor(pc, 32);
-        pc *= tau;
-        const double vc = c < len ? vs[c] : 0.0;
-        double pv = h == 0 ? pc * vc : 0.0;
-        for (int o = 16; o >= 1; o >>= 1) pv += __shfl_xor(pv, o);
-        pv += __shfl_xor(pv, 32);
-        const double wc = fma(-0.5 * tau * pv, vc, pc);  // w_c
-        if (h == 0 && c < len) Ds[0][c] = wc;             // reuse row 0 of Ds as the w vector
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int q = 0; q < H; ++q) {
-          const int i = H * h + q;
-          const double wi = i < len ? Ds[0][i] : 0.0;
-          D[q] = D[q] - v[q] * wc - wi * vc;
-        }
-      }
-      // ---- right: row r1 + c times H: R[c][j] -= tau (R[c] . v) v_j ------------------------
-      {
-        double d = 0.0;
-#pragma unroll
-        for (int q = 0; q < H; ++q) d = fma(R[q], v[q], d);
-        d += __shfl_xor(d, 32);
-        const double f = tau * d;
-#pragma unroll
-        for (int q = 0; q < H; ++q) R[q] = fma(-f, v[q], R[q]);
-      }
-      if (tr) tr[3] = (int64_t)__builtin_amdgcn_s_memrealtime();
-      // ---- stores (lower triangle of D) -------------------------------------------------
-#pragma unroll
-      for (int q = 0; q < H; ++q) {
-        const int i = H * h + q;
-        if (c < nl && i < len) st(idx(r0 + i, col + c), L[q]);
-        if (c < len && i < len && i >= c) st(idx(r0 + i, r0 + c), D[q]);
-        if (c < nr && i < len) st(idx(r1 + c, r0 + i), R[q]);
-      }
-      drain();
-      __builtin_amdgcn_wave_barrier();
-      if (tr) tr[4] = (int64_t)__builtin_amdgcn_s_memrealtime();
-      if (lane == 0) st_f(prog + s, (uint32_t)(k + 1));
-    }
-    drain();
-    if (lane == 0) st_f(prog + s, DONE);
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// Stage 2, windowed: k_sbtrd_win<B, G>.  The tasks (s, k) of k_sbtrd with its arithmetic,
-// scheduled so the chase runs out of LDS:
+// (both sides) and A[r1:r1+B, R_k] (right; the new bulge).
+// Task (s, k) follows (s-1, k+2).  (One wave per task over L2, each task handed off through
+// memory, took 198 against ~100 ms at n = 8192.)  The tasks are scheduled so the chase runs
+// out of LDS:
 //   * a workgroup runs a GROUP of G consecutive sweeps s0 .. s0+G-1 in lock step: at step
-//     tau, task wave g runs task (s0+g, tau - 3g).  The 3-task lag is k_sbtrd's dependency
+//     tau, task wave g runs task (s0+g, tau - 3g).  The 3-task lag is the chase's dependency
 //     ((s, k) after (s-1, k+2)) and the tasks of one step touch disjoint band elements, so
 //     one workgroup barrier per step orders everything;
 //   * the group's band columns live in an LDS ring of W = 8B column slots of 64 doubles
@@ -1528,9 +1352,7 @@ hipError_t launch_syevd2(const double* C, int n, int nvec, double* ws, const Sye
   if (e != hipSuccess) return e;
   int64_t vxo = 0;
   int pi = 0;
-  const char* lim = std::getenv("PODS_SY2SB_PANELS");  // diagnostics: stop stage 1 early
-  const int maxp = lim ? std::atoi(lim) : 1 << 30;
-  for (int c0 = 0; c0 < n - B - 1 && pi < maxp; c0 += B, ++pi) {
+  for (int c0 = 0; c0 < n - B - 1; c0 += B, ++pi) {
     const int r0 = c0 + B, m = n - r0;
     double* Vx = ws + p.off_vx + vxo;
     double* T = ws + p.off_t + (int64_t)pi * B * B;
@@ -1597,22 +1419,7 @@ hipError_t launch_syevd2(const double* C, int n, int nvec, double* ws, const Sye
   hipLaunchKernelGGL(sb::k_band<B>, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, Aw, (int64_t)n, n, band);
   e = hipMemcpyAsync(band0, band, (size_t)nb * sizeof(double), hipMemcpyDeviceToDevice, st);
   if (e != hipSuccess) return e;
-  const int NG = std::max(1, std::min(256, n - 2));
-  // PODS_SBTRD_TRACE=s: per-task timestamps of sweep s (diagnostics, printed to stderr)
-  const char* trs = std::getenv("PODS_SBTRD_TRACE");
-  int64_t* trace = nullptr;
-  if (trs) {
-    e = hipMallocAsync(reinterpret_cast<void**>(&trace), 256 * 6 * sizeof(int64_t), st);
-    if (e != hipSuccess) return e;
-    e = hipMemsetAsync(trace, 0, 256 * 6 * sizeof(int64_t), st);
-    if (e != hipSuccess) return e;
-  }
-  if (n > 2 && (trs || std::getenv("PODS_SBTRD_OLD"))) {  // the per-task chase over L2 (diagnostics)
-    e = check_persistent(reinterpret_cast<const void*>(&sb::k_sbtrd<B>), 64, 0, NG);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(sb::k_sbtrd<B>, dim3(NG), dim3(64), 0, st, band, n, NG, prog, abortw + 1, trace,
-                       trs ? std::atoi(trs) : -1);
-  } else if (n > 2) {
+  if (n > 2) {
     constexpr int GW = 2;
     using SW = sb::SbWin<B, GW>;
     const int ngroups = (n - 2 + GW - 1) / GW;
@@ -1675,22 +1482,6 @@ hipError_t launch_syevd2(const double* C, int n, int nvec, double* ws, const Sye
       }
     }
   }
-  if (trace) {
-    int64_t h[256 * 6];
-    e = hipMemcpyAsync(h, trace, sizeof(h), hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    (void)hipFreeAsync(trace, st);
-    if (e != hipSuccess) return e;
-    double acc[4] = {0, 0, 0, 0};
-    int cnt = 0;
-    for (int k = 1; k < 256 && h[k * 6] != 0 && h[k * 6 + 4] != 0; ++k) {
-      for (int q = 0; q < 4; ++q) acc[q] += (double)(h[k * 6 + q + 1] - h[k * 6 + q]) * 0.01;
-      ++cnt;
-    }
-    std::fprintf(stderr, "sbtrd trace sweep %s: %d tasks, per task us: wait %.2f load %.2f compute %.2f store+drain %.2f; task-to-task %.2f\n",
-                 trs, cnt, acc[0] / std::max(cnt, 1), acc[1] / std::max(cnt, 1), acc[2] / std::max(cnt, 1),
-                 acc[3] / std::max(cnt, 1), cnt > 1 ? (double)(h[cnt * 6] - h[6]) * 0.01 / (cnt - 1) : 0.0);
-  }
   double* D = ws + p.off_de;
   double* E = D + n;
   double* bounds = D + 2 * (int64_t)n;
@@ -1702,7 +1493,6 @@ hipError_t launch_syevd2(const double* C, int n, int nvec, double* ws, const Sye
   e = launch_orth(lam_desc, bounds, n, nvec, vec, nvec, st);
   if (e != hipSuccess) return e;
   // Y <- Q_0 Q_1 ... Q_{np-1} Y
-  if (std::getenv("PODS_SY2SB_NOBT")) return hipGetLastError();  // diagnostics: band eigenvectors
   for (int q = p.np - 1; q >= 0; --q) {
     int64_t off = 0;
     for (int r = 0; r < q; ++r) off += (int64_t)(n - r * B - B) * B;

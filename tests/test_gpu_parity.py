@@ -79,16 +79,13 @@ def ctx():
     c.close()
 
 
-@pytest.mark.parametrize("jump", ["window3", "per_bit", "window3_long_substreams"])
-def test_rng_stream_bit_exact(ctx, monkeypatch, jump):
-    """numpy's legacy MT19937 stream bit for bit, through both jump-ahead kernels
-    (k_mt_jump3, the default, and k_mt_jump behind PODS_MT_JUMP_BITS; read at launch), and
-    with a different substream layout (PODS_MT_SUBSTREAMS=64: twice the blocks per substream)."""
-    monkeypatch.delenv("PODS_MT_JUMP_BITS", raising=False)
+@pytest.mark.parametrize("layout", ["default", "long_substreams"])
+def test_rng_stream_bit_exact(ctx, monkeypatch, layout):
+    """numpy's legacy MT19937 stream bit for bit through the jump-ahead (k_mt_jump3) and the
+    generator, with the default substream layout and a different one (PODS_MT_SUBSTREAMS=64:
+    twice the blocks per substream)."""
     monkeypatch.delenv("PODS_MT_SUBSTREAMS", raising=False)
-    if jump == "per_bit":
-        monkeypatch.setenv("PODS_MT_JUMP_BITS", "1")
-    elif jump == "window3_long_substreams":
+    if layout == "long_substreams":
         monkeypatch.setenv("PODS_MT_SUBSTREAMS", "64")
     lib = ctx.lib
     for seed, n in [(12345, 1000), (7, 3_000_001), (2**32 - 1, 25_000_000)]:
@@ -226,12 +223,9 @@ def test_fourier_rank_matches_host(ctx, et):
         assert np.array_equal(E.fc_rows(c, ci, cc), ref_FC), ns
 
 
-@pytest.mark.parametrize("kernel", ["3", "2", "1"])
-def test_syrk_mfma_layout(ctx, monkeypatch, kernel):
+def test_syrk_mfma_layout(ctx):
     """Asymmetric data through pods_set_snapshots: catches row/col swaps in the MFMA C map,
-    for each SYRK kernel (3: 128x128 tiles, two workgroups per CU, the default; 2: 256x128;
-    1: register-staged), including a case with several tile rows and K splits."""
-    monkeypatch.setenv("PODS_SYRK_KERNEL", kernel)
+    including a case with several tile rows and K splits."""
     rng = np.random.default_rng(3)
     for ns, rows in [(64, 300), (100, 1000), (130, 77), (1, 5), (300, 5000)]:
         A = rng.standard_normal((rows, ns)) * np.arange(1, ns + 1)[None, :] + np.arange(rows)[:, None]
@@ -300,24 +294,10 @@ def test_center_in_place(ctx):
 
 
 @pytest.mark.parametrize("kw", [dict(jma=32, kma=32, ns=64, seed=12345),
-                                dict(jma=40, kma=27, ns=30, seed=5, normal=(1.0, -0.4, 0.2)),
-                                dict(jma=256, kma=256, ns=24, seed=4242)])
-def test_generate_fused_xyz_opt_in(ctx, monkeypatch, kw):
-    """The opt-in fused x+y+z generator pass (PODS_GEN_FUSED=1, k_filter_xyz: no x-filtered
-    planes in HBM) is bit-exact against the oracle: full tiles, ragged edge tiles (40 x 27) with
-    a rotated normal, and the 256^2 inlet."""
-    monkeypatch.setenv("PODS_GEN_FUSED", "1")
-    A = E.Generator(podsgen.DFSetup(**kw), ctx=ctx).generate().to_host()
-    assert np.array_equal(A, O.generate(O.DFConfig(**kw)))
-
-
-@pytest.mark.parametrize("kw", [dict(jma=40, kma=27, ns=30, seed=5, normal=(1.0, -0.4, 0.2)),
-                                dict(jma=256, kma=256, ns=40, seed=4242)])
-def test_generate_yz_xcd_order_opt_in(ctx, monkeypatch, kw):
-    """The opt-in XCD-aware block order of the y/z pass (PODS_YZ_REMAP=1) only renumbers
-    independent blocks: generation stays bit-exact against the oracle (ragged tiles and a grid
-    whose block count is not a multiple of 8, and the 256^2 inlet)."""
-    monkeypatch.setenv("PODS_YZ_REMAP", "1")
+                                dict(jma=40, kma=27, ns=30, seed=5, normal=(1.0, -0.4, 0.2))])
+def test_generate_ragged_tiles_vs_oracle(ctx, kw):
+    """Generation bit-exact against the oracle on full tiles and ragged edge tiles (40 x 27)
+    with a rotated normal."""
     A = E.Generator(podsgen.DFSetup(**kw), ctx=ctx).generate().to_host()
     assert np.array_equal(A, O.generate(O.DFConfig(**kw)))
 
