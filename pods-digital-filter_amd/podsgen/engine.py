@@ -239,25 +239,39 @@ class SpectrumQueue:
     Nothing in a step consumes eigenvalues past lambda_{nm-1}, so the eigenvalues-only
     tridiagonalisation of step s (pods_eigvals_*, 33 ms at ns = 4096) runs on an owner rank,
     spread over that rank's following steps in units of one 512-column range (the bisection is
-    the last unit).  Owners rotate over ranks 1..world-1 from world 3 on (rank 0 carries the
-    leading-pair solve and the DFT), over all ranks below that.  Each owner runs units while it
-    has time credit: every step adds (total cost / owners), every unit spends its estimated
-    cost (UNIT_MS, measured at ns = 4096), so the per-step load evens out at the average.
-    drain() runs what is left (inside a caller's timed region); results() returns {step:
-    eigenvalues} for the steps this rank owned.  ns <= 4096; beyond that each owner solves its
-    step at once (pods_syev2, no vectors)."""
+    the last unit).  Per-step budgets even out the ranks' extra work: rank 0 already carries
+    the leading-pair solve, the DFT and the ranking (LEAD_MS), so with E the cost of one
+    spectrum and T = (E + LEAD_MS) / world, rank 0 gets max(0, T - LEAD_MS) and the others
+    share the rest equally (rank 0 gets none from world ~8 on at C3).  Step s is owned by the
+    rank a smooth weighted round robin over those budgets picks (the same sequence on every
+    rank), and each rank runs units while it has time credit: every step adds its budget,
+    every unit spends its measured cost (UNIT_MS at ns = 4096).  Ranks other than 0 run their
+    units while rank 0 solves (run_pod submits before the broadcast there).  drain() runs what
+    is left (inside a caller's timed region); results() returns {step: eigenvalues} for the
+    steps this rank owned.  ns <= 4096; beyond that each owner solves its step at once
+    (pods_syev2, no vectors)."""
 
     # per-unit time (ms) of k_trd column ranges 0..7 and the bisection at ns = 4096
     # (profiles/r3/c3_kernel_stats.csv); used only to even out the per-step load
     UNIT_MS = [7.8, 5.5, 4.6, 4.0, 3.0, 2.9, 2.5, 2.2, 1.6]
+    # rank 0's own extra work per step at ns = 4096 (leading pairs 5.0, DFT + ranking ~1 ms)
+    LEAD_MS = 6.0
 
     def __init__(self, ctx, ns, rank=0, world=1, max_slots=16):
         self.ctx, self.ns, self.rank, self.world = ctx, ns, rank, world
         self.units = (ns - 1) // 512 + 2
         self.cost = (self.UNIT_MS if self.units == len(self.UNIT_MS)
                      else [1.0] * self.units)
-        self.owners = list(range(1, world)) if world >= 3 else list(range(world))
-        self.budget = sum(self.cost) / len(self.owners)
+        E = sum(self.cost)
+        lead = self.LEAD_MS * (ns / 4096.0) ** 2 * sum(self.cost) / sum(self.UNIT_MS)
+        if world == 1:
+            self.budgets = [E]
+        else:
+            b0 = max(0.0, (E + lead) / world - lead)
+            self.budgets = [b0] + [(E - b0) / (world - 1)] * (world - 1)
+        self.owners = [r for r in range(world) if self.budgets[r] > 0.0]
+        self.budget = self.budgets[rank]
+        self._seq, self._cur = [], [0.0] * world
         self.credit = 0.0
         self.max_slots = max_slots
         self.pending = []      # [step, slot, next unit, lam tensor]
@@ -265,7 +279,16 @@ class SpectrumQueue:
         self.step_no = 0
 
     def owner(self, step):
-        return self.owners[step % len(self.owners)]
+        """The rank that solves step `step`'s spectrum: smooth weighted round robin over the
+        budgets (deterministic, identical on every rank)."""
+        total = sum(self.budgets)
+        while len(self._seq) <= step:
+            for r in range(self.world):
+                self._cur[r] += self.budgets[r]
+            pick = max(range(self.world), key=lambda r: (self._cur[r], -r))
+            self._cur[pick] -= total
+            self._seq.append(pick)
+        return self._seq[step]
 
     def _slot(self):
         used = {p[1] for p in self.pending}
@@ -280,8 +303,7 @@ class SpectrumQueue:
         self.step_no += 1
         lib = self.ctx.lib
         with tm("eig_full"):
-            if self.rank in self.owners:
-                self.credit += self.budget
+            self.credit += self.budget
             if self.owner(s) == self.rank:
                 if self.ns > SYEV_MAX_N:
                     self.finished[s] = eigvals_full(self.ctx, C, self.ns)
@@ -451,6 +473,8 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
     meta = torch.zeros(4, dtype=torch.int64, device=dev)
     T = lam_desc = nvalid = None
     defer = spectrum is not None
+    if defer and rank != 0:   # this rank's spectrum units run while rank 0 solves
+        spectrum.submit(C, timer)
     if rank == 0:
         lam_desc, nvalid, nmt, T, lam_modes = eigen_solve(ctx, C, ns, nm, tol_CN, full_temporal, tm, world,
                                                           defer_full=defer)
@@ -488,7 +512,7 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
         with tm("spatial"):
             check(lib.pods_spatial_modes(ctx.h, ptr(Tsel), ldT, ptr(np.ascontiguousarray(lam_modes[:nmt])),
                                          nmt, ptr(phi)), "pods_spatial_modes")
-    if defer:  # the full spectrum, spread over this and the following steps (SpectrumQueue)
+    if defer and rank == 0:  # the full spectrum, spread over the following steps (SpectrumQueue)
         spectrum.submit(C, timer)
     return PODResult(energy=lam_desc, num_valid=nvalid, nm=nmt, mean=mean, T=T, phi=phi[:, :nmt],
                      C=C if keep_C else None)

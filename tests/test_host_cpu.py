@@ -374,3 +374,28 @@ def test_num_valid_modes_vectorised_matches_reference_loop():
                     e = np.abs(rng.standard_normal(ns))
                 for tol in (1e-15, 1e-3, 0.5):
                     assert num_valid_modes(e, ns, tol) == num_valid_modes_loop(e, ns, tol), (ns, tol, trial)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_spectrum_queue_ownership(world):
+    """SpectrumQueue's owner sequence (host logic, no device): identical on every rank, shares
+    of the spectra proportional to the per-step budgets, rank 0 (which carries the leading-pair
+    solve) owning less than the others and none at world 8 (C3 costs)."""
+    from podsgen import engine as E
+
+    class _Ctx:
+        lib = None
+
+    qs = [E.SpectrumQueue(_Ctx(), 4096, r, world) for r in range(world)]
+    seq = [qs[0].owner(s) for s in range(400)]
+    for q in qs[1:]:
+        assert [q.owner(s) for s in range(400)] == seq
+    b = qs[0].budgets
+    assert abs(sum(b) - sum(E.SpectrumQueue.UNIT_MS)) < 1e-9
+    counts = np.bincount(seq, minlength=world)
+    for r in range(world):
+        assert abs(counts[r] / 400 - b[r] / sum(b)) <= 0.01, (r, counts, b)
+    if world > 1:
+        assert b[0] < b[1]
+    if world == 8:
+        assert counts[0] == 0
