@@ -245,8 +245,9 @@ class SpectrumQueue:
     share the rest equally (rank 0 gets none from world ~8 on at C3).  Step s is owned by the
     rank a smooth weighted round robin over those budgets picks (the same sequence on every
     rank), and each rank runs units while it has time credit: every step adds its budget,
-    every unit spends its measured cost (UNIT_MS at ns = 4096).  Ranks other than 0 run their
-    units while rank 0 solves (run_pod submits before the broadcast there).  drain() runs what
+    every unit spends its measured cost (UNIT_MS at ns = 4096).  Ranks other than 0 run up to
+    LEAD_MS of their units while rank 0 solves (before the broadcast of its result, which
+    waits for them) and the rest after their spatial modes.  drain() runs what
     is left (inside a caller's timed region); results() returns {step: eigenvalues} for the
     steps this rank owned.  ns <= 4096; beyond that each owner solves its step at once
     (pods_syev2, no vectors)."""
@@ -264,6 +265,7 @@ class SpectrumQueue:
                      else [1.0] * self.units)
         E = sum(self.cost)
         lead = self.LEAD_MS * (ns / 4096.0) ** 2 * sum(self.cost) / sum(self.UNIT_MS)
+        self.lead = lead
         if world == 1:
             self.budgets = [E]
         else:
@@ -297,7 +299,10 @@ class SpectrumQueue:
                 return s
         raise RuntimeError("SpectrumQueue: all %d slots busy" % self.max_slots)
 
-    def submit(self, C, timer=None):
+    def submit(self, C, timer=None, limit=None):
+        """Registers this step's matrix (begins its spectrum when this rank owns the step), adds
+        the step's credit and runs units while credit lasts -- at most `limit` ms of them (the
+        rest is left to run())."""
         tm = timer or (lambda name: _NullCtx())
         s = self.step_no
         self.step_no += 1
@@ -314,13 +319,21 @@ class SpectrumQueue:
                     lam = torch.empty(self.ns, dtype=torch.float64, device=C.device)
                     self.pending.append([s, slot, 1, lam])
                     self.credit -= self.cost[0]
+            self._advance(limit=limit)
+
+    def run(self, timer=None):
+        """Runs units while this step's credit lasts (after a submit with a limit)."""
+        tm = timer or (lambda name: _NullCtx())
+        with tm("eig_full"):
             self._advance()
 
-    def _advance(self, drain=False):
+    def _advance(self, drain=False, limit=None):
         lib = self.ctx.lib
         rem = ctypes.c_int(0)
-        while self.pending and (drain or self.credit > 0.0):
+        spent = 0.0
+        while self.pending and (drain or (self.credit > 0.0 and (limit is None or spent < limit))):
             p = self.pending[0]
+            spent += self.cost[min(p[2], len(self.cost) - 1)]
             check(lib.pods_eigvals_advance(self.ctx.h, p[1], 1, ctypes.byref(rem)), "pods_eigvals_advance")
             self.credit -= self.cost[min(p[2], len(self.cost) - 1)]
             p[2] += 1
@@ -473,8 +486,9 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
     meta = torch.zeros(4, dtype=torch.int64, device=dev)
     T = lam_desc = nvalid = None
     defer = spectrum is not None
-    if defer and rank != 0:   # this rank's spectrum units run while rank 0 solves
-        spectrum.submit(C, timer)
+    if defer and rank != 0:   # this rank's spectrum units run while rank 0 solves (about as long
+        spectrum.submit(C, timer, limit=spectrum.lead)   # as that takes: rank 0 waits for them at
+                                                         # the broadcast), the rest after Phi
     if rank == 0:
         lam_desc, nvalid, nmt, T, lam_modes = eigen_solve(ctx, C, ns, nm, tol_CN, full_temporal, tm, world,
                                                           defer_full=defer)
@@ -514,6 +528,8 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
                                          nmt, ptr(phi)), "pods_spatial_modes")
     if defer and rank == 0:  # the full spectrum, spread over the following steps (SpectrumQueue)
         spectrum.submit(C, timer)
+    elif defer:
+        spectrum.run(timer)
     return PODResult(energy=lam_desc, num_valid=nvalid, nm=nmt, mean=mean, T=T, phi=phi[:, :nmt],
                      C=C if keep_C else None)
 
