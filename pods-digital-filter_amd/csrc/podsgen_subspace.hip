@@ -83,8 +83,12 @@ __global__ __launch_bounds__(256) void k_tile_c(const double* __restrict__ C, in
 // chunk is loaded into registers while the current one is multiplied.
 // With KS > 1 each workgroup writes its partial tile and k_cheb_sum adds the KS partials in
 // order (deterministic) and applies the recurrence; with KS = 1 the epilogue is applied here.
-// (Loading the C operand straight into the MFMA registers from a copy laid out in operand
-// order -- only Y through LDS -- measured the same: 57.8 vs 56.2 us per step with the sum.)
+// Measured the same (55-58 us per step with the partial sum, r3): the C operand loaded
+// straight into the MFMA registers from a copy laid out in operand order with only Y through
+// LDS, either staged by ds_write or streamed by LDS-DMA into a 2-stage ring with one barrier
+// per chunk; scheduling fences that keep each block's LDS reads 16 MFMAs ahead; two chunks of
+// register prefetch; 4 or 16 K splits.  The fp64 MFMA pipe is busy 45 % of the kernel
+// (profiles/r3/mfma_util_syrk_c3.json).
 __global__ __launch_bounds__(256) void k_cheb(const double* __restrict__ Ct, int nt, int n,
                                               const double* __restrict__ Y, const double* __restrict__ Z,
                                               double alpha, double beta, double gamma, int kper,
