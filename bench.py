@@ -249,8 +249,8 @@ def main():
     split = (world > 1 or os.environ.get("PODS_EIGEN") == "split") and ns >= E.SPLIT_MIN_N
     spectrum = E.SpectrumQueue(gen.ctx, ns, rank, world) if split else None
 
-    def step(timer=None):
-        return E.pipeline(setup, device=device, dist=d, gen=gen, timer=timer, spectrum=spectrum)
+    def step(timer=None, backlog=None):
+        return E.pipeline(setup, device=device, dist=d, gen=gen, timer=timer, spectrum=spectrum, backlog=backlog)
 
     for _ in range(args.warmup):
         step()
@@ -265,10 +265,15 @@ def main():
     # HIP events (torch.cuda.Event = hipEvent_t on the stream the kernels run on) bracket
     # every stage inside the timed steps; they are read only after the timed region
     tm_run = E.StageTimer()
+    # each step's host-side Fourier results (copies, FC rows) finish during the next step's
+    # SYRK (E.FourierBacklog); the last one, and the last steps' spectra, inside the timed region
+    backlog = E.FourierBacklog()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        _, pod, fo = step(timer=tm_run)
-    if spectrum is not None:   # the last steps' spectra finish inside the timed region
+        _, pod, _ = step(timer=tm_run, backlog=backlog)
+    backlog.flush()
+    fo = backlog.results[-1]
+    if spectrum is not None:
         with tm_run("eig_full_drain"):
             spectrum.drain()
     torch.cuda.synchronize()

@@ -139,7 +139,8 @@ int pods_unpack_lower(pods_ctx* ctx, const double* packed_dev, int n, double div
  * (i, j) at V_dev[i*v_rs + j*v_cs].  Output T_dev (ns x ncols, row-major) holds column j
  * = V[:, ns-1-j] (descending order) scaled by sqrt(lambda_j / (sum_i V_ij^2 / ns)) for
  * j < nvalid (sequential sum, Python builtin).  lambda_desc_host: ncols eigenvalues in
- * descending order. */
+ * descending order (copied before the call returns).  Stream-ordered: returns without
+ * synchronising the bound stream. */
 int pods_temporal_modes(pods_ctx* ctx, const double* V_dev, int64_t v_rs, int64_t v_cs,
                         const double* lambda_desc_host, int nvalid, int ncols, double* T_dev);
 
@@ -220,7 +221,8 @@ int pods_syev2_status(pods_ctx* ctx);
 int pods_syev2_inspect(pods_ctx* ctx, int n, int nvec, int what, double* out_host, int64_t count);
 
 /* Spatial modes Phi = ((A-m) T[:, :nm]) * (1/lambda) / ns (PODFS.py:1330-1333).
- * T_dev: ns x ldT row-major.  phi_dev: 3*P_local x nm row-major (reference layout). */
+ * T_dev: ns x ldT row-major.  phi_dev: 3*P_local x nm row-major (reference layout).
+ * lambda_host is copied before the call returns; stream-ordered (no synchronisation). */
 int pods_spatial_modes(pods_ctx* ctx, const double* T_dev, int ldT, const double* lambda_host,
                        int nm, double* phi_dev);
 

@@ -251,9 +251,54 @@ struct pods_ctx {
                                              // partials, the tiled copy of C
   const double* sub_ct_src = nullptr;        // the C that sub_ct holds (pods_cheb_prepare)
   int sub_ct_n = 0;
+  DevBuf inv_lam;  // 1 / lambda of the spatial modes (its own buffer: no reuse hazard with lam)
+  // pinned staging ring for small host -> device uploads: a slot is reused only after the
+  // event recorded behind its copy, so uploads need no stream synchronisation
+  static constexpr int kStageSlots = 16;
+  static constexpr size_t kStageSlot = 64 * 1024;
+  char* pin = nullptr;
+  hipEvent_t pin_ev[kStageSlots] = {};
+  bool pin_used[kStageSlots] = {};
+  int pin_next = 0;
 };
 
 namespace {
+
+// dst_dev <- bytes of src (host) on the context's stream, without synchronising it: through
+// the pinned ring (slot reused after its copy's event), or a synchronous copy when too large
+hipError_t stage_upload(pods_ctx* c, void* dst_dev, const void* src, size_t bytes) {
+  if (bytes == 0) return hipSuccess;
+  if (bytes > pods_ctx::kStageSlot) {
+    hipError_t e = hipMemcpyAsync(dst_dev, src, bytes, hipMemcpyHostToDevice, c->stream);
+    return e != hipSuccess ? e : hipStreamSynchronize(c->stream);
+  }
+  hipError_t e = hipSuccess;
+  if (!c->pin) {
+    e = hipHostMalloc(reinterpret_cast<void**>(&c->pin), pods_ctx::kStageSlots * pods_ctx::kStageSlot,
+                      hipHostMallocDefault);
+    if (e != hipSuccess) {
+      c->pin = nullptr;
+      return e;
+    }
+    for (int i = 0; i < pods_ctx::kStageSlots; ++i) {
+      e = hipEventCreateWithFlags(&c->pin_ev[i], hipEventDisableTiming);
+      if (e != hipSuccess) return e;
+    }
+  }
+  const int sl = c->pin_next;
+  c->pin_next = (sl + 1) % pods_ctx::kStageSlots;
+  if (c->pin_used[sl]) {
+    e = hipEventSynchronize(c->pin_ev[sl]);
+    if (e != hipSuccess) return e;
+  }
+  char* slot = c->pin + (size_t)sl * pods_ctx::kStageSlot;
+  std::memcpy(slot, src, bytes);
+  e = hipMemcpyAsync(dst_dev, slot, bytes, hipMemcpyHostToDevice, c->stream);
+  if (e != hipSuccess) return e;
+  e = hipEventRecord(c->pin_ev[sl], c->stream);
+  c->pin_used[sl] = e == hipSuccess;
+  return e;
+}
 
 
 int upload_rng(pods_ctx* c, const RngLayout& L, uint32_t seed, RngBuffers& rb) {
@@ -354,6 +399,12 @@ int pods_destroy(pods_ctx* c) {
   release(c->sub_ct);
   for (EigvalSlot& sl : c->eslots)
     for (DevBuf* b : {&sl.wm, &sl.x, &sl.flags, &sl.det, &sl.v, &sl.cnt, &sl.lam}) release(*b);
+  release(c->inv_lam);
+  if (c->pin) {
+    for (int i = 0; i < pods_ctx::kStageSlots; ++i)
+      if (c->pin_ev[i]) (void)hipEventDestroy(c->pin_ev[i]);
+    (void)hipHostFree(c->pin);
+  }
   delete c;
   return PODS_OK;
   PODS_CATCH
@@ -748,12 +799,9 @@ int pods_temporal_modes(pods_ctx* c, const double* V, int64_t v_rs, int64_t v_cs
   if (ncols <= 0 || ncols > ns || nvalid > ncols) return fail(PODS_ERR_ARG, "bad ncols/nvalid");
   PODS_HIP(ensure(c->lam, (size_t)ncols * sizeof(double)));
   PODS_HIP(ensure(c->mag, (size_t)ncols * sizeof(double)));
-  c->stage.assign(lam_desc, lam_desc + ncols);
-  PODS_HIP(hipMemcpyAsync(c->lam.p, c->stage.data(), (size_t)ncols * sizeof(double),
-                          hipMemcpyHostToDevice, c->stream));
+  PODS_HIP(stage_upload(c, c->lam.p, lam_desc, (size_t)ncols * sizeof(double)));
   PODS_HIP(pods::launch_temporal(V, v_rs, v_cs, ns, ncols, std::max(nvalid, 0), c->lam.as<double>(),
                                  c->mag.as<double>(), T, c->stream));
-  PODS_HIP(hipStreamSynchronize(c->stream));  // staging buffer reuse
   return PODS_OK;
   PODS_CATCH
 }
@@ -763,17 +811,15 @@ int pods_spatial_modes(pods_ctx* c, const double* T, int ldT, const double* lam,
   if (int e = check_ctx(c)) return e;
   if (!c->have_snapshots || !c->mean_valid) return fail(PODS_ERR_STATE, "pods_spatial_modes needs pods_mean");
   if (!T || !lam || !phi || nm <= 0 || ldT < nm) return fail(PODS_ERR_ARG, "bad arguments");
-  PODS_HIP(ensure(c->lam, (size_t)nm * sizeof(double)));
+  PODS_HIP(ensure(c->inv_lam, (size_t)nm * sizeof(double)));
   c->stage.resize(nm);
   for (int m = 0; m < nm; ++m) c->stage[m] = 1.0 / lam[m];  // np.ones(nm)/energy (PODFS.py:1331)
-  PODS_HIP(hipMemcpyAsync(c->lam.p, c->stage.data(), (size_t)nm * sizeof(double), hipMemcpyHostToDevice,
-                          c->stream));
+  PODS_HIP(stage_upload(c, c->inv_lam.p, c->stage.data(), (size_t)nm * sizeof(double)));
   const size_t wb = pods::spatial_work_bytes(c->rowlen, c->p.ns);
   if (wb) PODS_HIP(ensure(c->spwork, wb));
   PODS_HIP(pods::launch_spatial(c->A.as<double>(), c->rowlen, c->p.ns,
                                 c->centered ? c->zero.as<double>() : c->mean.as<double>(), T, ldT, nm,
-                                c->lam.as<double>(), phi, wb ? c->spwork.as<double>() : nullptr, c->stream));
-  PODS_HIP(hipStreamSynchronize(c->stream));
+                                c->inv_lam.as<double>(), phi, wb ? c->spwork.as<double>() : nullptr, c->stream));
   return PODS_OK;
   PODS_CATCH
 }

@@ -457,16 +457,22 @@ def eigen_solve(ctx: Context, C, ns, nm, tol_CN, full_temporal, tm=None, world=1
 
 
 def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=False,
-            keep_C=False, timer=None, on_temporal=None, spectrum=None):
+            keep_C=False, timer=None, on_temporal=None, spectrum=None, before_eigen=None):
     """PODFS.POD (PODFS.py:1294-1393) with correct_for_cell_volumes='false'.
 
     spectrum: a SpectrumQueue -- the eigenvalues past the nm leading ones are then computed by
     it (spread over the following steps, energy/num_valid of the result are None); without one
     the whole spectrum is computed in this call.
 
-    on_temporal(T, nm_trunc), if given, is called on rank 0 as soon as the scaled temporal
-    modes exist, before the spatial modes are enqueued (pipeline() starts the Fourier
-    stage there on a side stream, so it runs beside the spatial-mode pass)."""
+    on_temporal(T, nm_trunc, ready), if given, is called on rank 0 with `ready` an event recorded
+    behind the temporal modes: on one rank right after the spatial modes are enqueued (so the
+    spatial pass does not wait for the host to launch the Fourier stage), on several ranks
+    before the broadcasts.  pipeline() starts the Fourier stage there on a side stream that
+    waits for `ready` only, so it runs beside the spatial-mode pass.
+
+    before_eigen(), if given, is called once the correlation is enqueued, before the first
+    host synchronisation of the eigensolve (pipeline() finishes the previous step's Fourier
+    results there, while the device runs this step's SYRK)."""
     ctx, lib = snap.ctx, snap.ctx.lib
     ns = snap.ns
     dist, rank, world = _dist_info(dist)
@@ -483,6 +489,8 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
     if world > 1:
         with tm("allreduce"):
             allreduce_correlation(dist, C, ns, *device_triangle_ops(ctx))
+    if before_eigen is not None:
+        before_eigen()
     meta = torch.zeros(4, dtype=torch.int64, device=dev)
     T = lam_desc = nvalid = None
     defer = spectrum is not None
@@ -492,8 +500,10 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
     if rank == 0:
         lam_desc, nvalid, nmt, T, lam_modes = eigen_solve(ctx, C, ns, nm, tol_CN, full_temporal, tm, world,
                                                           defer_full=defer)
-        if on_temporal is not None:
-            on_temporal(T, nmt)
+        t_ready = torch.cuda.Event()
+        t_ready.record()
+        if world > 1 and on_temporal is not None:   # beside the broadcasts and the spatial pass
+            on_temporal(T, nmt, t_ready)
         meta[0] = -1 if nvalid is None else nvalid
         meta[1] = nmt
         meta[2] = 0 if lam_desc is None else 1
@@ -526,6 +536,8 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
         with tm("spatial"):
             check(lib.pods_spatial_modes(ctx.h, ptr(Tsel), ldT, ptr(np.ascontiguousarray(lam_modes[:nmt])),
                                          nmt, ptr(phi)), "pods_spatial_modes")
+    if world == 1 and on_temporal is not None:   # after the spatial pass is enqueued
+        on_temporal(T, nmt, t_ready)
     if defer and rank == 0:  # the full spectrum, spread over the following steps (SpectrumQueue)
         spectrum.submit(C, timer)
     elif defer:
@@ -594,12 +606,12 @@ def run_fourier(ctx: Context, T, nm, ns, dt, et, timer=None):
     return launch_fourier(ctx, T, nm, ns, dt, et, timer)()
 
 
-def launch_fourier(ctx: Context, T, nm, ns, dt, et, timer=None, side=False):
+def launch_fourier(ctx: Context, T, nm, ns, dt, et, timer=None, side=False, ready=None):
     """Enqueue the DFT and the ranking kernels; returns finish() -> FourierResult.
 
-    side=True runs them on the context's side stream (forked from the current stream, so it
-    sees T), concurrently with what the caller enqueues next on the current stream (the
-    spatial modes: an HBM-bound pass beside this VALU-bound one).  finish() copies on that
+    side=True runs them on the context's side stream (forked from the current stream, or from
+    the event `ready` recorded behind T), concurrently with the caller's work on the current
+    stream (the spatial modes: an HBM-bound pass beside this VALU-bound one).  finish() copies on that
     stream and the pods context is bound back to the current stream before returning."""
     tm = timer or (lambda name: _NullCtx())
     time_, period = time_axis(ns, dt)
@@ -615,7 +627,10 @@ def launch_fourier(ctx: Context, T, nm, ns, dt, et, timer=None, side=False):
     stream = main
     if side:
         stream = ctx.side_stream()
-        stream.wait_stream(main)
+        if ready is not None:   # T complete; later work on the main stream is not waited for
+            stream.wait_event(ready)
+        else:
+            stream.wait_stream(main)
         T.record_stream(stream)
     with torch.cuda.stream(stream):
         if side:
@@ -694,9 +709,30 @@ class StageTimer:
         return out
 
 
-def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=None, gen=None, spectrum=None):
+class FourierBacklog:
+    """Fourier results of a multi-step run finished one step late: the host-side part (copies
+    of c, the ranking and the FC rows) of step s runs while the device computes step s+1's
+    correlation, instead of leaving the device idle between steps.  results[s] is step s's
+    FourierResult (None without modes); flush() finishes what is left."""
+
+    def __init__(self):
+        self.pending = []
+        self.results = []
+
+    def finish_pending(self):
+        while self.pending:
+            fin = self.pending.pop(0)
+            self.results.append(fin() if fin is not None else None)
+
+    flush = finish_pending
+
+
+def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=None, gen=None, spectrum=None,
+             backlog=None):
     """The whole hot path; returns (Generator, PODResult, FourierResult | None).
-    spectrum: a SpectrumQueue for multi-step runs (see run_pod)."""
+    spectrum: a SpectrumQueue for multi-step runs (see run_pod).  backlog: a FourierBacklog --
+    this step's Fourier result is then finished during the next step (or by backlog.flush())
+    and the returned FourierResult is None."""
     dist_, rank, world = _dist_info(dist)
     tm = timer or (lambda name: _NullCtx())
     gen = gen or Generator(setup, device=device, rank=rank, world=world)
@@ -704,11 +740,15 @@ def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=Non
         snap = gen.generate()
     pending = []
 
-    def start_fourier(T, nmt):
+    def start_fourier(T, nmt, ready):
         pending.append(launch_fourier(gen.ctx, T, nmt, setup.ns, setup.dt_eff, setup.et, timer=timer,
-                                      side=True))
+                                      side=True, ready=ready))
     pod = run_pod(snap, setup.nm, dist=dist_, full_temporal=full_temporal, timer=timer,
-                  on_temporal=start_fourier, spectrum=spectrum)
+                  on_temporal=start_fourier, spectrum=spectrum,
+                  before_eigen=backlog.finish_pending if backlog is not None else None)
+    if backlog is not None:
+        backlog.pending.append(pending[0] if pending else None)
+        return gen, pod, None
     fo = pending[0]() if pending else None
     return gen, pod, fo
 
