@@ -249,11 +249,15 @@ def main():
     split = (world > 1 or os.environ.get("PODS_EIGEN") == "split") and ns >= E.SPLIT_MIN_N
     spectrum = E.SpectrumQueue(gen.ctx, ns, rank, world) if split else None
 
-    def step(timer=None, backlog=None):
-        return E.pipeline(setup, device=device, dist=d, gen=gen, timer=timer, spectrum=spectrum, backlog=backlog)
+    def step(timer=None, backlog=None, ahead=False):
+        return E.pipeline(setup, device=device, dist=d, gen=gen, timer=timer, spectrum=spectrum, backlog=backlog,
+                          prefetch_next=ahead)
 
-    for _ in range(args.warmup):
-        step()
+    # ahead: the next step's random planes and x pass run on a second stream beside this step's
+    # correlation (Generator.prefetch_next).  The last warm-up step and the last timed step do
+    # not prefetch, so the timed region holds exactly `steps` whole generations.
+    for w in range(args.warmup):
+        step(ahead=w < args.warmup - 1)
     if spectrum is not None:
         spectrum.drain()
         spectrum.results()
@@ -269,8 +273,8 @@ def main():
     # SYRK (E.FourierBacklog); the last one, and the last steps' spectra, inside the timed region
     backlog = E.FourierBacklog()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        _, pod, _ = step(timer=tm_run, backlog=backlog)
+    for s in range(args.steps):
+        _, pod, _ = step(timer=tm_run, backlog=backlog, ahead=s < args.steps - 1)
     backlog.flush()
     fo = backlog.results[-1]
     if spectrum is not None:
@@ -337,6 +341,10 @@ def main():
                          "traffic": traffic, "launch_ms": round(corr_ms, 3),
                          "flops_per_launch": flops},
             "stages_ms": {k: round(v, 3) for k, v in stages.items()},
+            "stages_note": ("per-step means of HIP-event times on the stream each stage runs on; "
+                            "generate_ahead (the next step's random planes + x pass) runs on a second "
+                            "stream beside mean/center/corr, so the stages overlap and do not sum to "
+                            "ms_per_step"),
             "results": {"nm": int(pod.nm), "num_valid": None if num_valid is None else int(num_valid),
                         "eigensolve": "split: leading pairs by subspace iteration + full spectrum spread over "
                                       "steps (SpectrumQueue)" if spectrum is not None else "fused (pods_syev)",

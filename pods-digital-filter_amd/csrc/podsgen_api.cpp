@@ -472,7 +472,8 @@ int pods_df_configure(pods_ctx* c, const pods_df_params* prm, const double* bx, 
   // padded K columns of the K-tiled snapshot matrix (and of the mean) stay zero
   PODS_HIP(hipMemset(c->A.p, 0, (size_t)p.ns * c->rowpad * sizeof(double)));
   PODS_HIP(hipMemset(c->mean.p, 0, (size_t)c->rowpad * sizeof(double)));
-  PODS_HIP(ensure(c->lund, (size_t)9 * c->Pl * sizeof(double)));
+  PODS_HIP(ensure(c->lund, (size_t)std::max<int64_t>(9 * c->Pl, pods::lund_chunk_size(c->jl, p.kma)) *
+                                sizeof(double)));
   PODS_HIP(ensure(c->taps, (size_t)(c->NX + c->NY + c->NZ) * sizeof(double)));
   PODS_HIP(ensure(c->rot, 9 * sizeof(double)));
   std::vector<double> taps(c->NX + c->NY + c->NZ);
@@ -482,15 +483,25 @@ int pods_df_configure(pods_ctx* c, const pods_df_params* prm, const double* bx, 
   PODS_HIP(hipMemcpy(c->taps.p, taps.data(), taps.size() * sizeof(double), hipMemcpyHostToDevice));
   c->lund_sj = p.kma;
   if (lund_host) {
-    PODS_HIP(hipMemcpy(c->lund.p, lund_host, (size_t)9 * c->Pl * sizeof(double), hipMemcpyHostToDevice));
-    // a profile that does not vary along j (adapt1d's 1-D profiles) is read with j-stride 0
+    // a profile that does not vary along j (adapt1d's 1-D profiles) is staged per block in LDS
+    // from its first row; a j-varying one is stored chunk-major (coalesced 16-B loads)
     bool same = true;
     for (int e = 0; e < 9 && same; ++e) {
       const double* row0 = lund_host + (int64_t)e * c->Pl;
       for (int jj = 1; jj < c->jl && same; ++jj)
         same = std::memcmp(row0, row0 + (int64_t)jj * p.kma, (size_t)p.kma * sizeof(double)) == 0;
     }
-    if (same) c->lund_sj = 0;
+    if (same) {
+      c->lund_sj = 0;
+      PODS_HIP(hipMemcpy(c->lund.p, lund_host, (size_t)9 * c->Pl * sizeof(double), hipMemcpyHostToDevice));
+    } else {
+      std::vector<double> ch((size_t)pods::lund_chunk_size(c->jl, p.kma), 0.0);
+      for (int64_t jj = 0; jj < c->jl; ++jj)
+        for (int e = 0; e < 9; ++e)
+          for (int k = 0; k < p.kma; ++k)
+            ch[pods::lund_chunk_index(jj, e, k, p.kma)] = lund_host[(int64_t)e * c->Pl + jj * p.kma + k];
+      PODS_HIP(hipMemcpy(c->lund.p, ch.data(), ch.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
   }
   double r9[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
   if (p.rotate) std::memcpy(r9, rot_host, sizeof(r9));
@@ -505,35 +516,44 @@ int pods_df_configure(pods_ctx* c, const pods_df_params* prm, const double* bx, 
   PODS_CATCH
 }
 
-int pods_df_generate(pods_ctx* c) {
+int pods_df_generate_parts(pods_ctx* c, int parts) {
   PODS_TRY
   if (int e = check_ctx(c)) return e;
   if (!c->configured) return fail(PODS_ERR_STATE, "pods_df_generate before pods_df_configure");
+  if (parts & ~PODS_GEN_ALL) return fail(PODS_ERR_ARG, "bad generation parts");
   PODS_HIP(hipSetDevice(c->device));
   const pods_df_params& p = c->p;
   const RngLayout& L = c->layout;
-  if (int e = run_jumps(c, L, c->rng)) return e;
-  PODS_HIP(pods::launch_mt_generate(c->rng.states.as<uint32_t>(), L.G, L.Bs, L.ntot, c->S, c->Kp, p.j0,
-                                    p.j1 + 2 * p.nfy, c->Sl, p.rng_low, p.rng_range, c->R.as<double>(),
-                                    c->stream));
+  if (parts & PODS_GEN_PLANES) {
+    if (int e = run_jumps(c, L, c->rng)) return e;
+    PODS_HIP(pods::launch_mt_generate(c->rng.states.as<uint32_t>(), L.G, L.Bs, L.ntot, c->S, c->Kp, p.j0,
+                                      p.j1 + 2 * p.nfy, c->Sl, p.rng_low, p.rng_range, c->R.as<double>(),
+                                      c->stream));
+  }
   const double* taps = c->taps.as<double>();
-  // x pass: enough (component, point, step-chunk) threads to fill the chip
-  const int64_t pts = 3 * c->Sl;
-  int64_t nch = (256LL * 2048 + pts - 1) / pts;
-  nch = std::max<int64_t>(1, std::min<int64_t>(nch, std::max(1, p.ns / 16)));
-  const int chunk = (int)((p.ns + nch - 1) / nch);
-  PODS_HIP(pods::launch_filter_x(c->NX, c->R.as<double>(), taps, p.ns, c->Sl, 3, chunk,
-                                 c->T1.as<double>(), c->stream));
-  PODS_HIP(pods::launch_filter_yz(c->NY, c->T1.as<double>(), taps + c->NX, taps + c->NX + c->NY,
-                                  c->NZ, p.ns, c->jl, p.kma, c->Kp, c->Sl, 3, c->lund.as<double>(),
-                                  c->lund_sj, p.lund_mode, c->rot.as<double>(), p.rotate,
-                                  c->A.as<double>(), c->stream));
-  c->have_snapshots = true;
-  c->mean_valid = false;
-  c->centered = false;
+  if (parts & PODS_GEN_XPASS) {
+    // x pass: enough (component, point, step-chunk) threads to fill the chip
+    const int64_t pts = 3 * c->Sl;
+    int64_t nch = (256LL * 2048 + pts - 1) / pts;
+    nch = std::max<int64_t>(1, std::min<int64_t>(nch, std::max(1, p.ns / 16)));
+    const int chunk = (int)((p.ns + nch - 1) / nch);
+    PODS_HIP(pods::launch_filter_x(c->NX, c->R.as<double>(), taps, p.ns, c->Sl, 3, chunk,
+                                   c->T1.as<double>(), c->stream));
+  }
+  if (parts & PODS_GEN_YZPASS) {
+    PODS_HIP(pods::launch_filter_yz(c->NY, c->T1.as<double>(), taps + c->NX, taps + c->NX + c->NY,
+                                    c->NZ, p.ns, c->jl, p.kma, c->Kp, c->Sl, 3, c->lund.as<double>(),
+                                    c->lund_sj, p.lund_mode, c->rot.as<double>(), p.rotate,
+                                    c->A.as<double>(), c->stream));
+    c->have_snapshots = true;
+    c->mean_valid = false;
+    c->centered = false;
+  }
   return PODS_OK;
   PODS_CATCH
 }
+
+int pods_df_generate(pods_ctx* c) { return pods_df_generate_parts(c, PODS_GEN_ALL); }
 
 int pods_df_snapshots(pods_ctx* c, double** a_dev, int64_t* row_len) {
   if (int e = check_ctx(c)) return e;

@@ -20,7 +20,13 @@ hipError_t launch_mt_generate(const uint32_t* states, int G, int64_t Bs, int64_t
                               double* out, hipStream_t st);
 hipError_t launch_filter_x(int NX, const double* R, const double* bx, int ns, int64_t Sl, int ncomp,
                            int chunk, double* T1, hipStream_t st);
-// lund_sj: j-stride of the 9 x Pl Lund table (0 = the same row of parameters for every j)
+// lund_sj: 0 = one row of 9 x K parameters for every j (plain layout lund[e * Pl + k]);
+// otherwise the table is j-varying and in the chunk-major layout below
+inline int64_t lund_chunk_index(int64_t j, int e, int k, int K) {
+  const int QC = (K + 15) / 16, q = k / 16, kk = k % 16;
+  return ((((j * 9 + e) * 8 + kk / 2) * QC + q) * 2) + (kk & 1);
+}
+inline int64_t lund_chunk_size(int64_t jl, int K) { return jl * 9 * 16 * (int64_t)((K + 15) / 16); }
 hipError_t launch_filter_yz(int NY, const double* T1, const double* by, const double* bz, int NZ,
                             int ns, int jl, int K, int Kp, int64_t Sl, int ncomp,
                             const double* lund, int64_t lund_sj, int lund_mode, const double* rot,

@@ -458,8 +458,9 @@ __global__ __launch_bounds__(256) void k_filter_x2(const double* __restrict__ R,
 // window reads are LDS-bank-conflict-free.  The three components' results stay in registers
 // for the Lund transform (digitalfilters.py:174-176 / :227-229) and the rotation, and each
 // thread stores its 16 consecutive snapshot rows as one 128-B line (K-tiled layout).
-// lund_sj: j-stride of the Lund table (0 when the profile does not vary with j, e.g. the
-// 1-D profiles of adapt1d: the table then stays in L1).
+// lund_sj: 0 when the profile does not vary with j (the 1-D profiles of adapt1d): the table
+// (9 rows of K) is staged in LDS per block.  Otherwise (2-D profiles) it is in the chunk-major
+// layout of lund_chunk_index (built once by pods_df_configure).
 __device__ __forceinline__ int kpad(int k) { return k + (k >> 4); }
 
 // NZC: compile-time z width (0: runtime NZ <= 25, the generic instance)
@@ -468,21 +469,41 @@ __global__ __launch_bounds__(NT) void k_filter_yz(
     const double* __restrict__ T1, const double* __restrict__ by, const double* __restrict__ bz,
     int NZr, int ns, int jl, int K, int Kp, int64_t Sl, int ncomp,
     const double* __restrict__ lund, int64_t lund_sj, int lund_mode, const double* __restrict__ rot,
-    int rotate, double* __restrict__ AT, int nsb) {
+    int rotate, double* __restrict__ AT, int nsb, int KB) {
   extern __shared__ __attribute__((aligned(16))) double t2[];  // TJ x ldt
   constexpr int YR = TJ < 16 ? TJ : 16;  // rows per y-pass item
   constexpr int NZMAX = NZC > 0 ? NZC : 25;
   const int NZ = NZC > 0 ? NZC : NZr;
   constexpr int WIN = 16 + NZMAX - 1;
-  const int ldt = kpad(Kp + 16) + 1;
   // (An XCD-aware renumbering of the blocks, so the row tiles of one step group share an L2,
   // cut the HBM traffic 18.4 -> 14.5 GB at C3 at the same time and made C4 ~4 ms slower.)
-  const int tile_x = blockIdx.x, group_y = blockIdx.y;
+  int tile_x = blockIdx.x, group_y = blockIdx.y, tile_z = blockIdx.z;
+  if (lund_sj != 0) {
+    // j-varying Lund table (2-D profiles): the blocks of one (row, column) tile run their step
+    // groups back to back on ONE XCD (dispatch deals consecutive blocks round-robin over the 8
+    // XCDs), so the tile's 295 KB of Lund parameters stay in that XCD's L2
+    const int ntx = gridDim.x, ngy = gridDim.y;
+    const int total = ntx * ngy * gridDim.z;
+    const int b = blockIdx.x + ntx * (blockIdx.y + ngy * blockIdx.z);
+    const int xcd = b & 7, qq = total >> 3, rr = total & 7;
+    const int logical = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
+    const int tile = logical / ngy;
+    group_y = logical - tile * ngy;
+    tile_x = tile % ntx;
+    tile_z = tile / ntx;
+  }
+  // column tile: outputs [k0, k0 + Kt) of the K axis from padded columns [k0, k0 + Kpt)
+  // (KB = K: one tile; wider inlets are cut into 256-column tiles, so every shape runs the
+  // 16-row x 256-thread configuration with a z halo of (NZ - 1) / KB)
+  const int k0 = tile_z * KB;
+  const int Kt = min(KB, K - k0);
+  const int Kpt = Kt + NZ - 1;
+  const int ldt = kpad(KB + NZ - 1 + 16) + 1;
   const int jt = tile_x * TJ;
   const int tid0 = threadIdx.x;
   const int rows = min(TJ, jl - jt);
   const int64_t Pl = (int64_t)jl * K;
-  const int kch = (K + 15) >> 4;       // 16-wide output chunks per row
+  const int kch = (Kt + 15) >> 4;      // 16-wide output chunks per row
   const int zitems = TJ * kch;         // <= NT (host guarantees)
   double byr[NY];
 #pragma unroll
@@ -493,12 +514,12 @@ __global__ __launch_bounds__(NT) void k_filter_yz(
   // A Lund table that does not vary along j (lund_sj == 0) is staged once per block in LDS
   // (9 rows of K, padded like t2) and read conflict-free by the 16-wide output chunks.
   const bool lsh = lund_sj == 0 && lund_mode >= 0;
-  const int ldl = kpad(K) + 1;
+  const int ldl = kpad(KB) + 1;
   double* lt = t2 + (size_t)TJ * ldt;
   if (lsh) {
     const int ne = lund_mode == 1 ? 9 : 7;
     for (int e = 0; e < ne; ++e)
-      for (int k = tid0; k < K; k += NT) lt[e * ldl + kpad(k)] = lund[(int64_t)e * Pl + k];
+      for (int k = tid0; k < Kt; k += NT) lt[e * ldl + kpad(k)] = lund[(int64_t)e * Pl + k0 + k];
   }
   // NSB consecutive steps per block: each thread's stores for one snapshot-row group then
   // land on consecutive 128-B lines of the K-tiled layout (steps are contiguous there)
@@ -522,12 +543,12 @@ __global__ __launch_bounds__(NT) void k_filter_yz(
     for (int c = 0; c < 3; ++c) {
       // ncomp is 3 (generator) or 1 (pods_filter_block): the unrolled body is guarded
       if (c < ncomp) {
-      const double* src = T1i + ((int64_t)c * ns + i) * Sl + (int64_t)jt * Kp;
+      const double* src = T1i + ((int64_t)c * ns + i) * Sl + (int64_t)jt * Kp + k0;
       // main items: (column, YR-row group) for the first cmain columns, one per thread;
       // the remaining halo columns as single-output mini items spread over all threads
       // (2*Kp items on NT threads would leave a few threads a second full item)
       constexpr int GRP = TJ / YR;
-      const int cmain = min(Kp, NT / GRP);
+      const int cmain = min(Kpt, NT / GRP);
       for (int it = tid; it < GRP * cmain; it += NT) {
         const int grp = it / cmain, col = it - grp * cmain;
         const int r0 = grp * YR;
@@ -554,7 +575,7 @@ __global__ __launch_bounds__(NT) void k_filter_yz(
         for (int jj = 0; jj < YR; ++jj)
           if (r0 + jj < rows) t2[(r0 + jj) * ldt + kpad(col)] = acc[jj];
       }
-      for (int it = tid; it < (Kp - cmain) * TJ; it += NT) {
+      for (int it = tid; it < (Kpt - cmain) * TJ; it += NT) {
         const int col = cmain + it / TJ, jj = it - (it / TJ) * TJ;
         if (jj >= rows) continue;
         double v[NY];
@@ -590,10 +611,14 @@ __global__ __launch_bounds__(NT) void k_filter_yz(
       for (int e = 0; e < 9; ++e) R9[e] = roti[e];
     }
     const int j = jt + zr;
-    const int64_t p0 = (int64_t)j * K + zk0;
-    const int64_t lbase = (int64_t)j * lund_sj + zk0;
+    const int64_t p0 = (int64_t)j * K + k0 + zk0;
+    // j-varying table: chunk-major layout (lund_chunk_index), one coalesced 16-B load per
+    // (parameter, output pair)
+    const int QC = (K + 15) >> 4;
+    const double2* L2 = reinterpret_cast<const double2*>(lund_i) + (int64_t)j * 9 * 8 * QC + ((k0 + zk0) >> 4);
     // the Lund transform / rotation overwrite res in place
     double (&out)[3][16] = res;
+    double2 pp[9];
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
       if (lund_mode < 0) continue;
@@ -603,9 +628,13 @@ __global__ __launch_bounds__(NT) void k_filter_yz(
 #pragma unroll
         for (int e = 0; e < 9; ++e) prm[e] = (e < 7 || lund_mode == 1) ? L[e * ldl] : 0.0;
       } else {
-        const double* L = lund_i + lbase + kk;
+        if ((kk & 1) == 0) {
 #pragma unroll
-        for (int e = 0; e < 9; ++e) prm[e] = (e < 7 || lund_mode == 1) ? L[e * Pl] : 0.0;
+          for (int e = 0; e < 9; ++e)
+            pp[e] = (e < 7 || lund_mode == 1) ? L2[((int64_t)e * 8 + (kk >> 1)) * QC] : make_double2(0.0, 0.0);
+        }
+#pragma unroll
+        for (int e = 0; e < 9; ++e) prm[e] = (kk & 1) ? pp[e].y : pp[e].x;
       }
       const double xu = res[0][kk], xv = res[1][kk], xw = res[2][kk];
       const double a00 = prm[0], a10 = prm[1], a11 = prm[2];
@@ -631,7 +660,7 @@ __global__ __launch_bounds__(NT) void k_filter_yz(
       out[1][kk] = v;
       out[2][kk] = ww;
     }
-    const int nk = min(16, K - zk0);
+    const int nk = min(16, Kt - zk0);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       if (c >= ncomp) break;
@@ -775,88 +804,108 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds_byte_addr) 
 // (57.0 against 52.9 ms).  4 waves as 2 x 2, each 64 x 64 = 4 x 4 blocks of
 // v_mfma_f64_16x16x4_f64.  Partial tiles go to slab `split`; k_syrk_reduce sums the slabs in
 // split order (deterministic).
-namespace syrk3 {
-constexpr int BM = 128, BN = 128, KT = 16, NST = 2, NW = 4;
-constexpr int XB = BM * KT * 8;            // 16 KB
-constexpr int YB = BN * KT * 8;            // 16 KB
-constexpr int MBYTES = NW * 128;
-constexpr int STAGE = XB + YB + MBYTES;
-constexpr int XP = XB / 1024 / NW;         // 4
-constexpr int YP = YB / 1024 / NW;         // 4
-}  // namespace syrk3
+template <int KT_, int NST_>
+struct SyrkCfg {
+  static constexpr int BM = 128, BN = 128, KT = KT_, NST = NST_, NW = 4;
+  static constexpr int XB = BM * KT * 8;            // X panel bytes per stage
+  static constexpr int YB = BN * KT * 8;            // Y panel bytes per stage
+  static constexpr int MBYTES = NW * KT * 8;        // mean slice (CENTRED = 0)
+  static constexpr int STAGE = XB + YB + MBYTES;
+  static constexpr int XP = XB / 1024 / NW;         // 1 KB LDS-DMA instructions per wave
+  static constexpr int YP = YB / 1024 / NW;
+  static constexpr int SLOTS = KT / 2;              // 16-B slots per row
+  static constexpr int RPI = 64 / SLOTS;            // rows per 1 KB instruction
+  static constexpr int SWZ = SLOTS - 1;             // swizzle mask
+  static constexpr int RSH = KT == 16 ? 1 : 2;      // row bits that pick the swizzle
+};
 
-template <int CENTRED>
-__global__ __launch_bounds__(256, 2) void k_syrk_g128(const double* __restrict__ AT, int ns,
-                                                      int64_t Kdim, const double* __restrict__ mean,
-                                                      const int4* __restrict__ items, int nitems,
-                                                      int64_t ksplit, double* __restrict__ work,
-                                                      int64_t ldc, int64_t slab) {
-  using namespace syrk3;
+// s_waitcnt vmcnt(N) with the other counters left alone (gfx9 encoding)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+template <int CENTRED, int KT, int NST, int OCC>
+__global__ __launch_bounds__(256, OCC) void k_syrk_g128(const double* __restrict__ AT, int ns,
+                                                        int64_t Kdim, const double* __restrict__ mean,
+                                                        const int4* __restrict__ items, int nitems,
+                                                        int64_t ksplit, double* __restrict__ work,
+                                                        int64_t ldc, int64_t slab) {
+  using Cf = SyrkCfg<KT, NST>;
+  constexpr int XB = Cf::XB, YB = Cf::YB, STAGE = Cf::STAGE, XP = Cf::XP, YP = Cf::YP;
+  constexpr int SLOTS = Cf::SLOTS, RPI = Cf::RPI, SWZ = Cf::SWZ, RSH = Cf::RSH;
+  constexpr int Q = XP + YP + (CENTRED ? 0 : 1);    // DMA instructions per wave per K-tile
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int b = blockIdx.x;
   const int xcd = b & 7, qq = nitems >> 3, rr = nitems & 7;
   const int logical = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
   const int4 it = items[logical];
   const int bi = it.x, bj = it.y, sp = it.z;
-  const int i0 = bi * BM, j0 = bj * BN;
+  const int i0 = bi * Cf::BM, j0 = bj * Cf::BN;
   const int64_t kt0 = (int64_t)sp * (ksplit / KT);
   const int64_t kt1 = min(Kdim, (int64_t)(sp + 1) * ksplit) / KT;
   const int nt = (int)(kt1 - kt0);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = wave >> 1, wc = wave & 1;
   const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
-  const int lrow = lane >> 3, lslot = lane & 7;
+  const int lrow = lane / SLOTS, lslot = lane % SLOTS;
+  // K-tiled A: a K-tile of KT rows of one snapshot is KT contiguous doubles inside its 16-row
+  // group (KT = 8: the half `hk` of the group)
   int64_t xsrc[XP], ysrc[YP];
 #pragma unroll
   for (int q = 0; q < XP; ++q) {
-    const int R = (wave * XP + q) * 8 + lrow;
-    xsrc[q] = ((int64_t)min(i0 + R, ns - 1) << 4) + ((lslot ^ ((R >> 1) & 7)) << 1);
+    const int R = (wave * XP + q) * RPI + lrow;
+    xsrc[q] = ((int64_t)min(i0 + R, ns - 1) << 4) + ((lslot ^ ((R >> RSH) & SWZ)) << 1);
   }
 #pragma unroll
   for (int q = 0; q < YP; ++q) {
-    const int R = (wave * YP + q) * 8 + lrow;
-    ysrc[q] = ((int64_t)min(j0 + R, ns - 1) << 4) + ((lslot ^ ((R >> 1) & 7)) << 1);
+    const int R = (wave * YP + q) * RPI + lrow;
+    ysrc[q] = ((int64_t)min(j0 + R, ns - 1) << 4) + ((lslot ^ ((R >> RSH) & SWZ)) << 1);
   }
   const int64_t blk = (int64_t)ns << 4;
   auto issue = [&](int t) {
     const int64_t kt = kt0 + t;
     const uint32_t base = lds0 + (uint32_t)((t % NST) * STAGE);
-    const double* g = AT + kt * blk;
+    const double* g = AT + ((kt * KT) >> 4) * blk + ((kt * KT) & 15);
 #pragma unroll
     for (int q = 0; q < XP; ++q) glds16(g + xsrc[q], base + (wave * XP + q) * 1024);
 #pragma unroll
     for (int q = 0; q < YP; ++q) glds16(g + ysrc[q], base + XB + (wave * YP + q) * 1024);
-    if (lane < 8) glds16(mean + kt * KT + (lane << 1), base + XB + YB + wave * 128);
+    if (!CENTRED && lane < KT / 2) glds16(mean + kt * KT + (lane << 1), base + XB + YB + wave * KT * 8);
   };
   f64x4 acc[4][4];
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[m][n] = (f64x4){0.0, 0.0, 0.0, 0.0};
-  if (nt > 0) issue(0);
-  const int fr = lane & 15, fk = lane >> 4, fs = (fr >> 1) & 7;
-  const int xrow = (wr * 64 + fr) << 4, yrow = (wc * 64 + fr) << 4;
+#pragma unroll
+  for (int t = 0; t < NST - 1; ++t)
+    if (t < nt) issue(t);
+  const int fr = lane & 15, fk = lane >> 4, fs = (fr >> RSH) & SWZ;
+  const int xrow = (wr * 64 + fr) * KT, yrow = (wc * 64 + fr) * KT;
   for (int t = 0; t < nt; ++t) {
-    // K-tile t landed (the only DMA outstanding); after the barrier every wave has also
-    // finished reading stage (t+1) % 2 (K-tile t-1), which K-tile t+1 now overwrites
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // K-tile t landed (K-tiles t+1 .. t+NST-2 may still be in flight); after the barrier every
+    // wave has also finished reading stage (t-1) % NST, which K-tile t+NST-1 now overwrites
+    if (t + NST - 2 < nt) wait_vmcnt<Q * (NST - 2)>();
+    else wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (t + 1 < nt) issue(t + 1);
+    if (t + NST - 1 < nt) issue(t + NST - 1);
     const char* st = smem + (t % NST) * STAGE;
     const double* Xs = reinterpret_cast<const double*>(st);
     const double* Ys = reinterpret_cast<const double*>(st + XB);
-    const double* Ms = reinterpret_cast<const double*>(st + XB + YB + wave * 128);
+    const double* Ms = reinterpret_cast<const double*>(st + XB + YB + wave * KT * 8);
 #pragma unroll
     for (int kk = 0; kk < KT; kk += 4) {
       const int k = kk + fk;
       const int koff = ((((k >> 1) ^ fs)) << 1) + (k & 1);
-      const double mk = Ms[k];
+      const double mk = CENTRED ? 0.0 : Ms[k];
       double a[4], bv[4];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) a[m] = CENTRED ? Xs[xrow + koff + m * 256] : Xs[xrow + koff + m * 256] - mk;
+      for (int m = 0; m < 4; ++m) a[m] = CENTRED ? Xs[xrow + koff + m * 16 * KT] : Xs[xrow + koff + m * 16 * KT] - mk;
 #pragma unroll
-      for (int n = 0; n < 4; ++n) bv[n] = CENTRED ? Ys[yrow + koff + n * 256] : Ys[yrow + koff + n * 256] - mk;
+      for (int n = 0; n < 4; ++n) bv[n] = CENTRED ? Ys[yrow + koff + n * 16 * KT] : Ys[yrow + koff + n * 16 * KT] - mk;
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -1051,8 +1100,8 @@ __global__ __launch_bounds__(256) void k_spatial_modes(const double* __restrict_
       for (int u = 0; u < U; ++u) cur[u] = nxt[u];
     }
   }
-  if (!valid) return;
   if (part) {
+    if (!valid) return;
     double* pp = part + ((int64_t)blockIdx.y * rowpad + r) * NMB;
 #pragma unroll
     for (int m = 0; m < NMB; m += 2) {
@@ -1061,11 +1110,31 @@ __global__ __launch_bounds__(256) void k_spatial_modes(const double* __restrict_
     }
     return;
   }
+  // Phi rows leave through LDS, a quarter of the block (128 rows) at a time, so the stores of
+  // the block's (512 rows x nm) region are contiguous (a thread's own 2 x nm values would be
+  // scattered 8-B stores, 2 nm * 8 B apart from lane to lane)
+  __shared__ double ph[128 * NMB];
   const double dn = (double)ns;
+  const int64_t rb0 = (int64_t)blockIdx.x * 512;
+  for (int h = 0; h < 4; ++h) {
+    __syncthreads();
+    if ((threadIdx.x >> 6) == h) {
+      const int lr = 2 * (threadIdx.x & 63);
 #pragma unroll
-  for (int m = 0; m < NMB; ++m) {
-    if (m < nm && r < rowlen) phi[r * ldphi + col0 + m] = (acc0[m] * inv_lam[col0 + m]) / dn;
-    if (m < nm && r + 1 < rowlen) phi[(r + 1) * ldphi + col0 + m] = (acc1[m] * inv_lam[col0 + m]) / dn;
+      for (int m = 0; m < NMB; ++m) {
+        if (m < nm) {
+          ph[lr * NMB + m] = (acc0[m] * inv_lam[col0 + m]) / dn;
+          ph[(lr + 1) * NMB + m] = (acc1[m] * inv_lam[col0 + m]) / dn;
+        }
+      }
+    }
+    __syncthreads();
+    const int64_t r0 = rb0 + 128 * h;
+    const int nr = (int)(rowlen - r0 < 128 ? rowlen - r0 : 128);
+    for (int e = threadIdx.x; e < nr * nm; e += 256) {
+      const int lr = e / nm, m = e - lr * nm;
+      phi[(r0 + lr) * ldphi + col0 + m] = ph[lr * NMB + m];
+    }
   }
 }
 
@@ -1154,51 +1223,35 @@ hipError_t launch_filter_x(int NX, const double* R, const double* bx, int ns, in
   }
 }
 
-// Row-tile height for the y/z kernel: 32 rows when 32 x ceil(K/16) z items fit 512 threads.
-// y/z tile: TJ rows x NT threads.  16 rows on 256 threads where the 16-wide output chunks
-// fit (K <= 256): two workgroups per CU (LDS ~58 KB each), so one block's loads overlap the
-// other's filter arithmetic -- worth more than the 32-row tile's smaller halo (1.375 vs
-// 1.75 reads per output row), whose 97 KB of LDS allowed one block per CU.
-// (The 32 x 512 tile for K <= 256 measured 12.2 against 11.2 ms of generation at C3.)
-static int yz_tj(int K) {
-  const int kch = (K + 15) / 16;
-  if (16 * kch <= 256) return 16256;
-  if (32 * kch <= 512) return 32;
-  if (16 * kch <= 512) return 16;
-  if (8 * kch <= 512) return 8;
-  return 0;
-}
+// y/z tile: 16 rows x 256 threads, 256-column tiles of K (one tile when K <= 256): two
+// workgroups per CU (LDS ~58 KB each), so one block's loads overlap the other's filter
+// arithmetic.  Measured alternatives at C3: a 32-row x 512-thread tile (smaller y halo, 97 KB of
+// LDS, one block per CU) 12.2 against 11.2 ms of generation.  Wider inlets (C4, C5) used to
+// take taller-than-wide tiles of the whole row (16 x 512 at K = 512, 8 x 512 at K = 1024:
+// a 2.5x y halo on the T1 reads); they now run this same tile over 256-column slices.
+constexpr int YZ_TJ = 16, YZ_NT = 256, YZ_KB = 256;
 
-template <int TJ, int NY, int NZC, int NT>
+template <int NY, int NZC>
 static hipError_t launch_fyz_t(const double* T1, const double* by, const double* bz, int NZ, int ns,
                                int jl, int K, int Kp, int64_t Sl, int ncomp, const double* lund,
                                int64_t lund_sj, int lund_mode, const double* rot, int rotate,
                                double* AT, hipStream_t st) {
-  const int ldt = (Kp + 16) + ((Kp + 16) >> 4) + 1;
-  const int ldl = K + (K >> 4) + 1;
+  constexpr int TJ = YZ_TJ, NT = YZ_NT;
+  const int KB = std::min(K, YZ_KB);
+  const int ldt = (KB + NZ - 1 + 16) + ((KB + NZ - 1 + 16) >> 4) + 1;
+  const int ldl = KB + (KB >> 4) + 1;
   const size_t lds = ((size_t)TJ * ldt + (lund_sj == 0 ? 9 * (size_t)ldl : 0)) * sizeof(double);
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_filter_yz<TJ, NY, NZC, NT>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   // enough blocks to fill the chip twice over, at most 16 steps each
   const int tiles = (jl + TJ - 1) / TJ;
-  const int nsb = (int)std::max<int64_t>(1, std::min<int64_t>(16, (int64_t)tiles * ns / 512));
-  const dim3 grid((unsigned)tiles, (unsigned)((ns + nsb - 1) / nsb));
+  const int ktiles = (K + KB - 1) / KB;
+  const int nsb = (int)std::max<int64_t>(1, std::min<int64_t>(16, (int64_t)tiles * ktiles * ns / 512));
+  const dim3 grid((unsigned)tiles, (unsigned)((ns + nsb - 1) / nsb), (unsigned)ktiles);
   hipLaunchKernelGGL((k_filter_yz<TJ, NY, NZC, NT>), grid, dim3(NT), lds, st, T1, by, bz, NZ, ns, jl, K,
-                     Kp, Sl, ncomp, lund, lund_sj, lund_mode, rot, rotate, AT, nsb);
+                     Kp, Sl, ncomp, lund, lund_sj, lund_mode, rot, rotate, AT, nsb, KB);
   return hipGetLastError();
-}
-
-template <int TJ, int NY, int NT>
-static hipError_t launch_fyz_tj(const double* T1, const double* by, const double* bz, int NZ, int ns,
-                                int jl, int K, int Kp, int64_t Sl, int ncomp, const double* lund,
-                                int64_t lund_sj, int lund_mode, const double* rot, int rotate,
-                                double* AT, hipStream_t st) {
-  if (NZ == NY)  // isotropic y/z widths: the z taps are compile-time too
-    return launch_fyz_t<TJ, NY, NY, NT>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj, lund_mode,
-                                        rot, rotate, AT, st);
-  return launch_fyz_t<TJ, NY, 0, NT>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj, lund_mode,
-                                     rot, rotate, AT, st);
 }
 
 template <int NY>
@@ -1207,17 +1260,11 @@ static hipError_t launch_fyz(const double* T1, const double* by, const double* b
                              int64_t lund_sj, int lund_mode, const double* rot, int rotate,
                              double* AT, hipStream_t st) {
   if (NZ > 25) return hipErrorInvalidValue;
-  switch (yz_tj(K)) {
-    case 16256: return launch_fyz_tj<16, NY, 256>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj,
-                                                 lund_mode, rot, rotate, AT, st);
-    case 32: return launch_fyz_tj<32, NY, 512>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj,
-                                          lund_mode, rot, rotate, AT, st);
-    case 16: return launch_fyz_tj<16, NY, 512>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj,
-                                          lund_mode, rot, rotate, AT, st);
-    case 8: return launch_fyz_tj<8, NY, 512>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj,
-                                        lund_mode, rot, rotate, AT, st);
-    default: return hipErrorInvalidConfiguration;
-  }
+  if (NZ == NY)  // isotropic y/z widths: the z taps are compile-time too
+    return launch_fyz_t<NY, NY>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj, lund_mode, rot,
+                                rotate, AT, st);
+  return launch_fyz_t<NY, 0>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj, lund_mode, rot, rotate,
+                             AT, st);
 }
 
 hipError_t launch_filter_yz(int NY, const double* T1, const double* by, const double* bz, int NZ,
@@ -1238,7 +1285,7 @@ hipError_t launch_filter_yz(int NY, const double* T1, const double* by, const do
 
 int filter_yz_max_K(int Kp) {
   (void)Kp;
-  return 1024;  // 8-row tiles x 64 chunks of 16 outputs on 512 threads (yz_tj)
+  return 4096;  // 256-column tiles (the y/z kernel has no K limit; tested to K = 1024)
 }
 
 hipError_t launch_mean(const double* AT, int64_t rowlen, int ns, const int* prog, int nprog,
@@ -1257,10 +1304,17 @@ hipError_t launch_center(double* AT, int64_t rowpad, int ns, const double* mean,
 // Number of K splits for the 128 x 128 lower-triangle tiles on 512 concurrent workgroups
 // (two per CU): ~8+ rounds, chosen to minimise the partial last round, >= 64 K-tiles of 16
 // per item.
+// SYRK configuration: K-tile 16, 2-stage ring, two workgroups per CU.  Measured at C3 against
+// it (r3, tools/syrk_probe.py, same data): K-tile 8 with a 4-stage ring (prefetch distance 24
+// instead of 16) 50.7 vs 48.8 ms, K-tile 8 / 3 stages / three workgroups per CU 49.5 ms,
+// K-tile 8 / 3 stages / two per CU 49.8 ms -- the shorter K-tiles' extra barriers cost more
+// than the deeper prefetch gains.
+constexpr int SYRK_KT = 16, SYRK_NST = 2, SYRK_OCC = 2;
+
 int syrk_plan(int ns, int64_t Kdim, int64_t* ksplit) {
   constexpr int KT = 16;
   const int nb = (ns + 127) / 128;
-  const int tiles = nb * (nb + 1) / 2, slots = 512;
+  const int tiles = nb * (nb + 1) / 2, slots = 256 * SYRK_OCC;
   const int64_t kts = Kdim / KT;
   const int64_t maxsplit = std::max<int64_t>(1, kts / 64);
   int64_t best = 1;
@@ -1285,15 +1339,17 @@ hipError_t launch_syrk(const double* AT, int ns, int64_t Kdim, const double* mea
                        int nsplit, int64_t ksplit, double* C, int64_t ldc, int divide, double* work, int centred,
                        hipStream_t st) {
   const int64_t slab = (int64_t)ns * ldc;
-  auto launch = [&](auto kern) -> hipError_t {
+  auto launch = [&](auto kern, int lds) -> hipError_t {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, syrk3::NST * syrk3::STAGE);
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3(nitems), dim3(256), syrk3::NST * syrk3::STAGE, st, AT, ns, Kdim, mean,
+    hipLaunchKernelGGL(kern, dim3(nitems), dim3(256), lds, st, AT, ns, Kdim, mean,
                        reinterpret_cast<const int4*>(items), nitems, ksplit, work, ldc, slab);
     return hipGetLastError();
   };
-  hipError_t le = centred ? launch(k_syrk_g128<1>) : launch(k_syrk_g128<0>);
+  constexpr int lds = SYRK_NST * SyrkCfg<SYRK_KT, SYRK_NST>::STAGE;
+  hipError_t le = centred ? launch(k_syrk_g128<1, SYRK_KT, SYRK_NST, SYRK_OCC>, lds)
+                          : launch(k_syrk_g128<0, SYRK_KT, SYRK_NST, SYRK_OCC>, lds);
   if (le != hipSuccess) return le;
   hipLaunchKernelGGL(k_syrk_reduce, dim3(((ns + 63) / 64) * ((ns + 63) / 64 + 1) / 2), dim3(256), 0, st, work,
                      nsplit, slab, ns, ldc, C, divide);

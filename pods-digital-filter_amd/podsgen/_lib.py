@@ -13,6 +13,7 @@ PODS_OK = 0
 PODS_LUND_1D = 0
 PODS_LUND_PRF = 1
 PODS_LUND_NONE = -1
+PODS_GEN_PLANES, PODS_GEN_XPASS, PODS_GEN_YZPASS, PODS_GEN_ALL = 1, 2, 4, 7  # include/podsgen.h
 
 c_int = ctypes.c_int
 c_i64 = ctypes.c_int64
@@ -42,6 +43,7 @@ SIGNATURES = {
     "pods_df_configure": (c_int, [c_void_p, ctypes.POINTER(DFParams), c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_void_p]),
     "pods_df_generate": (c_int, [c_void_p]),
+    "pods_df_generate_parts": (c_int, [c_void_p, c_int]),
     "pods_df_snapshots": (c_int, [c_void_p, ctypes.POINTER(c_void_p), ctypes.POINTER(c_i64)]),
     "pods_set_snapshots": (c_int, [c_void_p, c_void_p, c_int, c_i64]),
     "pods_copy_snapshots": (c_int, [c_void_p, c_int, c_int, c_void_p]),

@@ -66,6 +66,32 @@ class Context:
             self._side = torch.cuda.Stream(device=self.device)
         return self._side
 
+    def gen_stream(self):
+        """The stream the next run's random planes and x pass go to (Generator.prefetch_next)."""
+        if getattr(self, "_gen", None) is None:
+            self._gen = torch.cuda.Stream(device=self.device)
+        return self._gen
+
+    def on_stream(self, stream):
+        """Context manager: the pods context and torch's current stream are `stream` inside."""
+        ctx = self
+
+        class _S:
+            def __enter__(self):
+                self.main = torch.cuda.current_stream(ctx.device)
+                self.tc = torch.cuda.stream(stream)
+                self.tc.__enter__()
+                check(ctx.lib.pods_set_stream(ctx.h, ctypes.c_void_p(stream.cuda_stream)), "pods_set_stream")
+                return self
+
+            def __exit__(self, *exc):
+                try:
+                    check(ctx.lib.pods_set_stream(ctx.h, ctypes.c_void_p(self.main.cuda_stream)), "pods_set_stream")
+                finally:
+                    self.tc.__exit__(*exc)
+                return False
+        return _S()
+
     def close(self):
         if getattr(self, "h", None):
             self.lib.pods_destroy(self.h)
@@ -131,9 +157,36 @@ class Generator:
                                              ptr(k[3]), ptr(k[4])), "pods_df_configure")
         self.rowlen = 3 * (self.j1 - self.j0) * setup.kma
 
+    _ahead = None   # event behind the next run's planes + x pass (prefetch_next)
+
     def generate(self):
-        check(self.ctx.lib.pods_df_generate(self.ctx.h), "pods_df_generate")
+        """The whole generation on the current stream -- or, after prefetch_next(), only its y/z
+        part, behind the event of the planes and x pass already enqueued on the gen stream."""
+        if self._ahead is not None:
+            torch.cuda.current_stream(self.ctx.device).wait_event(self._ahead)
+            self._ahead = None
+            check(self.ctx.lib.pods_df_generate_parts(self.ctx.h, _lib.PODS_GEN_YZPASS), "pods_df_generate_parts")
+        else:
+            check(self.ctx.lib.pods_df_generate(self.ctx.h), "pods_df_generate")
         return self.snapshots()
+
+    def prefetch_next(self, timer=None):
+        """Enqueue the NEXT run's random planes (jump-ahead + MT19937) and x pass on the gen
+        stream, after everything the main stream has enqueued so far (this run's y/z pass has
+        consumed the planes and T1 by then).  They then run beside this run's mean, centring and
+        correlation: the MT generator and the x pass are VALU / memory work that fits next to the
+        SYRK's two workgroups per CU (16 and 92 VGPRs, 5 KB and no LDS).  The next generate()
+        waits for them and runs only the y/z part."""
+        tm = timer or (lambda name: _NullCtx())
+        gs = self.ctx.gen_stream()
+        gs.wait_stream(torch.cuda.current_stream(self.ctx.device))
+        with self.ctx.on_stream(gs):
+            with tm("generate_ahead"):
+                check(self.ctx.lib.pods_df_generate_parts(self.ctx.h, _lib.PODS_GEN_PLANES | _lib.PODS_GEN_XPASS),
+                      "pods_df_generate_parts")
+            ev = torch.cuda.Event()
+            ev.record(gs)
+        self._ahead = ev
 
     def snapshots(self):
         return DeviceSnapshots(self.ctx, self.setup.ns, self.rowlen, self.j0, self.j1, self.setup.kma)
@@ -728,16 +781,20 @@ class FourierBacklog:
 
 
 def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=None, gen=None, spectrum=None,
-             backlog=None):
+             backlog=None, prefetch_next=False):
     """The whole hot path; returns (Generator, PODResult, FourierResult | None).
     spectrum: a SpectrumQueue for multi-step runs (see run_pod).  backlog: a FourierBacklog --
     this step's Fourier result is then finished during the next step (or by backlog.flush())
-    and the returned FourierResult is None."""
+    and the returned FourierResult is None.  prefetch_next: a next run follows on this
+    generator; its random planes and x pass are enqueued on the gen stream right after this
+    run's y/z pass (Generator.prefetch_next), so they overlap this run's correlation."""
     dist_, rank, world = _dist_info(dist)
     tm = timer or (lambda name: _NullCtx())
     gen = gen or Generator(setup, device=device, rank=rank, world=world)
     with tm("generate"):
         snap = gen.generate()
+    if prefetch_next:
+        gen.prefetch_next(timer)
     pending = []
 
     def start_fourier(T, nmt, ready):

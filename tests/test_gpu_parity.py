@@ -241,6 +241,25 @@ def test_syrk_mfma_layout(ctx):
         del snap
 
 
+def test_prefetched_generation_matches(ctx):
+    """The next run's planes + x pass enqueued on the gen stream (Generator.prefetch_next) while
+    the main stream still works on this run: the following generate() (y/z part only) gives the
+    same snapshot matrix bit for bit, and a prefetched pipeline step the same POD."""
+    s = podsgen.DFSetup(jma=40, kma=27, ns=30, seed=5)
+    gen = E.Generator(s, ctx=ctx)
+    ref = gen.generate().to_host()
+    gen.prefetch_next()
+    mean = torch.empty(gen.rowlen, dtype=torch.float64, device="cuda")
+    podsgen.check(ctx.lib.pods_mean(ctx.h, E.ptr(mean), 1), "pods_mean")  # main-stream work meanwhile
+    assert np.array_equal(gen.generate().to_host(), ref)
+    s2 = podsgen.DFSetup(jma=24, kma=20, ns=64, seed=2024)
+    g2 = E.Generator(s2, ctx=ctx)
+    _, p1, f1 = E.pipeline(s2, gen=g2, prefetch_next=True)
+    _, p2, f2 = E.pipeline(s2, gen=g2)
+    assert np.array_equal(p1.energy, p2.energy) and p1.nm == p2.nm
+    assert torch.equal(p1.phi, p2.phi) and np.array_equal(f1.c, f2.c)
+
+
 def test_row_slabs_match_full(ctx):
     """Multi-GPU sharding on one device: 3 row slabs concatenate to the full generation."""
     s = podsgen.DFSetup(jma=20, kma=17, ns=11, seed=99)
@@ -341,8 +360,9 @@ def test_mid_case_vs_reference(ctx, golden_dir):
 
 
 @pytest.mark.parametrize("J,K,ns,kw", [
-    (9, 1024, 3, {}),                                             # C5 width: 8-row tiles, 64 z chunks
+    (9, 1024, 3, {}),                                             # C5 width: four 256-column tiles
     (11, 600, 4, {"dt": 0.05}),                                   # K not a multiple of 16, nfx != nfy
+    (37, 530, 3, {}),                                             # ragged row and column tiles
 ])
 def test_generate_wide_inlet_vs_oracle(ctx, J, K, ns, kw):
     """kma up to 1024 (BASELINE config 5's 1024-point span): bit-exact against the oracle."""

@@ -1,4 +1,5 @@
-"""Time pods_corr alone at J x K x NS: python tools/syrk_probe.py J K NS reps"""
+"""Time pods_corr alone at J x K x NS: python tools/syrk_probe.py J K NS reps [regen]
+(regen: generate + mean + centre before every timed call, as in a pipeline step)"""
 import os, sys, time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "pods-digital-filter_amd"))
 import numpy as np, torch, podsgen
@@ -12,7 +13,12 @@ podsgen.check(ctx.lib.pods_mean(ctx.h, E.ptr(mean), 1))
 podsgen.check(ctx.lib.pods_center(ctx.h))  # the production path: A centred in place
 C = torch.empty((NS, NS), dtype=torch.float64, device="cuda")
 flops = 3 * J * K * NS * (NS + 1)
+regen = len(sys.argv) > 5 and sys.argv[5] == "regen"
 for r in range(reps):
+    if regen:
+        gen.generate()
+        podsgen.check(ctx.lib.pods_mean(ctx.h, E.ptr(mean), 1))
+        podsgen.check(ctx.lib.pods_center(ctx.h))
     torch.cuda.synchronize(); t = time.time()
     podsgen.check(ctx.lib.pods_corr(ctx.h, E.ptr(C), 1))
     torch.cuda.synchronize(); dt = time.time() - t
