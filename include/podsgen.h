@@ -85,16 +85,18 @@ int pods_df_configure(pods_ctx* ctx, const pods_df_params* params, const double*
  * The snapshot matrix stays on the device, snapshot-major: A_T[i][c*P_local + p]. */
 int pods_df_generate(pods_ctx* ctx);
 /* The same generation in parts, each on the context's current stream (pods_set_stream), so a
- * caller can run the random planes and the x pass of the NEXT run on a second stream while this
- * run's correlation occupies the first (main :1361-1367, :1454-1467 draw the planes; filter
- * :100-140 axis 0 is the x pass; axes 1-2 + adapt + rotate + A[:,i] = ... :1471 the y/z part).
- * parts: bit 0 = random planes (jump-ahead + MT19937), bit 1 = x pass, bit 2 = y/z pass (the
- * snapshot matrix).  Parts run in that order; PODS_GEN_ALL = 7 equals pods_df_generate.
- * The caller orders the streams (the x pass needs the planes, the y/z pass the x pass). */
-#define PODS_GEN_PLANES 1
-#define PODS_GEN_XPASS 2
-#define PODS_GEN_YZPASS 4
-#define PODS_GEN_ALL 7
+ * caller can run the random planes of the NEXT run on a second stream while this run's
+ * centring and correlation occupy the first (main :1361-1367, :1454-1467 draw the planes;
+ * filter :100-140 axis 0 is the x pass; axes 1-2 + adapt + rotate + A[:,i] = ... :1471 the y/z
+ * part).  parts: bit 0 = jump-ahead of the MT19937 substreams, bit 1 = the substreams' random
+ * planes, bit 2 = x pass, bit 3 = y/z pass (the snapshot matrix).  Parts run in that order;
+ * PODS_GEN_ALL = 15 equals pods_df_generate.  The caller orders the streams (each part needs
+ * the one before). */
+#define PODS_GEN_JUMP 1
+#define PODS_GEN_PLANES 2
+#define PODS_GEN_XPASS 4
+#define PODS_GEN_YZPASS 8
+#define PODS_GEN_ALL 15
 int pods_df_generate_parts(pods_ctx* ctx, int parts);
 /* Device pointer and row length (= 3*P_local) of the snapshot matrix.  Device layout is
  * K-tiled: element (snapshot i, row r of the reference A) is at

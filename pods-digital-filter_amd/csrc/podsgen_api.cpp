@@ -524,8 +524,10 @@ int pods_df_generate_parts(pods_ctx* c, int parts) {
   PODS_HIP(hipSetDevice(c->device));
   const pods_df_params& p = c->p;
   const RngLayout& L = c->layout;
-  if (parts & PODS_GEN_PLANES) {
+  if (parts & PODS_GEN_JUMP) {
     if (int e = run_jumps(c, L, c->rng)) return e;
+  }
+  if (parts & PODS_GEN_PLANES) {
     PODS_HIP(pods::launch_mt_generate(c->rng.states.as<uint32_t>(), L.G, L.Bs, L.ntot, c->S, c->Kp, p.j0,
                                       p.j1 + 2 * p.nfy, c->Sl, p.rng_low, p.rng_range, c->R.as<double>(),
                                       c->stream));

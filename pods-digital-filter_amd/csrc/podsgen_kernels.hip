@@ -277,8 +277,12 @@ __global__ __launch_bounds__(256) void k_mt_generate_full(const uint32_t* __rest
                                                           int64_t Bs, int64_t ntot, double low,
                                                           double range, double* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint32_t buf[2][MTN];
-  const int g = blockIdx.x, t = threadIdx.x;
-  if (g >= G) return;
+  const int t = threadIdx.x;
+  // (a grid smaller than G would take the substreams in turn; spreading the generation over
+  // 64-256 workgroups beside the SYRK measured 46-77 ms against 2.4: each substream is a
+  // latency-bound twist chain, so the substreams must run side by side)
+  for (int g = blockIdx.x; g < G; g += gridDim.x) {
+  __syncthreads();  // the previous substream's last tempering read buf
   for (int i = t; i < MTN; i += 256) buf[0][i] = states[(size_t)g * MTN + i];
   __syncthreads();
   const int64_t D0 = (int64_t)g * Bs * 312;
@@ -305,6 +309,7 @@ __global__ __launch_bounds__(256) void k_mt_generate_full(const uint32_t* __rest
     if (!tw) break;
     __syncthreads();  // nxt complete; cur (tempered above) becomes the next nxt
   }
+  }
 }
 
 // Row-slab generator (multi-GPU: this rank's rows [rlo, rhi) of every padded plane, the
@@ -319,8 +324,9 @@ __global__ __launch_bounds__(256) void k_mt_generate_slab(const uint32_t* __rest
                                                           int rlo, int rhi, int64_t Sl, double low,
                                                           double range, double* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint32_t buf[2][MTN];
-  const int g = blockIdx.x, t = threadIdx.x;
-  if (g >= G) return;
+  const int t = threadIdx.x;
+  for (int g = blockIdx.x; g < G; g += gridDim.x) {
+  __syncthreads();
   for (int i = t; i < MTN; i += 256) buf[0][i] = states[(size_t)g * MTN + i];
   __syncthreads();
   const int64_t D0 = (int64_t)g * Bs * 312;
@@ -363,6 +369,7 @@ __global__ __launch_bounds__(256) void k_mt_generate_slab(const uint32_t* __rest
     }
     if (!tw) break;
     __syncthreads();  // nxt complete; cur (tempered above) becomes the next nxt
+  }
   }
 }
 
@@ -412,13 +419,16 @@ template <int NX, int PD>
 __global__ __launch_bounds__(256) void k_filter_x2(const double* __restrict__ R,
                                                    const double* __restrict__ bx, int ns,
                                                    int64_t Sl, int steps_per_chunk,
-                                                   double* __restrict__ T1) {
-  const int64_t pp = (int64_t)blockIdx.x * 256 + threadIdx.x;  // point pair
-  const int c = blockIdx.y;
-  if (2 * pp >= Sl) return;
-  const int i0 = blockIdx.z * steps_per_chunk;
+                                                   double* __restrict__ T1, int nbx, int ncomp, int nch) {
+  // virtual blocks (point block, component, step chunk), one per workgroup
+  const int nvb = nbx * ncomp * nch;
+  for (int vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
+  const int bxi = vb % nbx, c = (vb / nbx) % ncomp, bz = vb / (ncomp * nbx);
+  const int64_t pp = (int64_t)bxi * 256 + threadIdx.x;  // point pair
+  if (2 * pp >= Sl) continue;
+  const int i0 = bz * steps_per_chunk;
   const int i1 = min(ns, i0 + steps_per_chunk);
-  if (i0 >= i1) return;
+  if (i0 >= i1) continue;
   double b[NX];
 #pragma unroll
   for (int a = 0; a < NX; ++a) b[a] = bx[NX - 1 - a];
@@ -447,6 +457,7 @@ __global__ __launch_bounds__(256) void k_filter_x2(const double* __restrict__ R,
     T2[((int64_t)c * ns + i) * Sl2 + pp] = make_double2(ax, ay);
 #pragma unroll
     for (int a = 0; a < NX - 1; ++a) w[a] = w[a + 1];
+  }
   }
 }
 
@@ -1168,13 +1179,14 @@ hipError_t launch_mt_generate(const uint32_t* states, int G, int64_t Bs, int64_t
                               int Kp, int rlo, int rhi, int64_t Sl, double low, double range,
                               double* out, hipStream_t st) {
   if (G <= 0) return hipSuccess;
+  const int gw = G;
   if (rlo == 0 && (int64_t)rhi * Kp == S && Sl == S && ((uintptr_t)out & 15) == 0 && Bs % 2 == 0) {
     // whole planes: out[D] for stream double D (even block starts keep the 16-B stores aligned)
-    hipLaunchKernelGGL(k_mt_generate_full, dim3(G), dim3(256), 0, st, states, G, Bs, ntot, low, range, out);
+    hipLaunchKernelGGL(k_mt_generate_full, dim3(gw), dim3(256), 0, st, states, G, Bs, ntot, low, range, out);
     return hipGetLastError();
   }
   if (S >= 312) {
-    hipLaunchKernelGGL(k_mt_generate_slab, dim3(G), dim3(256), 0, st, states, G, Bs, ntot, S, Kp, rlo, rhi,
+    hipLaunchKernelGGL(k_mt_generate_slab, dim3(gw), dim3(256), 0, st, states, G, Bs, ntot, S, Kp, rlo, rhi,
                        Sl, low, range, out);
     return hipGetLastError();
   }
@@ -1197,8 +1209,10 @@ static hipError_t launch_fx(const double* R, const double* bx, int ns, int64_t S
     const int64_t nch0 = std::max<int64_t>(1, std::min<int64_t>(ns, want / std::max<int64_t>(1, bx_ * ncomp)));
     const int chunk2 = (int)((ns + nch0 - 1) / nch0);
     const int nch = (ns + chunk2 - 1) / chunk2;
-    dim3 grid((unsigned)bx_, (unsigned)ncomp, (unsigned)nch);
-    hipLaunchKernelGGL((k_filter_x2<NX, 8>), grid, dim3(256), 0, st, R, bx, ns, Sl, chunk2, T1);
+    const int64_t nvb = bx_ * ncomp * nch;
+    const int64_t grid = nvb;
+    hipLaunchKernelGGL((k_filter_x2<NX, 8>), dim3((unsigned)grid), dim3(256), 0, st, R, bx, ns, Sl, chunk2, T1,
+                       (int)bx_, ncomp, nch);
     return hipGetLastError();
   }
   const int nch = (ns + chunk - 1) / chunk;

@@ -13,7 +13,7 @@ PODS_OK = 0
 PODS_LUND_1D = 0
 PODS_LUND_PRF = 1
 PODS_LUND_NONE = -1
-PODS_GEN_PLANES, PODS_GEN_XPASS, PODS_GEN_YZPASS, PODS_GEN_ALL = 1, 2, 4, 7  # include/podsgen.h
+PODS_GEN_JUMP, PODS_GEN_PLANES, PODS_GEN_XPASS, PODS_GEN_YZPASS, PODS_GEN_ALL = 1, 2, 4, 8, 15  # podsgen.h
 
 c_int = ctypes.c_int
 c_i64 = ctypes.c_int64

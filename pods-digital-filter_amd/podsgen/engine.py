@@ -157,36 +157,53 @@ class Generator:
                                              ptr(k[3]), ptr(k[4])), "pods_df_configure")
         self.rowlen = 3 * (self.j1 - self.j0) * setup.kma
 
-    _ahead = None   # event behind the next run's planes + x pass (prefetch_next)
+    _ahead = None   # event behind the next run's random planes (prefetch_*)
 
     def generate(self):
-        """The whole generation on the current stream -- or, after prefetch_next(), only its y/z
-        part, behind the event of the planes and x pass already enqueued on the gen stream."""
+        """The whole generation on the current stream -- or, after prefetch_jump() and
+        prefetch_planes(), its x and y/z passes behind the event of the planes already
+        enqueued on the gen stream."""
         if self._ahead is not None:
             torch.cuda.current_stream(self.ctx.device).wait_event(self._ahead)
             self._ahead = None
-            check(self.ctx.lib.pods_df_generate_parts(self.ctx.h, _lib.PODS_GEN_YZPASS), "pods_df_generate_parts")
+            check(self.ctx.lib.pods_df_generate_parts(self.ctx.h, _lib.PODS_GEN_XPASS | _lib.PODS_GEN_YZPASS),
+                  "pods_df_generate_parts")
         else:
             check(self.ctx.lib.pods_df_generate(self.ctx.h), "pods_df_generate")
         return self.snapshots()
 
-    def prefetch_next(self, timer=None):
-        """Enqueue the NEXT run's random planes (jump-ahead + MT19937) and x pass on the gen
-        stream, after everything the main stream has enqueued so far (this run's y/z pass has
-        consumed the planes and T1 by then).  They then run beside this run's mean, centring and
-        correlation: the MT generator and the x pass are VALU / memory work that fits next to the
-        SYRK's two workgroups per CU (16 and 92 VGPRs, 5 KB and no LDS).  The next generate()
-        waits for them and runs only the y/z part."""
+    def _on_gen_stream(self, parts, timer, name):
         tm = timer or (lambda name: _NullCtx())
         gs = self.ctx.gen_stream()
         gs.wait_stream(torch.cuda.current_stream(self.ctx.device))
         with self.ctx.on_stream(gs):
-            with tm("generate_ahead"):
-                check(self.ctx.lib.pods_df_generate_parts(self.ctx.h, _lib.PODS_GEN_PLANES | _lib.PODS_GEN_XPASS),
-                      "pods_df_generate_parts")
+            with tm(name):
+                check(self.ctx.lib.pods_df_generate_parts(self.ctx.h, parts), "pods_df_generate_parts")
             ev = torch.cuda.Event()
             ev.record(gs)
         self._ahead = ev
+
+    def prefetch_jump(self, timer=None):
+        """Enqueue the NEXT run's MT19937 jump-ahead on the gen stream, after everything the main
+        stream holds so far (call it after this run's generation: the substream states are free
+        again).  It runs beside this run's mean and centring (an LDS-bound kernel beside two
+        HBM-bound ones)."""
+        self._on_gen_stream(_lib.PODS_GEN_JUMP, timer, "gen_jump_ahead")
+
+    def prefetch_planes(self, timer=None):
+        """Enqueue the NEXT run's random planes on the gen stream after the main stream's current
+        point (call it once this run's x pass is done -- it is, after the y/z pass -- and just
+        before the correlation): the MT generator (16 VGPRs, 5 KB of LDS, VALU work and 16-B
+        stores) runs beside the SYRK's two workgroups per CU.  The next generate() waits for it
+        and runs the x and y/z passes."""
+        self._on_gen_stream(_lib.PODS_GEN_PLANES, timer, "gen_planes_ahead")
+
+    def join_ahead(self):
+        """Make the current stream wait for the prefetched planes (if any): called before the
+        persistent eigensolver kernels, which need every CU's registers and must not find
+        generator workgroups in the way."""
+        if self._ahead is not None:
+            torch.cuda.current_stream(self.ctx.device).wait_event(self._ahead)
 
     def snapshots(self):
         return DeviceSnapshots(self.ctx, self.setup.ns, self.rowlen, self.j0, self.j1, self.setup.kma)
@@ -510,7 +527,7 @@ def eigen_solve(ctx: Context, C, ns, nm, tol_CN, full_temporal, tm=None, world=1
 
 
 def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=False,
-            keep_C=False, timer=None, on_temporal=None, spectrum=None, before_eigen=None):
+            keep_C=False, timer=None, on_temporal=None, spectrum=None, before_eigen=None, before_corr=None):
     """PODFS.POD (PODFS.py:1294-1393) with correct_for_cell_volumes='false'.
 
     spectrum: a SpectrumQueue -- the eigenvalues past the nm leading ones are then computed by
@@ -522,6 +539,9 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
     spatial pass does not wait for the host to launch the Fourier stage), on several ranks
     before the broadcasts.  pipeline() starts the Fourier stage there on a side stream that
     waits for `ready` only, so it runs beside the spatial-mode pass.
+
+    before_corr(), if given, is called after the centring is enqueued, before the correlation
+    (pipeline() starts the next run's random planes there, beside the SYRK).
 
     before_eigen(), if given, is called once the correlation is enqueued, before the first
     host synchronisation of the eigensolve (pipeline() finishes the previous step's Fourier
@@ -537,6 +557,8 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
     with tm("center"):  # main() :1493-1495, in place
         check(lib.pods_center(ctx.h), "pods_center")
     C = torch.empty((ns, ns), dtype=torch.float64, device=dev)
+    if before_corr is not None:
+        before_corr()
     with tm("corr"):
         check(lib.pods_corr(ctx.h, ptr(C), 1 if world == 1 else 0), "pods_corr")
     if world > 1:
@@ -787,22 +809,27 @@ def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=Non
     this step's Fourier result is then finished during the next step (or by backlog.flush())
     and the returned FourierResult is None.  prefetch_next: a next run follows on this
     generator; its random planes and x pass are enqueued on the gen stream right after this
-    run's y/z pass (Generator.prefetch_next), so they overlap this run's correlation."""
+    run's generation: the jump-ahead beside this run's mean and centring, the MT generator
+    beside its correlation (Generator.prefetch_jump / prefetch_planes)."""
     dist_, rank, world = _dist_info(dist)
     tm = timer or (lambda name: _NullCtx())
     gen = gen or Generator(setup, device=device, rank=rank, world=world)
     with tm("generate"):
         snap = gen.generate()
     if prefetch_next:
-        gen.prefetch_next(timer)
+        gen.prefetch_jump(timer)
     pending = []
 
     def start_fourier(T, nmt, ready):
         pending.append(launch_fourier(gen.ctx, T, nmt, setup.ns, setup.dt_eff, setup.et, timer=timer,
                                       side=True, ready=ready))
+    def before_eigen():
+        gen.join_ahead()
+        if backlog is not None:
+            backlog.finish_pending()
     pod = run_pod(snap, setup.nm, dist=dist_, full_temporal=full_temporal, timer=timer,
-                  on_temporal=start_fourier, spectrum=spectrum,
-                  before_eigen=backlog.finish_pending if backlog is not None else None)
+                  on_temporal=start_fourier, spectrum=spectrum, before_eigen=before_eigen,
+                  before_corr=(lambda: gen.prefetch_planes(timer)) if prefetch_next else None)
     if backlog is not None:
         backlog.pending.append(pending[0] if pending else None)
         return gen, pod, None
