@@ -253,8 +253,8 @@ def main():
         return E.pipeline(setup, device=device, dist=d, gen=gen, timer=timer, spectrum=spectrum, backlog=backlog,
                           prefetch_next=ahead)
 
-    # ahead: the next step's jump-ahead and random planes run on a second stream beside this
-    # step's mean/centring and correlation (Generator.prefetch_jump / prefetch_planes).  The last warm-up step and the last timed step do
+    # ahead: the next step's MT19937 jump-ahead runs on a second stream beside this step's mean
+    # and centring (Generator.prefetch_jump).  The last warm-up step and the last timed step do
     # not prefetch, so the timed region holds exactly `steps` whole generations.
     for w in range(args.warmup):
         step(ahead=w < args.warmup - 1)
@@ -342,9 +342,8 @@ def main():
                          "flops_per_launch": flops},
             "stages_ms": {k: round(v, 3) for k, v in stages.items()},
             "stages_note": ("per-step means of HIP-event times on the stream each stage runs on; "
-                            "gen_jump_ahead / gen_planes_ahead (the next step's MT19937 jump-ahead and "
-                            "random planes) run on a second stream beside mean+center / corr, so the "
-                            "stages overlap and do not sum to ms_per_step"),
+                            "gen_jump_ahead (the next step's MT19937 jump-ahead) runs on a second "
+                            "stream beside mean+center, so the stages do not sum to ms_per_step"),
             "results": {"nm": int(pod.nm), "num_valid": None if num_valid is None else int(num_valid),
                         "eigensolve": "split: leading pairs by subspace iteration + full spectrum spread over "
                                       "steps (SpectrumQueue)" if spectrum is not None else "fused (pods_syev)",

@@ -157,17 +157,17 @@ class Generator:
                                              ptr(k[3]), ptr(k[4])), "pods_df_configure")
         self.rowlen = 3 * (self.j1 - self.j0) * setup.kma
 
-    _ahead = None   # event behind the next run's random planes (prefetch_*)
+    _ahead = None   # event behind the next run's jump-ahead (prefetch_jump)
 
     def generate(self):
-        """The whole generation on the current stream -- or, after prefetch_jump() and
-        prefetch_planes(), its x and y/z passes behind the event of the planes already
-        enqueued on the gen stream."""
+        """The whole generation on the current stream -- or, after prefetch_jump(), the planes,
+        x and y/z passes behind the event of the jump-ahead already enqueued on the gen stream."""
         if self._ahead is not None:
             torch.cuda.current_stream(self.ctx.device).wait_event(self._ahead)
             self._ahead = None
-            check(self.ctx.lib.pods_df_generate_parts(self.ctx.h, _lib.PODS_GEN_XPASS | _lib.PODS_GEN_YZPASS),
-                  "pods_df_generate_parts")
+            check(self.ctx.lib.pods_df_generate_parts(
+                self.ctx.h, _lib.PODS_GEN_PLANES | _lib.PODS_GEN_XPASS | _lib.PODS_GEN_YZPASS),
+                "pods_df_generate_parts")
         else:
             check(self.ctx.lib.pods_df_generate(self.ctx.h), "pods_df_generate")
         return self.snapshots()
@@ -186,22 +186,18 @@ class Generator:
     def prefetch_jump(self, timer=None):
         """Enqueue the NEXT run's MT19937 jump-ahead on the gen stream, after everything the main
         stream holds so far (call it after this run's generation: the substream states are free
-        again).  It runs beside this run's mean and centring (an LDS-bound kernel beside two
-        HBM-bound ones)."""
+        again).  It runs beside this run's mean and centring: an LDS-bound kernel (3 workgroups
+        per CU) beside two HBM-bound ones, which it does not slow (r3: 1.27 ms hidden, centring
+        2.19 ms either way).  The next generate() waits for it.
+        (The random planes were tried on the gen stream too: beside the centring they doubled
+        its time -- both stream 7-13 GB through HBM -- and beside the SYRK they took 10.9 ms
+        instead of 2.4 and cost the SYRK 2.7 ms, no net gain; spread over 64-256 workgroups they
+        took 46-77 ms, each substream being a latency-bound twist chain.)"""
         self._on_gen_stream(_lib.PODS_GEN_JUMP, timer, "gen_jump_ahead")
 
-    def prefetch_planes(self, timer=None):
-        """Enqueue the NEXT run's random planes on the gen stream after the main stream's current
-        point (call it once this run's x pass is done -- it is, after the y/z pass -- and just
-        before the correlation): the MT generator (16 VGPRs, 5 KB of LDS, VALU work and 16-B
-        stores) runs beside the SYRK's two workgroups per CU.  The next generate() waits for it
-        and runs the x and y/z passes."""
-        self._on_gen_stream(_lib.PODS_GEN_PLANES, timer, "gen_planes_ahead")
-
     def join_ahead(self):
-        """Make the current stream wait for the prefetched planes (if any): called before the
-        persistent eigensolver kernels, which need every CU's registers and must not find
-        generator workgroups in the way."""
+        """Make the current stream wait for the prefetched jump-ahead (if any): called before the
+        persistent eigensolver kernels, which must not find generator workgroups in the way."""
         if self._ahead is not None:
             torch.cuda.current_stream(self.ctx.device).wait_event(self._ahead)
 
@@ -809,8 +805,8 @@ def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=Non
     this step's Fourier result is then finished during the next step (or by backlog.flush())
     and the returned FourierResult is None.  prefetch_next: a next run follows on this
     generator; its random planes and x pass are enqueued on the gen stream right after this
-    run's generation: the jump-ahead beside this run's mean and centring, the MT generator
-    beside its correlation (Generator.prefetch_jump / prefetch_planes)."""
+    run's generation: the MT19937 jump-ahead, beside this run's mean and centring
+    (Generator.prefetch_jump)."""
     dist_, rank, world = _dist_info(dist)
     tm = timer or (lambda name: _NullCtx())
     gen = gen or Generator(setup, device=device, rank=rank, world=world)
@@ -828,8 +824,7 @@ def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=Non
         if backlog is not None:
             backlog.finish_pending()
     pod = run_pod(snap, setup.nm, dist=dist_, full_temporal=full_temporal, timer=timer,
-                  on_temporal=start_fourier, spectrum=spectrum, before_eigen=before_eigen,
-                  before_corr=(lambda: gen.prefetch_planes(timer)) if prefetch_next else None)
+                  on_temporal=start_fourier, spectrum=spectrum, before_eigen=before_eigen)
     if backlog is not None:
         backlog.pending.append(pending[0] if pending else None)
         return gen, pod, None

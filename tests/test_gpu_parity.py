@@ -242,17 +242,16 @@ def test_syrk_mfma_layout(ctx):
 
 
 def test_prefetched_generation_matches(ctx):
-    """The next run's jump-ahead and random planes enqueued on the gen stream
-    (Generator.prefetch_jump / prefetch_planes) while the main stream still works on this run:
-    the following generate() (x and y/z passes) gives the same snapshot matrix bit for bit, and
-    a prefetched pipeline step the same POD."""
+    """The next run's MT19937 jump-ahead enqueued on the gen stream (Generator.prefetch_jump)
+    while the main stream still works on this run: the following generate() (planes, x and y/z
+    passes) gives the same snapshot matrix bit for bit, and a prefetched pipeline step the same
+    POD."""
     s = podsgen.DFSetup(jma=40, kma=27, ns=30, seed=5)
     gen = E.Generator(s, ctx=ctx)
     ref = gen.generate().to_host()
     gen.prefetch_jump()
     mean = torch.empty(gen.rowlen, dtype=torch.float64, device="cuda")
     podsgen.check(ctx.lib.pods_mean(ctx.h, E.ptr(mean), 1), "pods_mean")  # main-stream work meanwhile
-    gen.prefetch_planes()
     podsgen.check(ctx.lib.pods_center(ctx.h), "pods_center")
     assert np.array_equal(gen.generate().to_host(), ref)
     s2 = podsgen.DFSetup(jma=24, kma=20, ns=64, seed=2024)
