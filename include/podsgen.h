@@ -157,6 +157,10 @@ int pods_unpack_lower(pods_ctx* ctx, const double* packed_dev, int n, double div
  * synchronising the bound stream. */
 int pods_temporal_modes(pods_ctx* ctx, const double* V_dev, int64_t v_rs, int64_t v_cs,
                         const double* lambda_desc_host, int nvalid, int ncols, double* T_dev);
+/* The same with the eigenvalues on the device (lambda_desc_dev, e.g. pods_syev's output), so
+ * the temporal modes can be enqueued before the host has seen the spectrum. */
+int pods_temporal_modes_dev(pods_ctx* ctx, const double* V_dev, int64_t v_rs, int64_t v_cs,
+                            const double* lambda_desc_dev, int nvalid, int ncols, double* T_dev);
 
 /* Symmetric eigensolve of the POD (replaces `linalg.eig(C)` + `sort_eigenvalues`,
  * PODFS.py:1309-1310 and :1430-1447): all n eigenvalues in descending order and the unit
@@ -177,6 +181,10 @@ int pods_sytrd_trace(pods_ctx* ctx, const double* C_dev, int n, int wg, int64_t*
 /* 0 if the last pods_syev / pods_sytrd ran to completion, PODS_ERR_INTERNAL if its
  * cross-workgroup wait timed out (results invalid).  Synchronises the stream. */
 int pods_syev_status(pods_ctx* ctx);
+/* The two abort words of the last pods_syev (tridiagonalisation, back-transformation; both 0
+ * when it completed) copied to flags_host (2 x uint32, pinned for a truly asynchronous copy),
+ * stream-ordered, without synchronising: the caller waits on an event behind it. */
+int pods_syev_flags_async(pods_ctx* ctx, uint32_t* flags_host);
 
 /* All n eigenvalues of C alone (the full spectrum POD.eigenvalues.dat and the valid-mode count
  * consume, PODFS.py:1309-1320, :1339), as a sequence of stream-ordered units that a caller can
@@ -239,6 +247,9 @@ int pods_syev2_inspect(pods_ctx* ctx, int n, int nvec, int what, double* out_hos
  * lambda_host is copied before the call returns; stream-ordered (no synchronisation). */
 int pods_spatial_modes(pods_ctx* ctx, const double* T_dev, int ldT, const double* lambda_host,
                        int nm, double* phi_dev);
+/* The same with lambda on the device (1/lambda formed there, IEEE division as numpy's). */
+int pods_spatial_modes_dev(pods_ctx* ctx, const double* T_dev, int ldT, const double* lambda_dev,
+                           int nm, double* phi_dev);
 
 /* Twiddle table of the DFT below, made on the host by the reference expression itself
  * (podsgen.host.dft_twiddles: np.exp(-1j*2*k*np.pi*time/period), PODFS.py:1566) so that the

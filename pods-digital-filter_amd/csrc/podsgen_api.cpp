@@ -828,6 +828,37 @@ int pods_temporal_modes(pods_ctx* c, const double* V, int64_t v_rs, int64_t v_cs
   PODS_CATCH
 }
 
+int pods_temporal_modes_dev(pods_ctx* c, const double* V, int64_t v_rs, int64_t v_cs,
+                            const double* lam_desc_dev, int nvalid, int ncols, double* T) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!V || !T || !lam_desc_dev) return fail(PODS_ERR_ARG, "null pointer");
+  const int ns = c->have_snapshots ? c->p.ns : 0;
+  if (ns <= 0) return fail(PODS_ERR_STATE, "no snapshots");
+  if (ncols <= 0 || ncols > ns || nvalid > ncols) return fail(PODS_ERR_ARG, "bad ncols/nvalid");
+  PODS_HIP(ensure(c->mag, (size_t)ncols * sizeof(double)));
+  PODS_HIP(pods::launch_temporal(V, v_rs, v_cs, ns, ncols, std::max(nvalid, 0), lam_desc_dev,
+                                 c->mag.as<double>(), T, c->stream));
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_spatial_modes_dev(pods_ctx* c, const double* T, int ldT, const double* lam_dev, int nm, double* phi) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!c->have_snapshots || !c->mean_valid) return fail(PODS_ERR_STATE, "pods_spatial_modes needs pods_mean");
+  if (!T || !lam_dev || !phi || nm <= 0 || ldT < nm) return fail(PODS_ERR_ARG, "bad arguments");
+  PODS_HIP(ensure(c->inv_lam, (size_t)nm * sizeof(double)));
+  PODS_HIP(pods::launch_recip(lam_dev, nm, c->inv_lam.as<double>(), c->stream));
+  const size_t wb = pods::spatial_work_bytes(c->rowlen, c->p.ns);
+  if (wb) PODS_HIP(ensure(c->spwork, wb));
+  PODS_HIP(pods::launch_spatial(c->A.as<double>(), c->rowlen, c->p.ns,
+                                c->centered ? c->zero.as<double>() : c->mean.as<double>(), T, ldT, nm,
+                                c->inv_lam.as<double>(), phi, wb ? c->spwork.as<double>() : nullptr, c->stream));
+  return PODS_OK;
+  PODS_CATCH
+}
+
 int pods_spatial_modes(pods_ctx* c, const double* T, int ldT, const double* lam, int nm, double* phi) {
   PODS_TRY
   if (int e = check_ctx(c)) return e;
@@ -1137,6 +1168,17 @@ int pods_sytrd_trace(pods_ctx* c, const double* C, int n, int wg, int64_t* trace
   (void)hipStreamSynchronize(c->stream);
   release(tb);
   return e;
+  PODS_CATCH
+}
+
+int pods_syev_flags_async(pods_ctx* c, uint32_t* flags_host) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!flags_host) return fail(PODS_ERR_ARG, "flags_host is null");
+  if (!c->e_flags.p) return fail(PODS_ERR_STATE, "no pods_syev ran");
+  PODS_HIP(hipMemcpyAsync(flags_host, c->e_flags.as<uint32_t>(), 2 * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                          c->stream));
+  return PODS_OK;
   PODS_CATCH
 }
 

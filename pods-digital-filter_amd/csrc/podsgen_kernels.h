@@ -51,6 +51,7 @@ hipError_t launch_pack_lower(const double* C, int64_t ldc, int n, double* packed
 // C[r][c] = C[c][r] = packed[r(r+1)/2 + c] / divisor
 hipError_t launch_unpack_lower(const double* packed, int n, double divisor, double* C, int64_t ldc,
                                hipStream_t st);
+hipError_t launch_recip(const double* x, int n, double* y, hipStream_t st);
 hipError_t launch_temporal(const double* V, int64_t v_rs, int64_t v_cs, int ns, int ncols,
                            int nvalid, const double* lam, double* mag, double* T, hipStream_t st);
 size_t spatial_work_bytes(int64_t rowlen, int ns);

@@ -992,6 +992,18 @@ __global__ __launch_bounds__(256) void k_syrk_reduce(const double* __restrict__ 
   }
 }
 
+// 1/lambda (np.ones(nm)/energy, PODFS.py:1331): IEEE division, as numpy's
+__global__ void k_recip(const double* __restrict__ x, int n, double* __restrict__ y) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = 1.0 / x[i];
+}
+
+hipError_t launch_recip(const double* x, int n, double* y, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_recip, dim3((n + 255) / 256), dim3(256), 0, st, x, n, y);
+  return hipGetLastError();
+}
+
 __global__ void k_divide(double* __restrict__ x, int64_t n, double d) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[i] = x[i] / d;

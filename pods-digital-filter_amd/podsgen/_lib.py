@@ -57,9 +57,11 @@ SIGNATURES = {
     "pods_pack_lower": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "pods_unpack_lower": (c_int, [c_void_p, c_void_p, c_int, c_dbl, c_void_p]),
     "pods_temporal_modes": (c_int, [c_void_p, c_void_p, c_i64, c_i64, c_void_p, c_int, c_int, c_void_p]),
+    "pods_temporal_modes_dev": (c_int, [c_void_p, c_void_p, c_i64, c_i64, c_void_p, c_int, c_int, c_void_p]),
     "pods_syev": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "pods_sytrd": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "pods_syev_status": (c_int, [c_void_p]),
+    "pods_syev_flags_async": (c_int, [c_void_p, c_void_p]),
     "pods_cheb_prepare": (c_int, [c_void_p, c_void_p, c_int]),
     "pods_cheb_step": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_dbl, c_dbl, c_dbl,
                                c_void_p]),
@@ -76,6 +78,7 @@ SIGNATURES = {
     "pods_syev2_inspect": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_i64]),
     "pods_sytrd_trace": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "pods_spatial_modes": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
+    "pods_spatial_modes_dev": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),
     "pods_fourier_twiddles": (c_int, [c_void_p, c_int, c_void_p, c_dbl, c_void_p]),
     "pods_fourier": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_dbl, c_void_p]),
     "pods_fourier_rank": (c_int, [c_void_p, c_void_p, c_int, c_int, c_dbl, c_void_p, c_void_p]),

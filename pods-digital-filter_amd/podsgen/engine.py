@@ -268,6 +268,24 @@ SPLIT_MIN_N = 1024   # below this the fused solve is cheaper than a 64-vector su
 SPLIT_MAX_VEC = 40   # leading pairs a 64-vector block resolves (nm <= 40; beyond, the fused solve)
 
 
+class _forced_eigen:
+    """Context manager: PODS_EIGEN forced to `method` inside (the speculative path's fallback)."""
+
+    def __init__(self, method):
+        self.method = method
+
+    def __enter__(self):
+        self.old = os.environ.get("PODS_EIGEN")
+        os.environ["PODS_EIGEN"] = self.method
+
+    def __exit__(self, *exc):
+        if self.old is None:
+            os.environ.pop("PODS_EIGEN", None)
+        else:
+            os.environ["PODS_EIGEN"] = self.old
+        return False
+
+
 def _eigen_method(world=1):
     method = os.environ.get("PODS_EIGEN", "auto")
     if method not in ("auto", "pods", "pods2", "torch", "split"):
@@ -522,6 +540,50 @@ def eigen_solve(ctx: Context, C, ns, nm, tol_CN, full_temporal, tm=None, world=1
     return lam_desc, nvalid, nmt, T, lam_desc[:ncols]
 
 
+def _speculation_applies(ns, nm, full_temporal, world, spectrum):
+    """One device, the fused pods_syev path, truncated temporal modes: the temporal and spatial
+    modes can be enqueued for nm_trunc = nm before the host has read the spectrum."""
+    return (world == 1 and spectrum is None and not full_temporal and 1 <= nm <= SYEV_MAX_VEC and
+            nm + 2 <= ns <= SYEV_MAX_N and _eigen_method() in ("auto", "pods"))
+
+
+def eigen_solve_speculative(ctx: Context, C, ns, nm, tol_CN, tm):
+    """pods_syev, then the temporal modes from the device eigenvalues for nm_trunc = nm -- the
+    truncation PODFS.py:1312-1320 gives whenever lambda_{nm-1} passes the valid-mode test (the
+    spectrum is sorted, so that one test decides it) -- without a host round trip between the
+    eigensolve and the modes.  Returns (T, lam_t, Y, verify); verify() synchronises on the
+    eigensolve and returns (lam_desc, nvalid) -- the caller redoes the modes on the host path
+    when nvalid < nm -- or raises RuntimeError when the persistent solver aborted."""
+    lib, dev = ctx.lib, C.device
+    lam_t = torch.empty(ns, dtype=torch.float64, device=dev)
+    Y = torch.empty((ns, nm), dtype=torch.float64, device=dev)
+    with tm("eigh"):
+        check(lib.pods_syev(ctx.h, ptr(C), ns, nm, ptr(lam_t), ptr(Y)), "pods_syev")
+    # the spectrum and the solver's abort words go to pinned host memory behind the solve; the
+    # host waits for that event only, not for the modes enqueued after it
+    pin = getattr(ctx, "_spec_pin", None)
+    if pin is None or pin[0].numel() != ns:
+        pin = ctx._spec_pin = (torch.empty(ns, dtype=torch.float64, pin_memory=True),
+                               torch.zeros(2, dtype=torch.int32, pin_memory=True))
+    lam_h, flags_h = pin
+    lam_h.copy_(lam_t, non_blocking=True)
+    check(lib.pods_syev_flags_async(ctx.h, ptr(flags_h)), "pods_syev_flags_async")
+    solved = torch.cuda.Event()
+    solved.record()
+    T = torch.empty((ns, nm), dtype=torch.float64, device=dev)
+    v0 = ctypes.c_void_p(Y.data_ptr() + (ns - 1) * 8)   # eigh's ascending columns, see eigen_solve
+    with tm("temporal"):
+        check(lib.pods_temporal_modes_dev(ctx.h, v0, nm, -1, ptr(lam_t), nm, nm, ptr(T)), "pods_temporal_modes_dev")
+
+    def verify():
+        solved.synchronize()
+        if int(flags_h[0]) or int(flags_h[1]):
+            raise RuntimeError("pods_syev: hand-off wait timed out (aborted)")
+        lam_desc = lam_h.numpy().copy()
+        return lam_desc, num_valid_modes(lam_desc, ns, tol_CN)
+    return T, lam_t, Y, verify
+
+
 def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=False,
             keep_C=False, timer=None, on_temporal=None, spectrum=None, before_eigen=None, before_corr=None):
     """PODFS.POD (PODFS.py:1294-1393) with correct_for_cell_volumes='false'.
@@ -562,6 +624,45 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
             allreduce_correlation(dist, C, ns, *device_triangle_ops(ctx))
     if before_eigen is not None:
         before_eigen()
+    if _speculation_applies(ns, nm, full_temporal, world, spectrum):
+        # the modes are enqueued straight behind the eigensolve; the host reads the spectrum while
+        # the device computes them (no idle gap for a round trip), then checks the truncation
+        T, lam_t, Y, verify = eigen_solve_speculative(ctx, C, ns, nm, tol_CN, tm)
+        phi = torch.empty((snap.rowlen, nm), dtype=torch.float64, device=dev)
+        with tm("spatial"):
+            check(lib.pods_spatial_modes_dev(ctx.h, ptr(T), nm, ptr(lam_t), nm, ptr(phi)), "pods_spatial_modes_dev")
+        try:
+            lam_desc, nvalid = verify()
+        except RuntimeError as exc:   # the persistent solver aborted: the whole solve again (fallback)
+            warnings.warn("podsgen: %s; falling back to torch.linalg.eigh" % exc)
+            lam_desc = None
+        if lam_desc is not None and nvalid >= nm:
+            nmt = nm
+        else:   # fewer valid modes than nm (or no spectrum): the host path
+            if lam_desc is not None:
+                nmt = nvalid
+                ncols = max(nmt, 1)
+                T = torch.empty((ns, ncols), dtype=torch.float64, device=dev)
+                v0 = ctypes.c_void_p(Y.data_ptr() + (ns - 1) * 8)
+                with tm("temporal"):
+                    check(lib.pods_temporal_modes(ctx.h, v0, nm, -1, ptr(lam_desc), min(nvalid, ncols), ncols,
+                                                  ptr(T)), "pods_temporal_modes")
+                lam_modes = lam_desc[:ncols]
+            else:
+                with _forced_eigen("torch"):
+                    lam_desc, nvalid, nmt, T, lam_modes = eigen_solve(ctx, C, ns, nm, tol_CN, full_temporal, tm)
+            phi = torch.empty((snap.rowlen, max(nmt, 1)), dtype=torch.float64, device=dev)
+            if nmt > 0:
+                with tm("spatial"):
+                    check(lib.pods_spatial_modes(ctx.h, ptr(T), T.shape[1],
+                                                 ptr(np.ascontiguousarray(lam_modes[:nmt])), nmt, ptr(phi)),
+                          "pods_spatial_modes")
+        t_ready = torch.cuda.Event()
+        t_ready.record()
+        if on_temporal is not None:
+            on_temporal(T, nmt, t_ready)
+        return PODResult(energy=lam_desc, num_valid=nvalid, nm=nmt, mean=mean, T=T, phi=phi[:, :nmt],
+                         C=C if keep_C else None)
     meta = torch.zeros(4, dtype=torch.int64, device=dev)
     T = lam_desc = nvalid = None
     defer = spectrum is not None

@@ -262,6 +262,27 @@ def test_prefetched_generation_matches(ctx):
     assert torch.equal(p1.phi, p2.phi) and np.array_equal(f1.c, f2.c)
 
 
+def test_speculative_modes_fallback(ctx):
+    """One device: the temporal/spatial modes are enqueued behind pods_syev for nm_trunc = nm
+    before the host reads the spectrum.  With fewer valid modes than nm (a rank-6 correlation,
+    nm = 10) they are redone on the host path: the result equals the oracle's POD."""
+    rng = np.random.default_rng(11)
+    A = rng.standard_normal((6, 30)) * np.arange(1, 7)[:, None]
+    snap = E.load_snapshots(A, ctx=ctx)
+    pod = E.run_pod(snap, 10, tol_CN=1e-6)
+    _, Ac = O.mean_and_center(A)
+    ref = O.pod(Ac, 30, 10, tol_CN=1e-6)
+    assert pod.num_valid == ref["num_valid"] and pod.nm == ref["nm"] and pod.nm < 10, (pod.num_valid, ref["num_valid"])
+    lam = ref["energy"].real
+    assert np.max(np.abs(pod.energy - lam)) <= 1e-12 * lam[0]
+    T, Phi = pod.T.cpu().numpy(), pod.phi.cpu().numpy()
+    for j in range(pod.nm):
+        sgn = np.sign(np.dot(T[:, j], ref["T"][:, j].real))
+        assert np.max(np.abs(sgn * T[:, j] - ref["T"][:, j].real)) <= 1e-10 * np.max(np.abs(ref["T"][:, j])), j
+        Pg = ref["spatial"][:, j].real
+        assert np.max(np.abs(sgn * Phi[:, j] - Pg)) <= 1e-10 * np.max(np.abs(Pg)), j
+
+
 def test_row_slabs_match_full(ctx):
     """Multi-GPU sharding on one device: 3 row slabs concatenate to the full generation."""
     s = podsgen.DFSetup(jma=20, kma=17, ns=11, seed=99)
