@@ -97,6 +97,9 @@ int pods_df_generate(pods_ctx* ctx);
 #define PODS_GEN_XPASS 4
 #define PODS_GEN_YZPASS 8
 #define PODS_GEN_ALL 15
+/* with PODS_GEN_PLANES: the planes' workgroups are limited to 6 per CU (padded LDS), so they
+ * can run beside the late tridiagonalisation ranges of a pods_syev (see pods_syev_marker) */
+#define PODS_GEN_BESIDE_SOLVER 16
 int pods_df_generate_parts(pods_ctx* ctx, int parts);
 /* Device pointer and row length (= 3*P_local) of the snapshot matrix.  Device layout is
  * K-tiled: element (snapshot i, row r of the reference A) is at
@@ -185,6 +188,13 @@ int pods_syev_status(pods_ctx* ctx);
  * when it completed) copied to flags_host (2 x uint32, pinned for a truly asynchronous copy),
  * stream-ordered, without synchronising: the caller waits on an event behind it. */
 int pods_syev_flags_async(pods_ctx* ctx, uint32_t* flags_host);
+/* The next pods_syev records a marker event on the stream once tridiagonalisation column
+ * range `after_range` (512 columns each) is done; pods_stream_wait_marker makes `stream` (a
+ * hipStream_t) wait for it, and fails if the last pods_syev recorded none (n <= 512 * (after_range
+ * + 1)).  Used to start the next run's random planes beside the late ranges, whose workgroups
+ * leave registers and LDS free (PODS_GEN_BESIDE_SOLVER). */
+int pods_syev_marker(pods_ctx* ctx, int after_range);
+int pods_stream_wait_marker(pods_ctx* ctx, void* stream);
 
 /* All n eigenvalues of C alone (the full spectrum POD.eigenvalues.dat and the valid-mode count
  * consume, PODFS.py:1309-1320, :1339), as a sequence of stream-ordered units that a caller can

@@ -260,6 +260,11 @@ struct pods_ctx {
   hipEvent_t pin_ev[kStageSlots] = {};
   bool pin_used[kStageSlots] = {};
   int pin_next = 0;
+  // marker recorded behind a tridiagonalisation column range of the next pods_syev
+  // (pods_syev_marker), for work another stream may start once that range is done
+  hipEvent_t marker = nullptr;
+  int marker_after = -1;
+  bool marker_recorded = false;
 };
 
 namespace {
@@ -405,6 +410,7 @@ int pods_destroy(pods_ctx* c) {
       if (c->pin_ev[i]) (void)hipEventDestroy(c->pin_ev[i]);
     (void)hipHostFree(c->pin);
   }
+  if (c->marker) (void)hipEventDestroy(c->marker);
   delete c;
   return PODS_OK;
   PODS_CATCH
@@ -520,7 +526,7 @@ int pods_df_generate_parts(pods_ctx* c, int parts) {
   PODS_TRY
   if (int e = check_ctx(c)) return e;
   if (!c->configured) return fail(PODS_ERR_STATE, "pods_df_generate before pods_df_configure");
-  if (parts & ~PODS_GEN_ALL) return fail(PODS_ERR_ARG, "bad generation parts");
+  if (parts & ~(PODS_GEN_ALL | PODS_GEN_BESIDE_SOLVER)) return fail(PODS_ERR_ARG, "bad generation parts");
   PODS_HIP(hipSetDevice(c->device));
   const pods_df_params& p = c->p;
   const RngLayout& L = c->layout;
@@ -530,7 +536,7 @@ int pods_df_generate_parts(pods_ctx* c, int parts) {
   if (parts & PODS_GEN_PLANES) {
     PODS_HIP(pods::launch_mt_generate(c->rng.states.as<uint32_t>(), L.G, L.Bs, L.ntot, c->S, c->Kp, p.j0,
                                       p.j1 + 2 * p.nfy, c->Sl, p.rng_low, p.rng_range, c->R.as<double>(),
-                                      c->stream));
+                                      c->stream, (parts & PODS_GEN_BESIDE_SOLVER) ? 6 : 0));
   }
   const double* taps = c->taps.as<double>();
   if (parts & PODS_GEN_XPASS) {
@@ -913,7 +919,17 @@ int run_sytrd(pods_ctx* c, const double* C, int n, int* R_out, int64_t* trace = 
   a.trace = trace;
   a.trace_wg = trace_wg;
   a.nrep = 8;  // one hand-off copy per XCD (-0.8 ms at n = 4096 against a single copy)
-  PODS_HIP(pods::launch_trd(a, R, c->stream));
+  const int mk = c->marker_after;
+  c->marker_after = -1;
+  c->marker_recorded = false;
+  if (mk >= 0 && mk < a.klast && c->marker) {
+    PODS_HIP(pods::launch_trd_ranges(a, R, 0, mk, c->stream));
+    PODS_HIP(hipEventRecord(c->marker, c->stream));
+    c->marker_recorded = true;
+    PODS_HIP(pods::launch_trd_ranges(a, R, mk + 1, a.klast, c->stream));
+  } else {
+    PODS_HIP(pods::launch_trd(a, R, c->stream));
+  }
   *R_out = R;
   return PODS_OK;
 }
@@ -1168,6 +1184,24 @@ int pods_sytrd_trace(pods_ctx* c, const double* C, int n, int wg, int64_t* trace
   (void)hipStreamSynchronize(c->stream);
   release(tb);
   return e;
+  PODS_CATCH
+}
+
+int pods_syev_marker(pods_ctx* c, int after_range) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!c->marker) PODS_HIP(hipEventCreateWithFlags(&c->marker, hipEventDisableTiming));
+  c->marker_after = after_range;
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_stream_wait_marker(pods_ctx* c, void* stream) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!c->marker_recorded) return fail(PODS_ERR_STATE, "the last pods_syev recorded no marker");
+  PODS_HIP(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), c->marker, 0));
+  return PODS_OK;
   PODS_CATCH
 }
 

@@ -1189,12 +1189,24 @@ hipError_t launch_mt_jump(const uint32_t* src, const int* src_idx, const uint32_
 
 hipError_t launch_mt_generate(const uint32_t* states, int G, int64_t Bs, int64_t ntot, int64_t S,
                               int Kp, int rlo, int rhi, int64_t Sl, double low, double range,
-                              double* out, hipStream_t st) {
+                              double* out, hipStream_t st, int per_cu) {
   if (G <= 0) return hipSuccess;
   const int gw = G;
+  // per_cu > 0: pad the whole-plane generator's LDS so that at most per_cu of its workgroups
+  // share a CU (beside the late tridiagonalisation ranges, which must always find room)
+  size_t pad = 0;
+  if (per_cu > 0) {
+    const size_t want = (160 * 1024) / (per_cu + 1) + 1024, have = 2 * MTN * sizeof(uint32_t);
+    pad = want > have ? want - have : 0;
+  }
   if (rlo == 0 && (int64_t)rhi * Kp == S && Sl == S && ((uintptr_t)out & 15) == 0 && Bs % 2 == 0) {
     // whole planes: out[D] for stream double D (even block starts keep the 16-B stores aligned)
-    hipLaunchKernelGGL(k_mt_generate_full, dim3(gw), dim3(256), 0, st, states, G, Bs, ntot, low, range, out);
+    if (pad) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mt_generate_full),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)pad);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_mt_generate_full, dim3(gw), dim3(256), pad, st, states, G, Bs, ntot, low, range, out);
     return hipGetLastError();
   }
   if (S >= 312) {

@@ -14,6 +14,7 @@ PODS_LUND_1D = 0
 PODS_LUND_PRF = 1
 PODS_LUND_NONE = -1
 PODS_GEN_JUMP, PODS_GEN_PLANES, PODS_GEN_XPASS, PODS_GEN_YZPASS, PODS_GEN_ALL = 1, 2, 4, 8, 15  # podsgen.h
+PODS_GEN_BESIDE_SOLVER = 16
 
 c_int = ctypes.c_int
 c_i64 = ctypes.c_int64
@@ -62,6 +63,8 @@ SIGNATURES = {
     "pods_sytrd": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "pods_syev_status": (c_int, [c_void_p]),
     "pods_syev_flags_async": (c_int, [c_void_p, c_void_p]),
+    "pods_syev_marker": (c_int, [c_void_p, c_int]),
+    "pods_stream_wait_marker": (c_int, [c_void_p, c_void_p]),
     "pods_cheb_prepare": (c_int, [c_void_p, c_void_p, c_int]),
     "pods_cheb_step": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_dbl, c_dbl, c_dbl,
                                c_void_p]),

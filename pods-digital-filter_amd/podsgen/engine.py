@@ -157,31 +157,34 @@ class Generator:
                                              ptr(k[3]), ptr(k[4])), "pods_df_configure")
         self.rowlen = 3 * (self.j1 - self.j0) * setup.kma
 
-    _ahead = None   # event behind the next run's jump-ahead (prefetch_jump)
+    _ahead = None      # event behind the next run's prefetched parts (prefetch_*)
+    _ahead_parts = 0   # which parts: PODS_GEN_JUMP, + PODS_GEN_PLANES
 
     def generate(self):
-        """The whole generation on the current stream -- or, after prefetch_jump(), the planes,
-        x and y/z passes behind the event of the jump-ahead already enqueued on the gen stream."""
+        """The whole generation on the current stream -- or, after prefetch_jump() (and
+        prefetch_planes_beside_solver()), the parts not yet done, behind the event of those
+        already enqueued on the gen stream."""
         if self._ahead is not None:
             torch.cuda.current_stream(self.ctx.device).wait_event(self._ahead)
-            self._ahead = None
-            check(self.ctx.lib.pods_df_generate_parts(
-                self.ctx.h, _lib.PODS_GEN_PLANES | _lib.PODS_GEN_XPASS | _lib.PODS_GEN_YZPASS),
-                "pods_df_generate_parts")
+            rest = _lib.PODS_GEN_ALL & ~self._ahead_parts
+            self._ahead, self._ahead_parts = None, 0
+            check(self.ctx.lib.pods_df_generate_parts(self.ctx.h, rest), "pods_df_generate_parts")
         else:
             check(self.ctx.lib.pods_df_generate(self.ctx.h), "pods_df_generate")
         return self.snapshots()
 
-    def _on_gen_stream(self, parts, timer, name):
+    def _on_gen_stream(self, parts, timer, name, wait_main=True):
         tm = timer or (lambda name: _NullCtx())
         gs = self.ctx.gen_stream()
-        gs.wait_stream(torch.cuda.current_stream(self.ctx.device))
+        if wait_main:
+            gs.wait_stream(torch.cuda.current_stream(self.ctx.device))
         with self.ctx.on_stream(gs):
             with tm(name):
                 check(self.ctx.lib.pods_df_generate_parts(self.ctx.h, parts), "pods_df_generate_parts")
             ev = torch.cuda.Event()
             ev.record(gs)
         self._ahead = ev
+        self._ahead_parts |= parts & _lib.PODS_GEN_ALL
 
     def prefetch_jump(self, timer=None):
         """Enqueue the NEXT run's MT19937 jump-ahead on the gen stream, after everything the main
@@ -194,6 +197,22 @@ class Generator:
         instead of 2.4 and cost the SYRK 2.7 ms, no net gain; spread over 64-256 workgroups they
         took 46-77 ms, each substream being a latency-bound twist chain.)"""
         self._on_gen_stream(_lib.PODS_GEN_JUMP, timer, "gen_jump_ahead")
+
+    def prefetch_planes_beside_solver(self, timer=None):
+        """Enqueue the NEXT run's random planes on the gen stream behind the marker the current
+        pods_syev records after tridiagonalisation range 3 (pods_syev_marker): from range 4 on
+        the k_trd workgroups hold at most 168 VGPRs per wave and ~2 KB of LDS, so the MT
+        generator (16 VGPRs; LDS padded so at most 6 workgroups share a CU, PODS_GEN_BESIDE_SOLVER)
+        runs beside them and every later range still finds room on every CU.  Called right after
+        pods_syev is enqueued (after prefetch_jump); does nothing when no marker was recorded
+        (ns <= 2048)."""
+        if self._ahead_parts != _lib.PODS_GEN_JUMP:
+            return
+        gs = self.ctx.gen_stream()
+        if self.ctx.lib.pods_stream_wait_marker(self.ctx.h, ctypes.c_void_p(gs.cuda_stream)) != _lib.PODS_OK:
+            return
+        self._on_gen_stream(_lib.PODS_GEN_PLANES | _lib.PODS_GEN_BESIDE_SOLVER, timer, "gen_planes_ahead",
+                            wait_main=False)
 
     def join_ahead(self):
         """Make the current stream wait for the prefetched jump-ahead (if any): called before the
@@ -361,7 +380,7 @@ class SpectrumQueue:
         self.credit = 0.0
         self.max_slots = max_slots
         self.pending = []      # [step, slot, next unit, lam tensor]
-        self.finished = {}     # step -> (lam tensor, status check)
+        self.finished = {}     # step -> (lam tensor, status check, C until checked)
         self.step_no = 0
 
     def owner(self, step):
@@ -395,13 +414,14 @@ class SpectrumQueue:
             self.credit += self.budget
             if self.owner(s) == self.rank:
                 if self.ns > SYEV_MAX_N:
-                    self.finished[s] = eigvals_full(self.ctx, C, self.ns)
+                    lam_t, st = eigvals_full(self.ctx, C, self.ns)
+                    self.finished[s] = (lam_t, st, C)
                     self.credit = 0.0
                 else:
                     slot = self._slot()
                     check(lib.pods_eigvals_begin(self.ctx.h, slot, ptr(C), self.ns), "pods_eigvals_begin")
                     lam = torch.empty(self.ns, dtype=torch.float64, device=C.device)
-                    self.pending.append([s, slot, 1, lam])
+                    self.pending.append([s, slot, 1, lam, C])
                     self.credit -= self.cost[0]
             self._advance(limit=limit)
 
@@ -425,7 +445,7 @@ class SpectrumQueue:
                 check(lib.pods_eigvals_fetch(self.ctx.h, p[1], ptr(p[3])), "pods_eigvals_fetch")
                 slot = p[1]
                 self.finished[p[0]] = (p[3], lambda slot=slot: check(lib.pods_eigvals_status(self.ctx.h, slot),
-                                                                     "pods_eigvals"))
+                                                                     "pods_eigvals"), p[4])
                 self.pending.pop(0)
         if not self.pending:
             self.credit = min(self.credit, self.budget)  # no banking of idle time
@@ -435,11 +455,19 @@ class SpectrumQueue:
         self.credit = 0.0
 
     def results(self):
-        """{step: eigenvalues (numpy, descending)} of the finished steps this rank owned."""
+        """{step: eigenvalues (numpy, descending)} of the finished steps this rank owned.  A
+        spectrum whose persistent kernels aborted their hand-off wait (their workgroups could
+        not all be resident: another process on the device) is recomputed with
+        torch.linalg.eigvalsh from the step's C, which the queue keeps until then."""
         out = {}
-        for s, (lam, status) in sorted(self.finished.items()):
-            status()
-            out[s] = lam.cpu().numpy()
+        for s, (lam, status, C) in sorted(self.finished.items()):
+            try:
+                status()
+                out[s] = lam.cpu().numpy()
+            except RuntimeError as exc:
+                warnings.warn("podsgen: %s; spectrum of step %d by torch.linalg.eigvalsh" % (exc, s))
+                out[s] = torch.flip(torch.linalg.eigvalsh(C), dims=(0,)).cpu().numpy()
+            self.finished[s] = (torch.from_numpy(out[s]), lambda: None, None)   # C no longer held
         return out
 
 
@@ -547,7 +575,7 @@ def _speculation_applies(ns, nm, full_temporal, world, spectrum):
             nm + 2 <= ns <= SYEV_MAX_N and _eigen_method() in ("auto", "pods"))
 
 
-def eigen_solve_speculative(ctx: Context, C, ns, nm, tol_CN, tm):
+def eigen_solve_speculative(ctx: Context, C, ns, nm, tol_CN, tm, beside=None):
     """pods_syev, then the temporal modes from the device eigenvalues for nm_trunc = nm -- the
     truncation PODFS.py:1312-1320 gives whenever lambda_{nm-1} passes the valid-mode test (the
     spectrum is sorted, so that one test decides it) -- without a host round trip between the
@@ -557,8 +585,12 @@ def eigen_solve_speculative(ctx: Context, C, ns, nm, tol_CN, tm):
     lib, dev = ctx.lib, C.device
     lam_t = torch.empty(ns, dtype=torch.float64, device=dev)
     Y = torch.empty((ns, nm), dtype=torch.float64, device=dev)
+    if beside is not None:   # a marker behind tridiagonalisation range 3 for beside()
+        check(lib.pods_syev_marker(ctx.h, 3), "pods_syev_marker")
     with tm("eigh"):
         check(lib.pods_syev(ctx.h, ptr(C), ns, nm, ptr(lam_t), ptr(Y)), "pods_syev")
+    if beside is not None:
+        beside()
     # the spectrum and the solver's abort words go to pinned host memory behind the solve; the
     # host waits for that event only, not for the modes enqueued after it
     pin = getattr(ctx, "_spec_pin", None)
@@ -585,7 +617,7 @@ def eigen_solve_speculative(ctx: Context, C, ns, nm, tol_CN, tm):
 
 
 def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=False,
-            keep_C=False, timer=None, on_temporal=None, spectrum=None, before_eigen=None, before_corr=None):
+            keep_C=False, timer=None, on_temporal=None, spectrum=None, before_eigen=None, beside_solve=None):
     """PODFS.POD (PODFS.py:1294-1393) with correct_for_cell_volumes='false'.
 
     spectrum: a SpectrumQueue -- the eigenvalues past the nm leading ones are then computed by
@@ -598,8 +630,9 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
     before the broadcasts.  pipeline() starts the Fourier stage there on a side stream that
     waits for `ready` only, so it runs beside the spatial-mode pass.
 
-    before_corr(), if given, is called after the centring is enqueued, before the correlation
-    (pipeline() starts the next run's random planes there, beside the SYRK).
+    beside_solve(), if given, is called right after one device's pods_syev is enqueued
+    (pipeline() starts the next run's random planes there, beside the late tridiagonalisation
+    ranges).
 
     before_eigen(), if given, is called once the correlation is enqueued, before the first
     host synchronisation of the eigensolve (pipeline() finishes the previous step's Fourier
@@ -615,8 +648,6 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
     with tm("center"):  # main() :1493-1495, in place
         check(lib.pods_center(ctx.h), "pods_center")
     C = torch.empty((ns, ns), dtype=torch.float64, device=dev)
-    if before_corr is not None:
-        before_corr()
     with tm("corr"):
         check(lib.pods_corr(ctx.h, ptr(C), 1 if world == 1 else 0), "pods_corr")
     if world > 1:
@@ -627,7 +658,7 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
     if _speculation_applies(ns, nm, full_temporal, world, spectrum):
         # the modes are enqueued straight behind the eigensolve; the host reads the spectrum while
         # the device computes them (no idle gap for a round trip), then checks the truncation
-        T, lam_t, Y, verify = eigen_solve_speculative(ctx, C, ns, nm, tol_CN, tm)
+        T, lam_t, Y, verify = eigen_solve_speculative(ctx, C, ns, nm, tol_CN, tm, beside=beside_solve)
         phi = torch.empty((snap.rowlen, nm), dtype=torch.float64, device=dev)
         with tm("spatial"):
             check(lib.pods_spatial_modes_dev(ctx.h, ptr(T), nm, ptr(lam_t), nm, ptr(phi)), "pods_spatial_modes_dev")
@@ -924,8 +955,9 @@ def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=Non
         gen.join_ahead()
         if backlog is not None:
             backlog.finish_pending()
+    beside = (lambda: gen.prefetch_planes_beside_solver(timer)) if prefetch_next else None
     pod = run_pod(snap, setup.nm, dist=dist_, full_temporal=full_temporal, timer=timer,
-                  on_temporal=start_fourier, spectrum=spectrum, before_eigen=before_eigen)
+                  on_temporal=start_fourier, spectrum=spectrum, before_eigen=before_eigen, beside_solve=beside)
     if backlog is not None:
         backlog.pending.append(pending[0] if pending else None)
         return gen, pod, None

@@ -19,7 +19,8 @@ torch = pytest.importorskip("torch")
 
 from oracle import pods_oracle as O  # noqa: E402
 import podsgen  # noqa: E402
-from podsgen import engine as E  # noqa: E402
+from podsgen import engine as E
+from podsgen import _lib  # noqa: E402
 
 CASES = ["c1_32x32x64", "cli_10x11x5", "odd_12x9x17_aniso", "prf_8x12x9", "rot_6x7x6",
          "dtanh_9x12x7", "circ_11x10x6", "ring_12x13x6", "readprf_case", "prof1d_14x16x8"]
@@ -260,6 +261,30 @@ def test_prefetched_generation_matches(ctx):
     _, p2, f2 = E.pipeline(s2, gen=g2)
     assert np.array_equal(p1.energy, p2.energy) and p1.nm == p2.nm
     assert torch.equal(p1.phi, p2.phi) and np.array_equal(f1.c, f2.c)
+
+
+def test_planes_prefetched_beside_solver(ctx):
+    """ns > 2048: the next run's random planes start on the gen stream behind the marker of
+    tridiagonalisation range 3 (Generator.prefetch_planes_beside_solver) while the solver's
+    late ranges run.  The next step's snapshot matrix and POD equal a plain run's bit for bit,
+    and no persistent kernel aborted (no fallback warning)."""
+    import warnings
+    s = podsgen.DFSetup(jma=24, kma=20, ns=2560, seed=31)
+    g1 = E.Generator(s, ctx=ctx)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        E.pipeline(s, gen=g1, prefetch_next=True)
+        assert g1._ahead_parts == _lib.PODS_GEN_JUMP | _lib.PODS_GEN_PLANES
+        _, p2, f2 = E.pipeline(s, gen=g1)
+        A2 = g1.snapshots().to_host()
+    assert not [x for x in w if "podsgen" in str(x.message)], [str(x.message) for x in w]
+    c2 = E.Context(0)
+    g2 = E.Generator(s, ctx=c2)
+    _, p3, f3 = E.pipeline(s, gen=g2)
+    assert np.array_equal(A2, g2.snapshots().to_host())
+    assert np.array_equal(p2.energy, p3.energy) and p2.nm == p3.nm
+    assert torch.equal(p2.phi, p3.phi) and np.array_equal(f2.c, f3.c)
+    c2.close()
 
 
 def test_speculative_modes_fallback(ctx):
