@@ -625,7 +625,8 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
     the whole spectrum is computed in this call.
 
     on_temporal(T, nm_trunc, ready), if given, is called on rank 0 with `ready` an event recorded
-    behind the temporal modes: on one rank right after the spatial modes are enqueued (so the
+    behind the temporal modes (again, superseding the first call, when one device's truncation
+    check redoes the modes): on one rank right after the spatial modes are enqueued (so the
     spatial pass does not wait for the host to launch the Fourier stage), on several ranks
     before the broadcasts.  pipeline() starts the Fourier stage there on a side stream that
     waits for `ready` only, so it runs beside the spatial-mode pass.
@@ -662,6 +663,10 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
         phi = torch.empty((snap.rowlen, nm), dtype=torch.float64, device=dev)
         with tm("spatial"):
             check(lib.pods_spatial_modes_dev(ctx.h, ptr(T), nm, ptr(lam_t), nm, ptr(phi)), "pods_spatial_modes_dev")
+        t_ready = torch.cuda.Event()
+        t_ready.record()
+        if on_temporal is not None:   # the Fourier stage beside the spatial pass (redone on a miss)
+            on_temporal(T, nm, t_ready)
         try:
             lam_desc, nvalid = verify()
         except RuntimeError as exc:   # the persistent solver aborted: the whole solve again (fallback)
@@ -688,10 +693,10 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
                     check(lib.pods_spatial_modes(ctx.h, ptr(T), T.shape[1],
                                                  ptr(np.ascontiguousarray(lam_modes[:nmt])), nmt, ptr(phi)),
                           "pods_spatial_modes")
-        t_ready = torch.cuda.Event()
-        t_ready.record()
-        if on_temporal is not None:
-            on_temporal(T, nmt, t_ready)
+            t_ready = torch.cuda.Event()
+            t_ready.record()
+            if on_temporal is not None:   # supersedes the speculative launch
+                on_temporal(T, nmt, t_ready)
         return PODResult(energy=lam_desc, num_valid=nvalid, nm=nmt, mean=mean, T=T, phi=phi[:, :nmt],
                          C=C if keep_C else None)
     meta = torch.zeros(4, dtype=torch.int64, device=dev)
@@ -958,10 +963,12 @@ def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=Non
     beside = (lambda: gen.prefetch_planes_beside_solver(timer)) if prefetch_next else None
     pod = run_pod(snap, setup.nm, dist=dist_, full_temporal=full_temporal, timer=timer,
                   on_temporal=start_fourier, spectrum=spectrum, before_eigen=before_eigen, beside_solve=beside)
+    # the last launch counts (a speculative Fourier launch is superseded when the truncation
+    # check redoes the modes)
     if backlog is not None:
-        backlog.pending.append(pending[0] if pending else None)
+        backlog.pending.append(pending[-1] if pending else None)
         return gen, pod, None
-    fo = pending[0]() if pending else None
+    fo = pending[-1]() if pending else None
     return gen, pod, fo
 
 
