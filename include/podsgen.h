@@ -97,7 +97,7 @@ int pods_df_generate(pods_ctx* ctx);
 #define PODS_GEN_XPASS 4
 #define PODS_GEN_YZPASS 8
 #define PODS_GEN_ALL 15
-/* with PODS_GEN_PLANES: the planes' workgroups are limited to 6 per CU (padded LDS), so they
+/* with PODS_GEN_PLANES: the planes' workgroups are limited to 2 per CU (padded LDS), so they
  * can run beside the late tridiagonalisation ranges of a pods_syev (see pods_syev_marker) */
 #define PODS_GEN_BESIDE_SOLVER 16
 int pods_df_generate_parts(pods_ctx* ctx, int parts);

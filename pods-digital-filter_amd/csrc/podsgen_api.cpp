@@ -536,7 +536,7 @@ int pods_df_generate_parts(pods_ctx* c, int parts) {
   if (parts & PODS_GEN_PLANES) {
     PODS_HIP(pods::launch_mt_generate(c->rng.states.as<uint32_t>(), L.G, L.Bs, L.ntot, c->S, c->Kp, p.j0,
                                       p.j1 + 2 * p.nfy, c->Sl, p.rng_low, p.rng_range, c->R.as<double>(),
-                                      c->stream, (parts & PODS_GEN_BESIDE_SOLVER) ? 6 : 0));
+                                      c->stream, (parts & PODS_GEN_BESIDE_SOLVER) ? 2 : 0));
   }
   const double* taps = c->taps.as<double>();
   if (parts & PODS_GEN_XPASS) {

@@ -200,12 +200,14 @@ class Generator:
 
     def prefetch_planes_beside_solver(self, timer=None):
         """Enqueue the NEXT run's random planes on the gen stream behind the marker the current
-        pods_syev records after tridiagonalisation range 3 (pods_syev_marker): from range 4 on
-        the k_trd workgroups hold at most 168 VGPRs per wave and ~2 KB of LDS, so the MT
-        generator (16 VGPRs; LDS padded so at most 6 workgroups share a CU, PODS_GEN_BESIDE_SOLVER)
-        runs beside them and every later range still finds room on every CU.  Called right after
-        pods_syev is enqueued (after prefetch_jump); does nothing when no marker was recorded
-        (ns <= 2048)."""
+        pods_syev records after tridiagonalisation range 2 (pods_syev_marker): from range 3 on
+        the k_trd workgroups hold at most 192 VGPRs per wave (2 waves per SIMD) and <= 42 KB of
+        LDS, so the MT generator (16 VGPRs; LDS padded to 55 KB so at most 2 of its workgroups
+        share a CU, PODS_GEN_BESIDE_SOLVER) runs beside them and every later range still finds
+        room on every CU whatever the dispatch order.  Measured against a marker after range 3
+        / 4 with up to 3 or 6 generator workgroups per CU: the solver grows least this way
+        (36.5 -> 36.9 ms against 37.1-37.2).  Called right after pods_syev is enqueued (after
+        prefetch_jump); does nothing when no marker was recorded (ns <= 1536)."""
         if self._ahead_parts != _lib.PODS_GEN_JUMP:
             return
         gs = self.ctx.gen_stream()
@@ -587,8 +589,8 @@ def eigen_solve_speculative(ctx: Context, C, ns, nm, tol_CN, tm, beside=None):
     lib, dev = ctx.lib, C.device
     lam_t = torch.empty(ns, dtype=torch.float64, device=dev)
     Y = torch.empty((ns, nm), dtype=torch.float64, device=dev)
-    if beside is not None:   # a marker behind tridiagonalisation range 3 for beside()
-        check(lib.pods_syev_marker(ctx.h, 3), "pods_syev_marker")
+    if beside is not None:   # a marker behind tridiagonalisation range 2 for beside()
+        check(lib.pods_syev_marker(ctx.h, 2), "pods_syev_marker")
     with tm("eigh"):
         check(lib.pods_syev(ctx.h, ptr(C), ns, nm, ptr(lam_t), ptr(Y)), "pods_syev")
     if beside is not None:
