@@ -79,9 +79,10 @@ class Context:
         class _S:
             def __enter__(self):
                 self.main = torch.cuda.current_stream(ctx.device)
+                # bind the pods context first: if that fails, nothing has been entered yet
+                check(ctx.lib.pods_set_stream(ctx.h, ctypes.c_void_p(stream.cuda_stream)), "pods_set_stream")
                 self.tc = torch.cuda.stream(stream)
                 self.tc.__enter__()
-                check(ctx.lib.pods_set_stream(ctx.h, ctypes.c_void_p(stream.cuda_stream)), "pods_set_stream")
                 return self
 
             def __exit__(self, *exc):
