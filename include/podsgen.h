@@ -68,6 +68,13 @@ int pods_destroy(pods_ctx* ctx);
 /* Enqueue all work on this hipStream_t (NULL = legacy default stream). */
 int pods_set_stream(pods_ctx* ctx, void* hip_stream);
 int pods_synchronize(pods_ctx* ctx);
+/* shared != 0: other processes run persistent grids on this context's device (more ranks than
+ * devices, e.g. a gloo run of several ranks on one GPU).  Every entry point that launches a
+ * persistent grid (pods_syev, pods_sytrd*, pods_eigvals_begin/advance, pods_syev2) then holds an
+ * exclusive per-device lock file (/tmp/podsgen-gpu-<PCI bus id>.lock) from before its launches
+ * until its stream has drained, so two processes' grids never wait on each other's workgroups.
+ * Those calls become synchronous in this mode.  Replaces nothing in the reference. */
+int pods_set_shared_device(pods_ctx* ctx, int shared);
 
 /* ---- generation: digitalfilters.py main() step loop :1403-1477 --------------------
  * bx/by/bz: filter taps (calccoeff, :73-89), lengths 2nf+1, host.
@@ -205,11 +212,23 @@ int pods_stream_wait_marker(pods_ctx* ctx, void* stream);
  *                         be reused by work enqueued after this call) and runs unit 0
  *   pods_eigvals_advance  runs up to max_units more units; *remaining = units still to run
  *   pods_eigvals_fetch    when none remain: copies the n eigenvalues, descending, to lam_desc_dev
- *   pods_eigvals_status   synchronises; PODS_ERR_INTERNAL if a hand-off wait timed out */
+ *   pods_eigvals_status   synchronises; PODS_ERR_INTERNAL if a hand-off wait timed out
+ *   pods_eigvals_flags_async  the slot's abort word (0: completed) copied to flags_dst (1 x
+ *                         uint32; pinned host or device), stream-ordered behind the slot's
+ *                         units, without synchronising -- captured when the spectrum finishes,
+ *                         so a later matrix that reuses the slot cannot overwrite it */
 int pods_eigvals_begin(pods_ctx* ctx, int slot, const double* C_dev, int n);
 int pods_eigvals_advance(pods_ctx* ctx, int slot, int max_units, int* remaining);
 int pods_eigvals_fetch(pods_ctx* ctx, int slot, double* lam_desc_dev);
 int pods_eigvals_status(pods_ctx* ctx, int slot);
+int pods_eigvals_flags_async(pods_ctx* ctx, int slot, uint32_t* flags_dst);
+/* Test entry: sets the slot's abort word (stream-ordered), as a timed-out hand-off wait would,
+ * so a caller's abort handling can be exercised without starving the device. */
+int pods_eigvals_inject_abort(pods_ctx* ctx, int slot);
+/* The two abort words of the last pods_syev2 (panel hand-offs, bulge chasing; both 0 when it
+ * completed) copied to flags_dst (2 x uint32), stream-ordered, without synchronising
+ * (PODFS.py:1309 on the ns > 4096 path; the counterpart of pods_syev_flags_async). */
+int pods_syev2_flags_async(pods_ctx* ctx, uint32_t* flags_dst);
 
 /* Prepares C_dev (n x n row-major) for pods_cheb_step: a 64 x 64-tiled copy in the context
  * (each tile contiguous, so the step streams C at the MFMA rate).  Call again whenever C_dev

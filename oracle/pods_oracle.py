@@ -648,11 +648,17 @@ def _step_column(cfg, xs, taps, loops, cache):
     return col
 
 
-def generate_steps(cfg, steps, chunk=1 << 24):
+JUMP_MIN = 1 << 26   # doubles: ~0.5 s of sequential draws, about one jump's cost
+
+
+def generate_steps(cfg, steps, chunk=1 << 24, jump=False):
     """Columns A[:, i] for the listed steps only, at any size: the planes step i filters
     (planes i..i+2nfx of each component, stream_plane_offset) are cut out of ONE sequential
     pass over the reference's draw stream (drawn in chunks and discarded), so late steps of a
     4096-step run cost one pass over ~0.9 G doubles instead of the whole step loop.
+    jump=True skips gaps longer than JUMP_MIN doubles with the MT19937 jump-ahead of
+    oracle.mt_jump (pinned against sequential numpy draws) instead of drawing them: a step
+    53 G doubles into BASELINE config 5's stream then costs seconds, not minutes.
     Returns {step: column (3P,)}, each equal to generate(cfg)[:, step]."""
     NX = 2 * cfg.nfx + 1
     S = cfg.S
@@ -672,7 +678,11 @@ def generate_steps(cfg, steps, chunk=1 << 24):
         need_end = starts[k] + S
         if buf0 + len(buf) < need_end:  # extend the window: keep the tail from starts[k]
             keep = buf[max(starts[k] - buf0, 0):] if starts[k] < buf0 + len(buf) else np.empty(0)
-            if starts[k] >= buf0 + len(buf):  # skip ahead (draw and discard)
+            if starts[k] >= buf0 + len(buf):  # skip ahead (draw and discard, or jump)
+                if jump and starts[k] - pos > JUMP_MIN:
+                    from .mt_jump import stream_at
+                    rs = stream_at(cfg.seed, starts[k])
+                    pos = starts[k]
                 while pos < starts[k]:
                     n = min(chunk, starts[k] - pos)
                     rs.uniform(low=-SQRT3, high=SQRT3, size=n)

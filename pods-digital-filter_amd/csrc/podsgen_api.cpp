@@ -9,6 +9,10 @@
 #include <string>
 #include <vector>
 
+#include <fcntl.h>
+#include <sys/file.h>
+#include <unistd.h>
+
 #include "mt_host.h"
 #include "podsgen.h"
 #include "podsgen_kernels.h"
@@ -265,9 +269,44 @@ struct pods_ctx {
   hipEvent_t marker = nullptr;
   int marker_after = -1;
   bool marker_recorded = false;
+  // pods_set_shared_device: the per-device lock file persistent launches hold (-1: not shared)
+  int lock_fd = -1;
 };
 
 namespace {
+
+// Persistent grids (k_trd, k_bt_fused, k_pqr, k_sbtrd_win) spin on hand-offs between their own
+// workgroups, so all of them must be resident at once.  Two processes on one device can each
+// hold part of the CUs and starve the other's grid until its spin limit aborts it (r3's 2-rank
+// run on one GPU).  With pods_set_shared_device every entry point that launches one takes this
+// per-device file lock first and keeps it until its stream has drained.
+class PersistentLock {
+ public:
+  explicit PersistentLock(pods_ctx* c) : c_(c) {
+    if (c_->lock_fd >= 0) held_ = flock(c_->lock_fd, LOCK_EX) == 0;
+  }
+  // drain the stream, then unlock (the success path of the entry point)
+  int release() {
+    if (!held_) return PODS_OK;
+    const hipError_t e = hipStreamSynchronize(c_->stream);
+    (void)flock(c_->lock_fd, LOCK_UN);
+    held_ = false;
+    if (e != hipSuccess) return fail(PODS_ERR_HIP, std::string("persistent grid: ") + hipGetErrorString(e));
+    return PODS_OK;
+  }
+  ~PersistentLock() {
+    if (held_) {
+      (void)hipStreamSynchronize(c_->stream);
+      (void)flock(c_->lock_fd, LOCK_UN);
+    }
+  }
+  PersistentLock(const PersistentLock&) = delete;
+  PersistentLock& operator=(const PersistentLock&) = delete;
+
+ private:
+  pods_ctx* c_;
+  bool held_ = false;
+};
 
 // dst_dev <- bytes of src (host) on the context's stream, without synchronising it: through
 // the pinned ring (slot reused after its copy's event), or a synchronous copy when too large
@@ -411,6 +450,7 @@ int pods_destroy(pods_ctx* c) {
     (void)hipHostFree(c->pin);
   }
   if (c->marker) (void)hipEventDestroy(c->marker);
+  if (c->lock_fd >= 0) (void)close(c->lock_fd);
   delete c;
   return PODS_OK;
   PODS_CATCH
@@ -426,6 +466,26 @@ int pods_synchronize(pods_ctx* c) {
   if (int e = check_ctx(c)) return e;
   PODS_HIP(hipStreamSynchronize(c->stream));
   return PODS_OK;
+}
+
+int pods_set_shared_device(pods_ctx* c, int shared) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (c->lock_fd >= 0) {
+    (void)close(c->lock_fd);
+    c->lock_fd = -1;
+  }
+  if (!shared) return PODS_OK;
+  char bus[64] = {0};
+  PODS_HIP(hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, c->device));
+  std::string path = "/tmp/podsgen-gpu-";
+  for (const char* q = bus; *q; ++q) path += (*q == ':' || *q == '.') ? '-' : *q;
+  path += ".lock";
+  const int fd = open(path.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
+  if (fd < 0) return fail(PODS_ERR_STATE, "pods_set_shared_device: cannot open " + path);
+  c->lock_fd = fd;
+  return PODS_OK;
+  PODS_CATCH
 }
 
 namespace {
@@ -968,6 +1028,7 @@ int pods_eigvals_begin(pods_ctx* c, int slot, const double* C, int n) {
   if (pods::trd_plan(n, &R, &G, &slab) != 0)
     return fail(PODS_ERR_UNSUPPORTED, "pods_eigvals_begin: n = " + std::to_string(n) + " > 4096");
   PODS_HIP(hipSetDevice(c->device));
+  PersistentLock lk(c);
   if ((int)c->eslots.size() <= slot) c->eslots.resize(slot + 1);
   EigvalSlot& sl = c->eslots[slot];
   if (sl.active && sl.next < eigval_units(sl))
@@ -1004,7 +1065,8 @@ int pods_eigvals_begin(pods_ctx* c, int slot, const double* C, int n) {
   sl.klast = a.klast;
   sl.next = 0;
   sl.active = true;
-  return eigval_run(c, sl, 1);  // range 0 is the only one that reads C
+  if (int e = eigval_run(c, sl, 1)) return e;  // range 0 is the only one that reads C
+  return lk.release();
   PODS_CATCH
 }
 
@@ -1015,9 +1077,10 @@ int pods_eigvals_advance(pods_ctx* c, int slot, int max_units, int* remaining) {
     return fail(PODS_ERR_ARG, "pods_eigvals_advance: no such slot");
   PODS_HIP(hipSetDevice(c->device));
   EigvalSlot& sl = c->eslots[slot];
+  PersistentLock lk(c);
   if (int e = eigval_run(c, sl, max_units)) return e;
   if (remaining) *remaining = eigval_units(sl) - sl.next;
-  return PODS_OK;
+  return lk.release();
   PODS_CATCH
 }
 
@@ -1048,12 +1111,47 @@ int pods_eigvals_status(pods_ctx* c, int slot) {
   PODS_CATCH
 }
 
+int pods_eigvals_flags_async(pods_ctx* c, int slot, uint32_t* flags_dst) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (slot < 0 || slot >= (int)c->eslots.size() || !c->eslots[slot].active || !flags_dst)
+    return fail(PODS_ERR_ARG, "pods_eigvals_flags_async: no such slot");
+  PODS_HIP(hipSetDevice(c->device));
+  PODS_HIP(hipMemcpyAsync(flags_dst, c->eslots[slot].flags.p, sizeof(uint32_t), hipMemcpyDefault, c->stream));
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_eigvals_inject_abort(pods_ctx* c, int slot) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (slot < 0 || slot >= (int)c->eslots.size() || !c->eslots[slot].active)
+    return fail(PODS_ERR_ARG, "pods_eigvals_inject_abort: no such slot");
+  PODS_HIP(hipSetDevice(c->device));
+  PODS_HIP(hipMemsetAsync(c->eslots[slot].flags.p, 1, sizeof(uint32_t), c->stream));
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_syev2_flags_async(pods_ctx* c, uint32_t* flags_dst) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!flags_dst) return fail(PODS_ERR_ARG, "flags_dst is null");
+  if (!c->e2_flags.p) return fail(PODS_ERR_STATE, "no pods_syev2 ran");
+  PODS_HIP(hipSetDevice(c->device));
+  PODS_HIP(hipMemcpyAsync(flags_dst, c->e2_flags.as<uint32_t>() + 64, 2 * sizeof(uint32_t), hipMemcpyDefault,
+                          c->stream));
+  return PODS_OK;
+  PODS_CATCH
+}
+
 int pods_syev(pods_ctx* c, const double* C, int n, int nvec, double* lam_desc, double* vec) {
   PODS_TRY
   if (int e = check_ctx(c)) return e;
   if (!C || !lam_desc || n < 1 || nvec < 0 || nvec > std::min(n, 64) || (nvec > 0 && !vec))
     return fail(PODS_ERR_ARG, "pods_syev: bad arguments");
   int R = 0;
+  PersistentLock lk(c);
   if (int e = run_sytrd(c, C, n, &R)) return e;
   double* det = c->e_det.as<double>();
   double* D = det;
@@ -1083,7 +1181,7 @@ int pods_syev(pods_ctx* c, const double* C, int n, int nvec, double* lam_desc, d
                                          c->e_flags.as<uint32_t>() + 1, vec,
                                          c->stream));
   }
-  return PODS_OK;
+  return lk.release();
   PODS_CATCH
 }
 
@@ -1109,9 +1207,10 @@ int pods_syev2(pods_ctx* c, const double* C, int n, int nvec, double* lam_desc, 
   PODS_HIP(ensure(c->e2_ipiv, (size_t)std::max(nvec, 1) * n * sizeof(int)));
   PODS_HIP(ensure(c->e_cnt, pods::tri_grid_bytes()));
   ++c->e2_epoch;
+  PersistentLock lk(c);
   PODS_HIP(pods::launch_syevd2(C, n, nvec, c->e2_ws.as<double>(), plan, c->e2_flags.as<uint32_t>(), c->e2_epoch,
                                c->e2_ipiv.as<int>(), c->e_cnt.as<int>(), lam_desc, vec, c->stream));
-  return PODS_OK;
+  return lk.release();
   PODS_CATCH
 }
 
@@ -1150,6 +1249,7 @@ int pods_sytrd(pods_ctx* c, const double* C, int n, double* d_host, double* e_ho
   if (int e = check_ctx(c)) return e;
   if (!C || !d_host || (n > 1 && !e_host) || n < 1) return fail(PODS_ERR_ARG, "pods_sytrd: bad arguments");
   int R = 0;
+  PersistentLock lk(c);
   if (int e = run_sytrd(c, C, n, &R)) return e;
   const double* det = c->e_det.as<double>();
   PODS_HIP(hipMemcpyAsync(d_host, det, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -1174,6 +1274,7 @@ int pods_sytrd_trace(pods_ctx* c, const double* C, int n, int wg, int64_t* trace
   PODS_HIP(ensure(tb, tbytes));
   PODS_HIP(hipMemsetAsync(tb.p, 0, tbytes, c->stream));
   int R = 0;
+  PersistentLock lk(c);
   int e = run_sytrd(c, C, n, &R, tb.as<int64_t>(), wg);
   if (e == PODS_OK) {
     hipError_t he = hipMemcpyAsync(trace_host, tb.p, tbytes, hipMemcpyDeviceToHost,

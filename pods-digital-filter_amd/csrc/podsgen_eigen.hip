@@ -1027,9 +1027,23 @@ __global__ __launch_bounds__(256) void k_orth(const double* __restrict__ lam_des
     }
     return touched;
   };
+  auto clustered = [&](int k) {
+    for (int jj = 0; jj < k; ++jj)
+      if (fabs(lam_desc[jj] - lam_desc[k]) <= 1e-3 * tnorm) return true;
+    return false;
+  };
   for (int k = 1; k < nvec; ++k) {
-    if (!project_out(k)) continue;
+    if (!clustered(k)) continue;
+    const double s0 = dot(k, k);
+    project_out(k);
     double s = dot(k, k);
+    // "twice is enough" (Kahan-Parlett): a projection that removed more than half of the
+    // squared norm leaves a vector whose orthogonality error grows like 1/sqrt(s / s0); a second
+    // pass restores it to rounding level
+    if (s < 0.5 * s0 && s >= 1e-16) {
+      project_out(k);
+      s = dot(k, k);
+    }
     // A vector that (nearly) lies in the span of the cluster's earlier ones -- identical
     // inverse-iteration results inside a degenerate cluster, e.g. a zero or diagonal block --
     // is replaced by a unit vector orthogonalised against them (dstein's restart, as a

@@ -76,8 +76,12 @@ SIGNATURES = {
     "pods_eigvals_advance": (c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_int)]),
     "pods_eigvals_fetch": (c_int, [c_void_p, c_int, c_void_p]),
     "pods_eigvals_status": (c_int, [c_void_p, c_int]),
+    "pods_eigvals_flags_async": (c_int, [c_void_p, c_int, c_void_p]),
+    "pods_eigvals_inject_abort": (c_int, [c_void_p, c_int]),
+    "pods_set_shared_device": (c_int, [c_void_p, c_int]),
     "pods_syev2": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "pods_syev2_status": (c_int, [c_void_p]),
+    "pods_syev2_flags_async": (c_int, [c_void_p, c_void_p]),
     "pods_syev2_inspect": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_i64]),
     "pods_sytrd_trace": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "pods_spatial_modes": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]),

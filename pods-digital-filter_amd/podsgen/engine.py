@@ -45,6 +45,23 @@ def _require_gpu():
                            "there is no CPU fallback")
 
 
+def shared_device():
+    """More processes than devices on this node (e.g. a gloo run of several ranks on one GPU):
+    their persistent grids must not run at the same time (pods_set_shared_device).
+    PODS_SHARED_DEVICE=0/1 overrides the detection (LOCAL_WORLD_SIZE, else the initialised
+    process group's world size, against the visible device count)."""
+    env = os.environ.get("PODS_SHARED_DEVICE")
+    if env in ("0", "1"):
+        return env == "1"
+    local = os.environ.get("LOCAL_WORLD_SIZE")
+    if local is None:
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()):
+            return False
+        local = dist.get_world_size()
+    return int(local) > max(torch.cuda.device_count(), 1)
+
+
 class Context:
     """One pods_ctx bound to a device and to torch's current stream on it."""
 
@@ -58,6 +75,9 @@ class Context:
         check(self.lib.pods_create(ctypes.byref(h), self.device), "pods_create")
         self.h = h
         check(self.lib.pods_set_stream(self.h, ctypes.c_void_p(self.stream.cuda_stream)), "pods_set_stream")
+        self.shared = shared_device()
+        if self.shared:
+            check(self.lib.pods_set_shared_device(self.h, 1), "pods_set_shared_device")
         self._side = None
 
     def side_stream(self):
@@ -292,27 +312,13 @@ SPLIT_MIN_N = 1024   # below this the fused solve is cheaper than a 64-vector su
 SPLIT_MAX_VEC = 40   # leading pairs a 64-vector block resolves (nm <= 40; beyond, the fused solve)
 
 
-class _forced_eigen:
-    """Context manager: PODS_EIGEN forced to `method` inside (the speculative path's fallback)."""
-
-    def __init__(self, method):
-        self.method = method
-
-    def __enter__(self):
-        self.old = os.environ.get("PODS_EIGEN")
-        os.environ["PODS_EIGEN"] = self.method
-
-    def __exit__(self, *exc):
-        if self.old is None:
-            os.environ.pop("PODS_EIGEN", None)
-        else:
-            os.environ["PODS_EIGEN"] = self.old
-        return False
+EIGEN_METHODS = ("auto", "pods", "pods2", "torch", "split")
 
 
-def _eigen_method(world=1):
-    method = os.environ.get("PODS_EIGEN", "auto")
-    if method not in ("auto", "pods", "pods2", "torch", "split"):
+def _eigen_method(world=1, method=None):
+    """The eigensolver path: `method` when a caller forces one (a fallback), else PODS_EIGEN."""
+    method = method or os.environ.get("PODS_EIGEN", "auto")
+    if method not in EIGEN_METHODS:
         raise ValueError("PODS_EIGEN must be auto, pods, pods2, torch or split")
     return method
 
@@ -338,6 +344,27 @@ def eigvals_full(ctx, C, ns, slot=0):
         return lam, lambda: check(lib.pods_eigvals_status(ctx.h, slot), "pods_eigvals")
     check(lib.pods_syev2(ctx.h, ptr(C), ns, 0, ptr(lam), None), "pods_syev2")
     return lam, lambda: check(lib.pods_syev2_status(ctx.h), "pods_syev2")
+
+
+def eigvals_full_checked(ctx, C, ns):
+    """eigvals_full on the host (numpy, descending), recomputed with torch.linalg.eigvalsh when
+    the persistent kernels aborted their hand-off wait (the fused path's fallback, for the
+    spectrum alone)."""
+    lam_t, status = eigvals_full(ctx, C, ns)
+    try:
+        status()
+    except RuntimeError as exc:
+        warnings.warn("podsgen: %s; full spectrum by torch.linalg.eigvalsh" % exc)
+        lam_t = torch.flip(torch.linalg.eigvalsh(C), dims=(0,))
+    return lam_t.cpu().numpy()
+
+
+def _split_converged(th, info, tol):
+    """The subspace iteration's result is usable: finite Ritz values and a final residual at or
+    below the tolerance it iterated to (a rank-deficient C can collapse the damped interval and
+    yield NaN; max_degree can stop it above tol)."""
+    res = info.get("residual", np.inf)
+    return bool(np.all(np.isfinite(th)) and np.isfinite(res) and res <= tol)
 
 
 class SpectrumQueue:
@@ -384,9 +411,40 @@ class SpectrumQueue:
         self._seq, self._cur = [], [0.0] * world
         self.credit = 0.0
         self.max_slots = max_slots
-        self.pending = []      # [step, slot, next unit, lam tensor]
-        self.finished = {}     # step -> (lam tensor, status check, C until checked)
+        self.pending = []      # [step, slot, next unit, lam tensor, C]
+        # step -> [lam tensor, abort words (pinned, captured on the stream when the spectrum
+        # finished), event behind that copy, C until the words were read as 0]
+        self.finished = {}
         self.step_no = 0
+
+    def _finish(self, step, lam, C, flags_async):
+        """Step `step`'s spectrum is enqueued in full: capture its abort words now (the slot or
+        the two-stage workspace is reused by the next matrix) behind an event."""
+        words = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+        flags_async(words)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.finished[step] = [lam, words, ev, C]
+
+    def _settle(self, step, wait):
+        """Reads step's abort words once its event has passed (waits for it when `wait`): a
+        completed spectrum drops its C; an aborted one (the persistent kernels' workgroups could
+        not all be resident: another process on the device) is recomputed from C with
+        torch.linalg.eigvalsh."""
+        ent = self.finished[step]
+        if ent[3] is None:
+            return
+        if not wait and not ent[2].query():
+            return
+        ent[2].synchronize()
+        if int(ent[1][0]) or int(ent[1][1]):
+            warnings.warn("podsgen: spectrum of step %d aborted its hand-off wait; torch.linalg.eigvalsh" % step)
+            ent[0] = torch.flip(torch.linalg.eigvalsh(ent[3]), dims=(0,))
+        ent[3] = None
+
+    def _reap(self):
+        for s in list(self.finished):
+            self._settle(s, wait=False)
 
     def owner(self, step):
         """The rank that solves step `step`'s spectrum: smooth weighted round robin over the
@@ -416,11 +474,14 @@ class SpectrumQueue:
         self.step_no += 1
         lib = self.ctx.lib
         with tm("eig_full"):
+            self._reap()
             self.credit += self.budget
             if self.owner(s) == self.rank:
                 if self.ns > SYEV_MAX_N:
-                    lam_t, st = eigvals_full(self.ctx, C, self.ns)
-                    self.finished[s] = (lam_t, st, C)
+                    lam_t = torch.empty(self.ns, dtype=torch.float64, device=C.device)
+                    check(lib.pods_syev2(self.ctx.h, ptr(C), self.ns, 0, ptr(lam_t), None), "pods_syev2")
+                    self._finish(s, lam_t, C, lambda w: check(lib.pods_syev2_flags_async(self.ctx.h, ptr(w)),
+                                                              "pods_syev2_flags_async"))
                     self.credit = 0.0
                 else:
                     slot = self._slot()
@@ -434,6 +495,7 @@ class SpectrumQueue:
         """Runs units while this step's credit lasts (after a submit with a limit)."""
         tm = timer or (lambda name: _NullCtx())
         with tm("eig_full"):
+            self._reap()
             self._advance()
 
     def _advance(self, drain=False, limit=None):
@@ -449,8 +511,9 @@ class SpectrumQueue:
             if rem.value == 0:
                 check(lib.pods_eigvals_fetch(self.ctx.h, p[1], ptr(p[3])), "pods_eigvals_fetch")
                 slot = p[1]
-                self.finished[p[0]] = (p[3], lambda slot=slot: check(lib.pods_eigvals_status(self.ctx.h, slot),
-                                                                     "pods_eigvals"), p[4])
+                self._finish(p[0], p[3], p[4],
+                             lambda w, slot=slot: check(lib.pods_eigvals_flags_async(self.ctx.h, slot, ptr(w)),
+                                                        "pods_eigvals_flags_async"))
                 self.pending.pop(0)
         if not self.pending:
             self.credit = min(self.credit, self.budget)  # no banking of idle time
@@ -463,16 +526,12 @@ class SpectrumQueue:
         """{step: eigenvalues (numpy, descending)} of the finished steps this rank owned.  A
         spectrum whose persistent kernels aborted their hand-off wait (their workgroups could
         not all be resident: another process on the device) is recomputed with
-        torch.linalg.eigvalsh from the step's C, which the queue keeps until then."""
+        torch.linalg.eigvalsh from the step's C, which the queue keeps until its abort words
+        (captured when the spectrum finished, _finish) have been read."""
         out = {}
-        for s, (lam, status, C) in sorted(self.finished.items()):
-            try:
-                status()
-                out[s] = lam.cpu().numpy()
-            except RuntimeError as exc:
-                warnings.warn("podsgen: %s; spectrum of step %d by torch.linalg.eigvalsh" % (exc, s))
-                out[s] = torch.flip(torch.linalg.eigvalsh(C), dims=(0,)).cpu().numpy()
-            self.finished[s] = (torch.from_numpy(out[s]), lambda: None, None)   # C no longer held
+        for s in sorted(self.finished):
+            self._settle(s, wait=True)
+            out[s] = self.finished[s][0].cpu().numpy()
         return out
 
 
@@ -482,7 +541,11 @@ def eigen_modes(ctx: Context, C, ns, nm, tol_CN, full_temporal, tm=None, world=1
     return eigen_solve(ctx, C, ns, nm, tol_CN, full_temporal, tm, world)[:4]
 
 
-def eigen_solve(ctx: Context, C, ns, nm, tol_CN, full_temporal, tm=None, world=1, defer_full=False):
+SPLIT_TOL = 3e-14    # leading_eigenpairs' residual target (/ theta_0)
+
+
+def eigen_solve(ctx: Context, C, ns, nm, tol_CN, full_temporal, tm=None, world=1, defer_full=False,
+                method=None):
     """Eigensolve + sort + valid-mode count + temporal scaling (PODFS.py:1309-1325).
 
     Returns (lambda descending (numpy; None when defer_full), num_valid (None when deferred),
@@ -496,11 +559,14 @@ def eigen_solve(ctx: Context, C, ns, nm, tol_CN, full_temporal, tm=None, world=1
              subspace iteration on fp64 MFMA (podsgen.subspace, stage "eigh"), which is all the
              step consumes; the full spectrum is computed apart (stage "eig_full": now, or by a
              SpectrumQueue when defer_full);
-      pods2  (4096 < ns <= 16384 on one device): the two-stage pods_syev2."""
+      pods2  (4096 < ns <= 16384 on one device): the two-stage pods_syev2.
+    method forces a path (the fallbacks pass "torch" or "pods"); None reads PODS_EIGEN.
+    The split path checks its result (finite, residual <= SPLIT_TOL) and otherwise solves again
+    with the fused pods_syev (ns <= 4096) or torch.linalg.eigh."""
     from .subspace import leading_eigenpairs
     tm = tm or (lambda name: _NullCtx())
     lib, dev = ctx.lib, C.device
-    method = _eigen_method(world)
+    method = _eigen_method(world, method)
     nvec = max(min(nm, ns), 1) if nm >= 0 else ns
     fits = not full_temporal and nvec <= SYEV_MAX_VEC
     split = (fits and nvec <= SPLIT_MAX_VEC and ns >= SPLIT_MIN_N and
@@ -513,7 +579,16 @@ def eigen_solve(ctx: Context, C, ns, nm, tol_CN, full_temporal, tm=None, world=1
                          % (method, SYEV_MAX_N if method == "pods" else SYEV2_MAX_N, SYEV_MAX_VEC))
     if split:
         with tm("eigh"):
-            th, X, _info = leading_eigenpairs(ctx, C, nvec, m=64, ws=_subspace_ws(ctx, ns))
+            try:
+                th, X, info = leading_eigenpairs(ctx, C, nvec, m=64, tol=SPLIT_TOL, ws=_subspace_ws(ctx, ns))
+                ok = _split_converged(th, info, SPLIT_TOL)
+                why = "residual %r" % info.get("residual")
+            except (np.linalg.LinAlgError, ValueError, FloatingPointError, ZeroDivisionError) as exc:
+                ok, why = False, str(exc)
+        if not ok:
+            alt = "pods" if (fits and ns <= SYEV_MAX_N) else "torch"
+            warnings.warn("podsgen: subspace iteration did not converge (%s); solving with %s" % (why, alt))
+            return eigen_solve(ctx, C, ns, nm, tol_CN, full_temporal, tm, world, method=alt)
         nv_top = num_valid_modes(th, ns, tol_CN)   # exact when < nvec, else a lower bound
         nmt = nm if (0 <= nm <= nv_top) else nv_top
         ncols = max(min(nmt, nvec), 1)
@@ -525,9 +600,7 @@ def eigen_solve(ctx: Context, C, ns, nm, tol_CN, full_temporal, tm=None, world=1
         if defer_full:
             return None, None, nmt, T, th
         with tm("eig_full"):
-            lam_t, status = eigvals_full(ctx, C, ns)
-            lam_desc = lam_t.cpu().numpy()
-            status()
+            lam_desc = eigvals_full_checked(ctx, C, ns)
         return lam_desc, num_valid_modes(lam_desc, ns, tol_CN), nmt, T, th
     if use_pods or use_pods2:
         lam_t = torch.empty(ns, dtype=torch.float64, device=dev)
@@ -690,8 +763,8 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
                                                   ptr(T)), "pods_temporal_modes")
                 lam_modes = lam_desc[:ncols]
             else:
-                with _forced_eigen("torch"):
-                    lam_desc, nvalid, nmt, T, lam_modes = eigen_solve(ctx, C, ns, nm, tol_CN, full_temporal, tm)
+                lam_desc, nvalid, nmt, T, lam_modes = eigen_solve(ctx, C, ns, nm, tol_CN, full_temporal, tm,
+                                                                  method="torch")
             phi = torch.empty((snap.rowlen, max(nmt, 1)), dtype=torch.float64, device=dev)
             if nmt > 0:
                 with tm("spatial"):

@@ -12,7 +12,9 @@ the oracle and fp64 torch without ever copying the 51.5 GB snapshot matrix whole
   (iii) C exactly symmetric; sampled 256 x 256 tiles within 1e-12 max|C| of torch A_c^T A_c/ns;
   (iv)  all 8192 eigenvalues within 1e-12 lambda_0 of torch.linalg.eigh on the same C, T
         sign-aligned within 1e-10 of eigh's scaled vectors (modes with relative gap > 1e-6);
-  (v)   Phi within 1e-10 (per mode) of torch's A_c T Lambda^-1 / ns, columns of unit norm.
+  (v)   Phi within 1e-10 (per mode) of torch's A_c T Lambda^-1 / ns, columns of unit norm;
+  (vi)  the DFT and ranking at ns = 8192 (PODFS.py:1560-1593): c bit-exact against the oracle's
+        reference expression for all nm modes, c_count / c_ind / FC exactly the oracle's.
 """
 import ctypes
 
@@ -63,7 +65,8 @@ def c4():
     pod = E.run_pod(snap, s.nm, keep_C=True)
     torch.cuda.synchronize()
     cen_rows = sample_rows(gen, rows)
-    yield dict(s=s, gen=gen, pod=pod, rows=rows, cols=cols, raw_rows=raw_rows, cen_rows=cen_rows)
+    fo = E.run_fourier(gen.ctx, pod.T, pod.nm, s.ns, s.dt_eff, s.et)
+    yield dict(s=s, gen=gen, pod=pod, rows=rows, cols=cols, raw_rows=raw_rows, cen_rows=cen_rows, fo=fo)
     gen.ctx.close()
 
 
@@ -143,3 +146,22 @@ def test_c4_spatial_modes(c4):
         assert err <= 1e-10 * float(ref[:, j].abs().max()), j
     norms = torch.linalg.vector_norm(phi, dim=0).cpu().numpy()
     assert np.all(np.abs(norms - 1.0) <= 1e-9), norms
+
+
+@pytest.mark.timeout(900)
+def test_c4_fourier_and_ranking(c4):
+    """PODFS.py:1560-1593 at ns = 8192 on C4's temporal modes: every coefficient bit-equal to the
+    oracle's reference expression (the device multiplies by the host's np.exp twiddles in numpy's
+    pairwise order), so c_count / c_ind / FC are the oracle's for every mode; the GPU ranking
+    kernel equals the host restatement on the same c."""
+    from podsgen import engine as E
+    pod, fo, s = c4["pod"], c4["fo"], c4["s"]
+    T = pod.T.cpu().numpy()
+    ref = O.fourier(T, NS, s.dt_eff, pod.nm, s.et)
+    assert fo.period == ref["period"]
+    assert np.array_equal(fo.c, ref["c"]), int(np.sum(fo.c != ref["c"]))
+    assert np.array_equal(fo.c_count, ref["c_count"]), (fo.c_count, ref["c_count"])
+    assert np.array_equal(fo.c_ind, ref["c_ind"])
+    assert np.array_equal(fo.FC, ref["FC"])
+    c_ind, c_count, FC = E.host_rank_and_count(fo.c, s.et)
+    assert np.array_equal(fo.c_count, c_count) and np.array_equal(fo.c_ind, c_ind)

@@ -10,7 +10,9 @@ order (the RCCL all-reduce's arithmetic) and unpacked / ns into C (pods_unpack_l
 Eigensolve on the summed C with the product's path for ns = 16384 (pods_syev2).
 Pass 2: each slab regenerated and its spatial modes formed (pods_spatial_modes).
 
-Checked: generation of every slab's rows bit-exact against the oracle at steps 0 and 1;
+Checked: generation of every slab's rows bit-exact against the oracle at steps 0, 1, 2047 (past
+the 2^32-word mark of the stream) and 16383 (the last, ~53 G doubles in: oracle.generate_steps
+with the independent MT19937 jump-ahead of oracle.mt_jump);
 sampled partial-C tiles of two slabs within 1e-12 max|C_g| of torch; C exactly symmetric;
 all 16384 eigenvalues within 1e-12 lambda_0 of torch.linalg.eigh on the same C and T
 sign-aligned within 1e-10 (gap rule); Phi of two slabs within 1e-10 of torch
@@ -28,6 +30,8 @@ from oracle import pods_oracle as O  # noqa: E402
 
 J, K, NS, SEED, WORLD = 1024, 1024, 16384, 2024, 8
 CHECK_SLABS = (0, WORLD - 1)
+LATE = (2047, NS - 1)        # stream offsets ~6.7 G and ~52.8 G doubles
+FOURIER_MODES = 4            # the oracle DFT at ns = 16384: ~3 s per mode on the host
 
 
 def snap_block(gen, i0, i1):
@@ -55,12 +59,13 @@ def c5():
     ctx = E.Context(0)
     lib = ctx.lib
     pack, unpack = E.device_triangle_ops(ctx)
-    early, tiles, slabs = {}, {}, []
+    early, late, tiles, slabs = {}, {}, {}, []
     packed_sum = None
     for r in range(WORLD):
         gen = E.Generator(s, ctx=ctx, rank=r, world=WORLD)
         gen.generate()
         early[r] = snap_block(gen, 0, 2).cpu().numpy()
+        late[r] = {i: snap_block(gen, i, i + 1)[0].cpu().numpy() for i in LATE}
         slabs.append((gen.j0, gen.j1))
         podsgen.check(lib.pods_mean(ctx.h, None, 0), "pods_mean")
         podsgen.check(lib.pods_center(ctx.h), "pods_center")
@@ -107,9 +112,10 @@ def c5():
             phis[r] = phi.cpu()
             del acc
         del phi
+    fo = E.run_fourier(ctx, T, nmt, NS, s.dt_eff, s.et)
     torch.cuda.synchronize()
-    yield dict(s=s, ctx=ctx, C=C, lam=lam_desc, nvalid=nvalid, nm=nmt, T=T, early=early, tiles=tiles,
-               slabs=slabs, phis=phis, phi_ref=phi_ref, sq=sq.cpu().numpy())
+    yield dict(s=s, ctx=ctx, C=C, lam=lam_desc, nvalid=nvalid, nm=nmt, T=T, early=early, late=late, tiles=tiles,
+               slabs=slabs, phis=phis, phi_ref=phi_ref, sq=sq.cpu().numpy(), fo=fo)
     ctx.close()
 
 
@@ -127,6 +133,41 @@ def test_c5_generation_every_slab_bit_exact_early_steps(c5):
         for i in (0, 1):
             got = c5["early"][r][i]
             assert np.array_equal(got, ref[i][rows]), (r, i)
+
+
+@pytest.mark.timeout(900)
+def test_c5_generation_every_slab_bit_exact_late_steps(c5):
+    """Steps 2047 and 16383 -- stream offsets past the 2^32-word mark up to the end of C5's
+    52.8 G-double stream (SURVEY Appendix A layout: 3 components interleaved per plane from plane
+    2nfx+1 on), every slab's rows bit-exact.  The oracle reaches them by the MT19937 jump-ahead of
+    oracle.mt_jump (pinned against numpy's sequential draws in test_oracle_golden.py)."""
+    import bench
+    prf = bench.c5_profile(J, K)
+    s = c5["s"]
+    cfg = O.DFConfig(jma=J, kma=K, ns=NS, seed=SEED, dt=s.dt, prf=prf)
+    P = J * K
+    for i in LATE:
+        ref = O.generate_steps(cfg, [i], jump=True)[i]
+        for r, (j0, j1) in enumerate(c5["slabs"]):
+            rows = np.concatenate([np.arange(c * P + j0 * K, c * P + j1 * K) for c in range(3)])
+            assert np.array_equal(c5["late"][r][i], ref[rows]), (r, i)
+        del ref
+
+
+@pytest.mark.timeout(900)
+def test_c5_fourier_and_ranking(c5):
+    """The DFT and ranking at ns = 16384 (PODFS.py:1560-1593) on C5's own temporal modes: c
+    bit-exact against the oracle's reference expression for the first FOURIER_MODES modes, and
+    c_count / c_ind / the FC rows of those modes exactly the oracle's."""
+    s, fo = c5["s"], c5["fo"]
+    k = min(FOURIER_MODES, c5["nm"])
+    T = c5["T"].cpu().numpy()[:, :k]
+    ref = O.fourier(T, NS, s.dt_eff, k, s.et)
+    assert fo.period == ref["period"]
+    assert np.array_equal(fo.c[:, :k], ref["c"]), int(np.sum(fo.c[:, :k] != ref["c"]))
+    assert np.array_equal(fo.c_count[:k], ref["c_count"]), (fo.c_count[:k], ref["c_count"])
+    assert np.array_equal(fo.c_ind[:k], ref["c_ind"])
+    assert np.array_equal(fo.FC[:int(np.sum(fo.c_count[:k]))], ref["FC"])
 
 
 def test_c5_partial_correlation_tiles(c5):

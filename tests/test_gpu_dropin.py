@@ -291,3 +291,28 @@ def test_bench_launches_its_own_ranks():
     assert "allreduce" in out["stages_ms"]
     assert out["metric"].startswith("filtered-snapshot Mpoints/s") and "32x32" in out["metric"]
     assert out["value"] > 0
+
+
+@pytest.mark.timeout(900)
+def test_bench_c3_two_ranks_one_device_no_fallback():
+    """`bench.py --gpus 2 --backend gloo` at C3 (ns = 4096: the split eigensolve, the spectrum
+    units of engine.SpectrumQueue on both ranks) with both ranks on this one GPU.  The ranks'
+    persistent grids take the per-device lock (pods_set_shared_device), so none of them starves
+    the other's: the run completes without any fallback (no 'eigvalsh', no 'falling back', no
+    unconverged subspace iteration) -- r3's run of the same command aborted its hand-off waits."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PYTHONWARNINGS"] = "always::UserWarning"   # inherited by the ranks
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--backend", "gloo", "--config", "c3", "--steps", "2", "--warmup", "1", "--no-cpu"],
+                       capture_output=True, text=True, timeout=840, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    for bad in ("eigvalsh", "falling back", "did not converge", "aborted"):
+        assert bad not in r.stderr, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["n_gpus"] == 2 and out["config"]["ns"] == 4096
+    assert out["results"]["eigensolve"].startswith("split")
+    assert out["results"]["num_valid"] is not None and out["results"]["nm"] == 20

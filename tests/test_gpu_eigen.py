@@ -212,6 +212,30 @@ def test_eigen_split_path_matches_fused(ctx, monkeypatch):
         assert np.max(np.abs(s * Ta[:, j] - Tb[:, j])) <= 1e-10 * np.max(np.abs(Ta[:, j])), j
 
 
+def test_split_path_rank_deficient(ctx, monkeypatch):
+    """The split path on a rank-6 correlation (rank far below the 64-vector block: the damped
+    interval's edge theta_59 is ~0) returns what the fused path returns -- the subspace result is
+    checked (finite, residual <= tol) and otherwise replaced by pods_syev, never passed on as NaN
+    or unconverged pairs; the eigenvalues-only spectrum is the fused solve's bit for bit."""
+    n, nm = 1200, 10
+    rng = np.random.default_rng(3)
+    B = torch.from_numpy(rng.standard_normal((6, n)) * np.arange(1, 7)[:, None]).cuda()
+    C = (B.T @ B / 6.0).contiguous()
+    C = (0.5 * (C + C.T)).contiguous()
+    E.load_snapshots(np.random.default_rng(0).standard_normal((48, n)), ctx=ctx)  # sets ns
+    monkeypatch.setenv("PODS_EIGEN", "pods")
+    la, nva, nma, Ta = E.eigen_modes(ctx, C, n, nm, 1e-6, False)
+    monkeypatch.setenv("PODS_EIGEN", "split")
+    lb, nvb, nmb, Tb = E.eigen_modes(ctx, C, n, nm, 1e-6, False)
+    assert np.array_equal(la, lb)
+    assert (nva, nma) == (nvb, nmb) and nmb == 6, (nva, nma, nvb, nmb)
+    Ta, Tb = Ta.cpu().numpy()[:, :nmb], Tb.cpu().numpy()[:, :nmb]
+    assert np.all(np.isfinite(Tb))
+    for j in range(nmb):
+        s = np.sign(np.dot(Ta[:, j], Tb[:, j]))
+        assert np.max(np.abs(s * Ta[:, j] - Tb[:, j])) <= 1e-10 * np.max(np.abs(Ta[:, j])), j
+
+
 @pytest.mark.parametrize("world", [1, 3, 8])
 def test_spectrum_queue_spreads_and_matches(ctx, world):
     """SpectrumQueue (one owner rank's view of a `world`-rank run): the steps it owns are
@@ -230,6 +254,46 @@ def test_spectrum_queue_spreads_and_matches(ctx, world):
     for s, lam in got.items():
         ref, _ = solve(ctx, mats[s], 0)
         assert np.array_equal(lam, ref), s
+
+
+def test_spectrum_queue_abort_captured_before_slot_reuse(ctx):
+    """Step 0's spectrum aborts (abort word injected into its slot); step 1 reuses the slot and
+    does not.  The abort words are captured when each spectrum finishes, so step 0 is recomputed
+    by torch.linalg.eigvalsh (with a warning naming it) and step 1 stays pods_syev's bit for bit;
+    every step's C is released once its words were read."""
+    n = 1500
+    mats = [pod_like(n, seed=70 + i) for i in range(3)]
+    lib = ctx.lib
+    begun = []
+
+    class _Lib:
+        def __getattr__(self, name):
+            return getattr(lib, name)
+
+        def pods_eigvals_begin(self, h, slot, C, n_):
+            r = lib.pods_eigvals_begin(h, slot, C, n_)
+            begun.append(slot)
+            if len(begun) == 1:
+                podsgen.check(lib.pods_eigvals_inject_abort(h, slot), "pods_eigvals_inject_abort")
+            return r
+
+    class _Ctx:
+        h, device, lib = ctx.h, ctx.device, _Lib()
+
+    q = E.SpectrumQueue(_Ctx(), n, rank=0, world=1)
+    with pytest.warns(UserWarning, match="step 0"):
+        for C in mats:
+            q.submit(C)
+        q.drain()
+        got = q.results()
+    assert begun[0] == begun[1], begun          # step 1 reused step 0's slot
+    assert sorted(got) == [0, 1, 2]
+    assert all(ent[3] is None for ent in q.finished.values())
+    ref0 = torch.flip(torch.linalg.eigvalsh(mats[0]), (0,)).cpu().numpy()
+    assert np.array_equal(got[0], ref0)
+    for s in (1, 2):
+        ref, _ = solve(ctx, mats[s], 0)
+        assert np.array_equal(got[s], ref), s
 
 
 @pytest.mark.parametrize("n", [64, 1000, 4096])

@@ -221,3 +221,31 @@ def test_verbose_outputs_match_reference(golden_dir, tmp_path):
     assert names == [str(s) for s in g["tmodes_names"]]
     for name, text in zip(names, g["tmodes_text"]):
         assert open(os.path.join(tmp_path, name)).read() == str(text)
+
+
+@pytest.mark.parametrize("seed,offset", [(1, 0), (3, 1), (12345, 1_000_003), (2024, 4_000_001)])
+def test_mt_jump_equals_sequential_draws(seed, offset):
+    """oracle.mt_jump.stream_at(seed, D) continues np.random.RandomState(seed)'s stream at double
+    D (Berlekamp-Massey characteristic polynomial, t^k mod phi, Horner on the word window): its
+    next draws equal numpy's own after drawing and discarding D doubles."""
+    from oracle import mt_jump
+    ref = np.random.RandomState(seed)
+    if offset:
+        for i in range(0, offset, 1 << 22):
+            ref.uniform(-O.SQRT3, O.SQRT3, size=min(1 << 22, offset - i))
+    got = mt_jump.stream_at(seed, offset)
+    assert np.array_equal(got.uniform(-O.SQRT3, O.SQRT3, size=4099), ref.uniform(-O.SQRT3, O.SQRT3, size=4099))
+    assert mt_jump.char_poly().bit_length() - 1 == mt_jump.DEGREE
+
+
+def test_generate_steps_jump_equals_draw(monkeypatch):
+    """generate_steps(jump=True) (gaps skipped by the MT19937 jump-ahead) == the sequential pass,
+    on late steps of a run where every gap exceeds the (lowered) jump threshold, with an
+    anisotropic x filter (nfx != nfy) as at BASELINE config 5."""
+    cfg = O.DFConfig(jma=20, kma=17, ns=400, seed=77, dt=0.5)
+    monkeypatch.setattr(O, "JUMP_MIN", 5000)
+    steps = [0, 150, 333, 399]
+    a = O.generate_steps(cfg, steps)
+    b = O.generate_steps(cfg, steps, jump=True)
+    for i in steps:
+        assert np.array_equal(a[i], b[i]), i
