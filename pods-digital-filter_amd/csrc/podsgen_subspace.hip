@@ -18,6 +18,8 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
+#include <string>
 
 #include "podsgen_ext.h"
 
@@ -196,6 +198,129 @@ __global__ __launch_bounds__(256) void k_cheb(const double* __restrict__ Ct, int
       for (int e = 0; e < 4; ++e) w[e] = fma(gamma, zv[e], fma(beta, yv[e], alpha * v[e]));
       *reinterpret_cast<f64x4*>(out + o) = w;
     }
+  }
+}
+
+// k_cheb_w: the same product without LDS or barriers.  Every wave streams its own operands
+// straight into the MFMA registers -- its 16 rows of the tiled C (one 32-B load per 16-k block)
+// and the 16 x 64 block of Y (four 32-B loads per 16-k block, L2-resident: Y is 2 MB) -- PD
+// blocks ahead, so the four waves of a workgroup never wait for each other (k_cheb's two
+// barriers per chunk and its LDS staging, ~1.25 LDS operand loads per MFMA, are gone).  Split-K
+// partials are summed by the LAST workgroup of each row block to finish (agent-scope counter),
+// in split order, with the recurrence in the same pass: no k_cheb_sum launch.  The KS
+// workgroups of a row block are dealt to one XCD, so their partials meet in its L2.
+// Same operand mapping as k_cheb (lane group g contributes k = 16 kb + 4 g + s; column tile q
+// holds columns 4 li + q).
+template <int PD>
+__global__ __launch_bounds__(256) void k_cheb_w(const double* __restrict__ Ct, int nt, int n,
+                                                const double* __restrict__ Y, const double* __restrict__ Z,
+                                                double alpha, double beta, double gamma, int kper, int ksn,
+                                                double* __restrict__ part, unsigned int* __restrict__ cnt,
+                                                double* __restrict__ out) {
+  __shared__ int last;
+  const int t = threadIdx.x, wave = t >> 6, l = t & 63;
+  const int g = l >> 4, li = l & 15;
+  // XCD-aware deal: dispatch sends workgroup b to XCD b % 8; logical ids are consecutive per XCD
+  const int total = nt * ksn;
+  const int b = blockIdx.x;
+  const int xcd = b & 7, qq = total >> 3, rr = total & 7;
+  const int logical = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
+  const int rb = logical / ksn, ks = logical - rb * ksn;
+  const int kc0 = ks * kper, kc1 = min(nt, kc0 + kper);
+  const int nblk = (kc1 - kc0) * 4;  // 16-k blocks of this split
+  const f64x4 zero4{0.0, 0.0, 0.0, 0.0};
+  const int arow = wave * 16 + li;
+  // A: row arow of tile (rb, kc), k = 16 (blk % 4) + 4 g .. + 3
+  const double* Cb = Ct + ((int64_t)rb * nt + kc0) * 4096 + arow * 64 + 4 * g;
+  // B: Y row 64 kc0 + 16 blk + 4 g + s, columns 4 li .. 4 li + 3
+  const double* Yb = Y + ((int64_t)kc0 * 64 + 4 * g) * 64 + 4 * li;
+  f64x4 a[PD], bq[PD][4];
+  auto load = [&](int blk, int u) {
+    if (blk < nblk) {
+      const int kc = blk >> 2, kb = blk & 3;
+      a[u] = *reinterpret_cast<const f64x4*>(Cb + (int64_t)kc * 4096 + 16 * kb);
+      const int64_t yr = (int64_t)16 * blk;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int64_t row = 64 * kc0 + yr + 4 * g + s;
+        bq[u][s] = row < n ? *reinterpret_cast<const f64x4*>(Yb + (yr + s) * 64) : zero4;
+      }
+    }
+  };
+  f64x4 acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = zero4;
+#pragma unroll
+  for (int u = 0; u < PD; ++u) load(u, u);
+  for (int blk0 = 0; blk0 < nblk; blk0 += PD) {
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      const int blk = blk0 + u;
+      if (blk >= nblk) break;
+      const f64x4 av = a[u];
+      f64x4 bv[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) bv[s] = bq[u][s];
+      load(blk + PD, u);  // refill this slot PD blocks ahead
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s][q], acc[q], 0, 0, 0);
+    }
+  }
+  const int r0 = rb * CB_ROWS + wave * 16;
+  if (ksn == 1) {
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg) {
+      const int r = r0 + g + 4 * rg;
+      if (r >= n) continue;
+      const int64_t o = (int64_t)r * 64 + 4 * li;
+      const f64x4 yv = *reinterpret_cast<const f64x4*>(Y + o);
+      const f64x4 zv = *reinterpret_cast<const f64x4*>(Z + o);
+      f64x4 w;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[e] = fma(gamma, zv[e], fma(beta, yv[e], alpha * acc[e][rg]));
+      *reinterpret_cast<f64x4*>(out + o) = w;
+    }
+    return;
+  }
+#pragma unroll
+  for (int rg = 0; rg < 4; ++rg) {
+    const int r = r0 + g + 4 * rg;
+    if (r >= n) continue;
+    const f64x4 v{acc[0][rg], acc[1][rg], acc[2][rg], acc[3][rg]};
+    *reinterpret_cast<f64x4*>(part + (int64_t)ks * n * 64 + (int64_t)r * 64 + 4 * li) = v;
+  }
+  // the last workgroup of row block rb to arrive sums the ksn partials in split order
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (t == 0) {
+    const unsigned int prev = __hip_atomic_fetch_add(cnt + rb, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == (unsigned int)(ksn - 1);
+    if (last) __hip_atomic_store(cnt + rb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+  }
+  __syncthreads();
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  // 64 rows x 16 quads per row block: 4 quads per thread
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int qd = t + 256 * p;
+    const int r = rb * CB_ROWS + (qd >> 4);
+    if (r >= n) continue;
+    const int64_t o = (int64_t)r * 64 + (qd & 15) * 4;
+    f64x4 s = *reinterpret_cast<const f64x4*>(part + o);
+    for (int k = 1; k < ksn; ++k) {
+      const f64x4 pk = *reinterpret_cast<const f64x4*>(part + (int64_t)k * n * 64 + o);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[e] += pk[e];
+    }
+    const f64x4 yv = *reinterpret_cast<const f64x4*>(Y + o);
+    const f64x4 zv = *reinterpret_cast<const f64x4*>(Z + o);
+    f64x4 w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w[e] = fma(gamma, zv[e], fma(beta, yv[e], alpha * s[e]));
+    *reinterpret_cast<f64x4*>(out + o) = w;
   }
 }
 
@@ -421,8 +546,30 @@ hipError_t launch_tile_c(const double* C, int64_t ldc, int n, double* Ct, hipStr
   return hipGetLastError();
 }
 
+size_t cheb_counter_words(int n) { return (size_t)((n + 63) / 64 + 64); }
+
+// PODS_CHEB selects the step kernel: w (default: k_cheb_w, no LDS / barriers, fused split-K
+// sum), lds (k_cheb + k_cheb_sum, r3); PODS_CHEB_PD the k_cheb_w prefetch depth (1..3)
+static int cheb_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PODS_CHEB");
+    v = (e && std::string(e) == "lds") ? 0 : 1;
+  }
+  return v;
+}
+static int cheb_pd() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PODS_CHEB_PD");
+    v = e ? std::max(1, std::min(3, atoi(e))) : 2;
+  }
+  return v;
+}
+
 hipError_t launch_cheb_step(const double* Ct, int n, const double* Y, const double* Z, int m, double alpha,
-                            double beta, double gamma, double* part, double* out, hipStream_t st) {
+                            double beta, double gamma, double* part, unsigned int* cnt, double* out,
+                            hipStream_t st) {
   if (n <= 0 || m != 64) return hipErrorInvalidValue;
   if (!Z) {
     Z = Y;
@@ -432,6 +579,20 @@ hipError_t launch_cheb_step(const double* Ct, int n, const double* Y, const doub
   const int ks = cheb_splits(n);
   const int kper = (nt + ks - 1) / ks;
   const int ksn = (nt + kper - 1) / kper;
+  if (cheb_variant() == 1) {
+    const dim3 g1((unsigned)(nt * ksn));
+    const int pd = cheb_pd();
+    if (pd == 1)
+      hipLaunchKernelGGL(k_cheb_w<1>, g1, dim3(256), 0, st, Ct, nt, n, Y, Z, alpha, beta, gamma, kper, ksn, part,
+                         cnt, out);
+    else if (pd == 2)
+      hipLaunchKernelGGL(k_cheb_w<2>, g1, dim3(256), 0, st, Ct, nt, n, Y, Z, alpha, beta, gamma, kper, ksn, part,
+                         cnt, out);
+    else
+      hipLaunchKernelGGL(k_cheb_w<3>, g1, dim3(256), 0, st, Ct, nt, n, Y, Z, alpha, beta, gamma, kper, ksn, part,
+                         cnt, out);
+    return hipGetLastError();
+  }
   const dim3 grid((unsigned)nt, (unsigned)ksn);
   auto kern = k_cheb;
   if (ksn == 1) {
