@@ -254,7 +254,7 @@ struct pods_ctx {
   DevBuf sub_part, sub_R, sub_cheb, sub_ct;  // subspace iteration: Gram partials, G / R^{-1}, split-K
                                              // partials, the tiled copy of C
   const double* sub_ct_src = nullptr;        // the C that sub_ct holds (pods_cheb_prepare)
-  size_t sub_cnt_off = 0;                    // byte offset of the k_cheb_w counters in sub_cheb
+  size_t sub_cnt_off = 0;                    // byte offset of the k_cheb arrival counters in sub_cheb
   int sub_ct_n = 0;
   DevBuf inv_lam;  // 1 / lambda of the spatial modes (its own buffer: no reuse hazard with lam)
   // pinned staging ring for small host -> device uploads: a slot is reused only after the

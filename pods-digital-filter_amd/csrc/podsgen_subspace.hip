@@ -1,10 +1,10 @@
 // Kernels of the Chebyshev-filtered subspace iteration for the leading POD modes
 // (podsgen/subspace.py; the eigenpairs PODFS.py:1309-1333 consumes):
 //
-//   k_cheb / k_cheb_sum   out = alpha (C Y) + beta Y + gamma Z on fp64 MFMA (v_mfma_f64_16x16x4),
+//   k_cheb                out = alpha (C Y) + beta Y + gamma Z on fp64 MFMA (v_mfma_f64_16x16x4),
 //                         C from a 64 x 64-tiled copy (k_tile_c), split-K partials summed in
-//                         order (deterministic), the filter's three-term recurrence fused into
-//                         the epilogue
+//                         order by the last workgroup of each row block (deterministic), the
+//                         filter's three-term recurrence fused into that epilogue
 //   k_gram_mfma / _reduce 64 x 64 Gram matrices Y^T Z on fp64 MFMA
 //   k_chol_inv            one wave: Cholesky of the Gram and R^{-1} (Cholesky QR)
 //   k_right_mul           Y M or Z - Y M for a 64 x 64 M (CholQR's Y R^{-1}, Rayleigh-Ritz
@@ -18,8 +18,6 @@
 
 #include <algorithm>
 #include <cstdint>
-#include <cstdlib>
-#include <string>
 
 #include "podsgen_ext.h"
 
@@ -43,15 +41,6 @@ __device__ __forceinline__ f64x4 ld4(const double* p, int64_t base, int64_t off,
   return v;
 }
 
-// Workgroup (256 threads) = 64 rows x 64 columns of out over one of KS ranges of k; wave w owns
-// rows 16 w .. 16 w + 15.  Each C element feeds exactly one MFMA k-step of 4 column tiles
-// (16 flop per byte of C), so the kernel is a stream of C at the fp64 MFMA rate (~5 TB/s): C
-// is read in 64 x 64 tiles whose rows are 512 contiguous bytes (8 lanes x 64 B per row per
-// load; MFMA-shaped loads -- 16 rows x 128 B per instruction -- streamed at 2.2 TB/s), staged
-// through LDS together with the 64 x 64 chunk of Y that all four waves share; the next chunk
-// is loaded into registers while the current one is multiplied.
-// With KS > 1 each workgroup writes its partial tile and k_cheb_sum adds the KS partials in
-// order (deterministic) and applies the recurrence; with KS = 1 the epilogue is applied here.
 constexpr int CB_ROWS = 64;  // rows per workgroup = tile edge
 constexpr int CB_K = 64;     // k per chunk = tile edge
 // LDS images in 16-byte slots, bank-conflict-free for the MFMA operand reads (ds_read_b128 lane
@@ -83,9 +72,11 @@ __global__ __launch_bounds__(256) void k_tile_c(const double* __restrict__ C, in
 // (16 flop per byte of C): the kernel streams C at the fp64 MFMA rate, one 32 KB tile per
 // chunk staged through LDS with the 64 x 64 chunk of Y that all four waves share; the next
 // chunk is loaded into registers while the current one is multiplied.
-// With KS > 1 each workgroup writes its partial tile and k_cheb_sum adds the KS partials in
-// order (deterministic) and applies the recurrence; with KS = 1 the epilogue is applied here.
-// Measured the same (55-58 us per step with the partial sum, r3): the C operand loaded
+// With KS > 1 each workgroup writes its partial tile and the last of the row block adds the KS
+// partials in order (deterministic) and applies the recurrence; with KS = 1 the epilogue is
+// applied directly.  Measured slower (r4): every wave streaming its own operands straight from
+// L2 into the MFMA registers, no LDS and no barriers (140 against 57 us: four waves each pulling
+// the whole Y chunk, 512 MB of L2 reads per step).  Measured the same (55-58 us per step with the partial sum, r3): the C operand loaded
 // straight into the MFMA registers from a copy laid out in operand order with only Y through
 // LDS, either staged by ds_write or streamed by LDS-DMA into a 2-stage ring with one barrier
 // per chunk; scheduling fences that keep each block's LDS reads 16 MFMAs ahead; two chunks of
@@ -93,14 +84,22 @@ __global__ __launch_bounds__(256) void k_tile_c(const double* __restrict__ C, in
 // (profiles/r3/mfma_util_syrk_c3.json).
 __global__ __launch_bounds__(256) void k_cheb(const double* __restrict__ Ct, int nt, int n,
                                               const double* __restrict__ Y, const double* __restrict__ Z,
-                                              double alpha, double beta, double gamma, int kper,
-                                              double* __restrict__ part, double* __restrict__ out) {
+                                              double alpha, double beta, double gamma, int kper, int ksn,
+                                              double* __restrict__ part, unsigned int* __restrict__ cnt,
+                                              double* __restrict__ out) {
   __shared__ double2 cs[CS_SLOTS];  // C tile [row][k]
   __shared__ double2 ys[YS_SLOTS];  // Y chunk [k][column]
+  __shared__ int last;
   const int t = threadIdx.x, wave = t >> 6, l = t & 63;
   const int g = l >> 4, li = l & 15;
-  const int rb = blockIdx.x;
-  const int ks = blockIdx.y;
+  // 1-D grid, XCD-aware deal (dispatch sends workgroup b to XCD b % 8): the ksn splits of a row
+  // block are consecutive logical ids, so they run on one XCD and their partials meet in its L2
+  const int total = nt * ksn;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, qq = total >> 3, rr = total & 7;
+  const int logical = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int rb = logical / ksn;
+  const int ks = logical - rb * ksn;
   const int kc0 = ks * kper, kc1 = min(nt, kc0 + kper);
   const f64x4 zero4{0.0, 0.0, 0.0, 0.0};
   const f64x4* Cq = reinterpret_cast<const f64x4*>(Ct) + (int64_t)rb * nt * 1024;
@@ -188,7 +187,7 @@ __global__ __launch_bounds__(256) void k_cheb(const double* __restrict__ Ct, int
     if (r >= n) continue;
     const f64x4 v{acc[0][rg], acc[1][rg], acc[2][rg], acc[3][rg]};
     const int64_t o = (int64_t)r * 64 + 4 * li;
-    if (part) {
+    if (ksn > 1) {
       *reinterpret_cast<f64x4*>(part + (int64_t)ks * n * 64 + o) = v;
     } else {
       const f64x4 yv = *reinterpret_cast<const f64x4*>(Y + o);
@@ -199,99 +198,10 @@ __global__ __launch_bounds__(256) void k_cheb(const double* __restrict__ Ct, int
       *reinterpret_cast<f64x4*>(out + o) = w;
     }
   }
-}
-
-// k_cheb_w: the same product without LDS or barriers.  Every wave streams its own operands
-// straight into the MFMA registers -- its 16 rows of the tiled C (one 32-B load per 16-k block)
-// and the 16 x 64 block of Y (four 32-B loads per 16-k block, L2-resident: Y is 2 MB) -- PD
-// blocks ahead, so the four waves of a workgroup never wait for each other (k_cheb's two
-// barriers per chunk and its LDS staging, ~1.25 LDS operand loads per MFMA, are gone).  Split-K
-// partials are summed by the LAST workgroup of each row block to finish (agent-scope counter),
-// in split order, with the recurrence in the same pass: no k_cheb_sum launch.  The KS
-// workgroups of a row block are dealt to one XCD, so their partials meet in its L2.
-// Same operand mapping as k_cheb (lane group g contributes k = 16 kb + 4 g + s; column tile q
-// holds columns 4 li + q).
-template <int PD>
-__global__ __launch_bounds__(256) void k_cheb_w(const double* __restrict__ Ct, int nt, int n,
-                                                const double* __restrict__ Y, const double* __restrict__ Z,
-                                                double alpha, double beta, double gamma, int kper, int ksn,
-                                                double* __restrict__ part, unsigned int* __restrict__ cnt,
-                                                double* __restrict__ out) {
-  __shared__ int last;
-  const int t = threadIdx.x, wave = t >> 6, l = t & 63;
-  const int g = l >> 4, li = l & 15;
-  // XCD-aware deal: dispatch sends workgroup b to XCD b % 8; logical ids are consecutive per XCD
-  const int total = nt * ksn;
-  const int b = blockIdx.x;
-  const int xcd = b & 7, qq = total >> 3, rr = total & 7;
-  const int logical = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
-  const int rb = logical / ksn, ks = logical - rb * ksn;
-  const int kc0 = ks * kper, kc1 = min(nt, kc0 + kper);
-  const int nblk = (kc1 - kc0) * 4;  // 16-k blocks of this split
-  const f64x4 zero4{0.0, 0.0, 0.0, 0.0};
-  const int arow = wave * 16 + li;
-  // A: row arow of tile (rb, kc), k = 16 (blk % 4) + 4 g .. + 3
-  const double* Cb = Ct + ((int64_t)rb * nt + kc0) * 4096 + arow * 64 + 4 * g;
-  // B: Y row 64 kc0 + 16 blk + 4 g + s, columns 4 li .. 4 li + 3
-  const double* Yb = Y + ((int64_t)kc0 * 64 + 4 * g) * 64 + 4 * li;
-  f64x4 a[PD], bq[PD][4];
-  auto load = [&](int blk, int u) {
-    if (blk < nblk) {
-      const int kc = blk >> 2, kb = blk & 3;
-      a[u] = *reinterpret_cast<const f64x4*>(Cb + (int64_t)kc * 4096 + 16 * kb);
-      const int64_t yr = (int64_t)16 * blk;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int64_t row = 64 * kc0 + yr + 4 * g + s;
-        bq[u][s] = row < n ? *reinterpret_cast<const f64x4*>(Yb + (yr + s) * 64) : zero4;
-      }
-    }
-  };
-  f64x4 acc[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) acc[q] = zero4;
-#pragma unroll
-  for (int u = 0; u < PD; ++u) load(u, u);
-  for (int blk0 = 0; blk0 < nblk; blk0 += PD) {
-#pragma unroll
-    for (int u = 0; u < PD; ++u) {
-      const int blk = blk0 + u;
-      if (blk >= nblk) break;
-      const f64x4 av = a[u];
-      f64x4 bv[4];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) bv[s] = bq[u][s];
-      load(blk + PD, u);  // refill this slot PD blocks ahead
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s][q], acc[q], 0, 0, 0);
-    }
-  }
-  const int r0 = rb * CB_ROWS + wave * 16;
-  if (ksn == 1) {
-#pragma unroll
-    for (int rg = 0; rg < 4; ++rg) {
-      const int r = r0 + g + 4 * rg;
-      if (r >= n) continue;
-      const int64_t o = (int64_t)r * 64 + 4 * li;
-      const f64x4 yv = *reinterpret_cast<const f64x4*>(Y + o);
-      const f64x4 zv = *reinterpret_cast<const f64x4*>(Z + o);
-      f64x4 w;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) w[e] = fma(gamma, zv[e], fma(beta, yv[e], alpha * acc[e][rg]));
-      *reinterpret_cast<f64x4*>(out + o) = w;
-    }
-    return;
-  }
-#pragma unroll
-  for (int rg = 0; rg < 4; ++rg) {
-    const int r = r0 + g + 4 * rg;
-    if (r >= n) continue;
-    const f64x4 v{acc[0][rg], acc[1][rg], acc[2][rg], acc[3][rg]};
-    *reinterpret_cast<f64x4*>(part + (int64_t)ks * n * 64 + (int64_t)r * 64 + 4 * li) = v;
-  }
-  // the last workgroup of row block rb to arrive sums the ksn partials in split order
+  if (ksn == 1) return;
+  // split-K: the LAST workgroup of row block rb to finish (agent-scope arrival counter) sums the
+  // ksn partials in split order (deterministic) and applies the recurrence -- no k_cheb_sum
+  // launch, and the partials are read back from this XCD's L2
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   __syncthreads();
   if (t == 0) {
@@ -302,7 +212,7 @@ __global__ __launch_bounds__(256) void k_cheb_w(const double* __restrict__ Ct, i
   __syncthreads();
   if (!last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  // 64 rows x 16 quads per row block: 4 quads per thread
+  // 64 rows x 16 quads: 4 quads per thread, all ksn partial loads issued before the adds
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const int qd = t + 256 * p;
@@ -322,28 +232,6 @@ __global__ __launch_bounds__(256) void k_cheb_w(const double* __restrict__ Ct, i
     for (int e = 0; e < 4; ++e) w[e] = fma(gamma, zv[e], fma(beta, yv[e], alpha * s[e]));
     *reinterpret_cast<f64x4*>(out + o) = w;
   }
-}
-
-// out = alpha * sum_ks part[ks] + beta * Y + gamma * Z  (partials in order), double4 per thread
-__global__ __launch_bounds__(256) void k_cheb_sum(const double* __restrict__ part, int ksn, int64_t nq,
-                                                  const double* __restrict__ Y, const double* __restrict__ Z,
-                                                  double alpha, double beta, double gamma,
-                                                  double* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // quad index
-  if (i >= nq) return;
-  const f64x4* P = reinterpret_cast<const f64x4*>(part);
-  f64x4 s = P[i];
-  for (int k = 1; k < ksn; ++k) {
-    const f64x4 p = P[(int64_t)k * nq + i];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) s[e] += p[e];
-  }
-  const f64x4 yv = reinterpret_cast<const f64x4*>(Y)[i];
-  const f64x4 zv = reinterpret_cast<const f64x4*>(Z)[i];
-  f64x4 w;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) w[e] = fma(gamma, zv[e], fma(beta, yv[e], alpha * s[e]));
-  reinterpret_cast<f64x4*>(out)[i] = w;
 }
 
 // ---- small dense pieces of the iteration: Gram matrices, Cholesky QR, block rotations ----
@@ -548,25 +436,6 @@ hipError_t launch_tile_c(const double* C, int64_t ldc, int n, double* Ct, hipStr
 
 size_t cheb_counter_words(int n) { return (size_t)((n + 63) / 64 + 64); }
 
-// PODS_CHEB selects the step kernel: w (default: k_cheb_w, no LDS / barriers, fused split-K
-// sum), lds (k_cheb + k_cheb_sum, r3); PODS_CHEB_PD the k_cheb_w prefetch depth (1..3)
-static int cheb_variant() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("PODS_CHEB");
-    v = (e && std::string(e) == "lds") ? 0 : 1;
-  }
-  return v;
-}
-static int cheb_pd() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("PODS_CHEB_PD");
-    v = e ? std::max(1, std::min(3, atoi(e))) : 2;
-  }
-  return v;
-}
-
 hipError_t launch_cheb_step(const double* Ct, int n, const double* Y, const double* Z, int m, double alpha,
                             double beta, double gamma, double* part, unsigned int* cnt, double* out,
                             hipStream_t st) {
@@ -579,31 +448,8 @@ hipError_t launch_cheb_step(const double* Ct, int n, const double* Y, const doub
   const int ks = cheb_splits(n);
   const int kper = (nt + ks - 1) / ks;
   const int ksn = (nt + kper - 1) / kper;
-  if (cheb_variant() == 1) {
-    const dim3 g1((unsigned)(nt * ksn));
-    const int pd = cheb_pd();
-    if (pd == 1)
-      hipLaunchKernelGGL(k_cheb_w<1>, g1, dim3(256), 0, st, Ct, nt, n, Y, Z, alpha, beta, gamma, kper, ksn, part,
-                         cnt, out);
-    else if (pd == 2)
-      hipLaunchKernelGGL(k_cheb_w<2>, g1, dim3(256), 0, st, Ct, nt, n, Y, Z, alpha, beta, gamma, kper, ksn, part,
-                         cnt, out);
-    else
-      hipLaunchKernelGGL(k_cheb_w<3>, g1, dim3(256), 0, st, Ct, nt, n, Y, Z, alpha, beta, gamma, kper, ksn, part,
-                         cnt, out);
-    return hipGetLastError();
-  }
-  const dim3 grid((unsigned)nt, (unsigned)ksn);
-  auto kern = k_cheb;
-  if (ksn == 1) {
-    hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, Ct, nt, n, Y, Z, alpha, beta, gamma, kper, (double*)nullptr,
-                       out);
-    return hipGetLastError();
-  }
-  hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, Ct, nt, n, Y, Z, alpha, beta, gamma, kper, part, out);
-  const int64_t nq = (int64_t)n * 16;
-  hipLaunchKernelGGL(k_cheb_sum, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, part, ksn, nq, Y, Z, alpha,
-                     beta, gamma, out);
+  hipLaunchKernelGGL(k_cheb, dim3((unsigned)(nt * ksn)), dim3(256), 0, st, Ct, nt, n, Y, Z, alpha, beta, gamma, kper,
+                     ksn, part, cnt, out);
   return hipGetLastError();
 }
 
