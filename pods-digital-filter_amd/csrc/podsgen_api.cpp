@@ -254,7 +254,6 @@ struct pods_ctx {
   DevBuf sub_part, sub_R, sub_cheb, sub_ct;  // subspace iteration: Gram partials, G / R^{-1}, split-K
                                              // partials, the tiled copy of C
   const double* sub_ct_src = nullptr;        // the C that sub_ct holds (pods_cheb_prepare)
-  size_t sub_cnt_off = 0;                    // byte offset of the k_cheb arrival counters in sub_cheb
   int sub_ct_n = 0;
   DevBuf inv_lam;  // 1 / lambda of the spatial modes (its own buffer: no reuse hazard with lam)
   // pinned staging ring for small host -> device uploads: a slot is reused only after the
@@ -822,18 +821,9 @@ int pods_cheb_step(pods_ctx* c, const double* C, int n, const double* Y, const d
     return fail(PODS_ERR_ARG, "pods_cheb_step: bad arguments (m = 64, out distinct)");
   if (C != c->sub_ct_src || n != c->sub_ct_n)
     return fail(PODS_ERR_STATE, "pods_cheb_step: C was not prepared (pods_cheb_prepare)");
-  // split-K partials, then the row blocks' arrival counters (zeroed whenever the buffer is new)
-  const size_t pbytes = (size_t)pods::cheb_splits(n) * n * 64 * sizeof(double);
-  const size_t cbytes = pods::cheb_counter_words(n) * sizeof(unsigned int);
-  void* before = c->sub_cheb.p;
-  PODS_HIP(ensure(c->sub_cheb, pbytes + cbytes));
-  unsigned int* cnt = reinterpret_cast<unsigned int*>(c->sub_cheb.as<char>() + pbytes);
-  if (c->sub_cheb.p != before || c->sub_cnt_off != pbytes) {
-    PODS_HIP(hipMemsetAsync(cnt, 0, cbytes, c->stream));
-    c->sub_cnt_off = pbytes;
-  }
+  PODS_HIP(ensure(c->sub_cheb, (size_t)pods::cheb_splits(n) * n * 64 * sizeof(double)));
   PODS_HIP(pods::launch_cheb_step(c->sub_ct.as<double>(), n, Y, Z, m, alpha, beta, gamma, c->sub_cheb.as<double>(),
-                                  cnt, out, c->stream));
+                                  out, c->stream));
   return PODS_OK;
 }
 

@@ -25,12 +25,8 @@ hipError_t launch_gather_snapshots(const double* AT, int ns, int64_t rowlen, int
 int cheb_splits(int n);
 size_t cheb_tiled_doubles(int n);
 hipError_t launch_tile_c(const double* C, int64_t ldc, int n, double* Ct, hipStream_t st);
-// cnt: cheb_counter_words(n) zeroed uint32 (row-block arrival counters of the fused split-K sum;
-// left zeroed by every launch)
-size_t cheb_counter_words(int n);
 hipError_t launch_cheb_step(const double* Ct, int n, const double* Y, const double* Z, int m, double alpha,
-                            double beta, double gamma, double* part, unsigned int* cnt, double* out,
-                            hipStream_t st);
+                            double beta, double gamma, double* part, double* out, hipStream_t st);
 
 // small dense pieces of the subspace iteration, m = 64 (podsgen_subspace.hip):
 // G = Y^T Z (64 x 64) through gram_slices(n) row-slice partials in part (summed in order);

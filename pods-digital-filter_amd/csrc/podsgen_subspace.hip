@@ -1,10 +1,10 @@
 // Kernels of the Chebyshev-filtered subspace iteration for the leading POD modes
 // (podsgen/subspace.py; the eigenpairs PODFS.py:1309-1333 consumes):
 //
-//   k_cheb                out = alpha (C Y) + beta Y + gamma Z on fp64 MFMA (v_mfma_f64_16x16x4),
+//   k_cheb / k_cheb_sum   out = alpha (C Y) + beta Y + gamma Z on fp64 MFMA (v_mfma_f64_16x16x4),
 //                         C from a 64 x 64-tiled copy (k_tile_c), split-K partials summed in
-//                         order by the last workgroup of each row block (deterministic), the
-//                         filter's three-term recurrence fused into that epilogue
+//                         order (deterministic), the filter's three-term recurrence fused into
+//                         the epilogue
 //   k_gram_mfma / _reduce 64 x 64 Gram matrices Y^T Z on fp64 MFMA
 //   k_chol_inv            one wave: Cholesky of the Gram and R^{-1} (Cholesky QR)
 //   k_right_mul           Y M or Z - Y M for a 64 x 64 M (CholQR's Y R^{-1}, Rayleigh-Ritz
@@ -41,6 +41,15 @@ __device__ __forceinline__ f64x4 ld4(const double* p, int64_t base, int64_t off,
   return v;
 }
 
+// Workgroup (256 threads) = 64 rows x 64 columns of out over one of KS ranges of k; wave w owns
+// rows 16 w .. 16 w + 15.  Each C element feeds exactly one MFMA k-step of 4 column tiles
+// (16 flop per byte of C), so the kernel is a stream of C at the fp64 MFMA rate (~5 TB/s): C
+// is read in 64 x 64 tiles whose rows are 512 contiguous bytes (8 lanes x 64 B per row per
+// load; MFMA-shaped loads -- 16 rows x 128 B per instruction -- streamed at 2.2 TB/s), staged
+// through LDS together with the 64 x 64 chunk of Y that all four waves share; the next chunk
+// is loaded into registers while the current one is multiplied.
+// With KS > 1 each workgroup writes its partial tile and k_cheb_sum adds the KS partials in
+// order (deterministic) and applies the recurrence; with KS = 1 the epilogue is applied here.
 constexpr int CB_ROWS = 64;  // rows per workgroup = tile edge
 constexpr int CB_K = 64;     // k per chunk = tile edge
 // LDS images in 16-byte slots, bank-conflict-free for the MFMA operand reads (ds_read_b128 lane
@@ -72,34 +81,29 @@ __global__ __launch_bounds__(256) void k_tile_c(const double* __restrict__ C, in
 // (16 flop per byte of C): the kernel streams C at the fp64 MFMA rate, one 32 KB tile per
 // chunk staged through LDS with the 64 x 64 chunk of Y that all four waves share; the next
 // chunk is loaded into registers while the current one is multiplied.
-// With KS > 1 each workgroup writes its partial tile and the last of the row block adds the KS
-// partials in order (deterministic) and applies the recurrence; with KS = 1 the epilogue is
-// applied directly.  Measured slower (r4): every wave streaming its own operands straight from
-// L2 into the MFMA registers, no LDS and no barriers (140 against 57 us: four waves each pulling
-// the whole Y chunk, 512 MB of L2 reads per step).  Measured the same (55-58 us per step with the partial sum, r3): the C operand loaded
+// With KS > 1 each workgroup writes its partial tile and k_cheb_sum adds the KS partials in
+// order (deterministic) and applies the recurrence; with KS = 1 the epilogue is applied here.
+// Measured the same (55-58 us per step with the partial sum, r3): the C operand loaded
 // straight into the MFMA registers from a copy laid out in operand order with only Y through
 // LDS, either staged by ds_write or streamed by LDS-DMA into a 2-stage ring with one barrier
 // per chunk; scheduling fences that keep each block's LDS reads 16 MFMAs ahead; two chunks of
 // register prefetch; 4 or 16 K splits.  The fp64 MFMA pipe is busy 45 % of the kernel
-// (profiles/r3/mfma_util_syrk_c3.json).
+// (profiles/r3/mfma_util_syrk_c3.json).  Measured slower in r4 (tools/cheb_bench.py, one call):
+// every wave streaming its own operands from L2 straight into the MFMA registers, no LDS and no
+// barriers, 140 against 57 us (four waves each pull the whole Y chunk: 512 MB of L2 reads per
+// step); the split-K sum fused into this kernel (the last workgroup of a row block adds the
+// partials), 127 us with an agent-scope release per workgroup (an XCD L2 write-back each) and
+// 63.7 us with sc1 partial stores and loads (the last workgroup's loads are a serial tail).
 __global__ __launch_bounds__(256) void k_cheb(const double* __restrict__ Ct, int nt, int n,
                                               const double* __restrict__ Y, const double* __restrict__ Z,
-                                              double alpha, double beta, double gamma, int kper, int ksn,
-                                              double* __restrict__ part, unsigned int* __restrict__ cnt,
-                                              double* __restrict__ out) {
+                                              double alpha, double beta, double gamma, int kper,
+                                              double* __restrict__ part, double* __restrict__ out) {
   __shared__ double2 cs[CS_SLOTS];  // C tile [row][k]
   __shared__ double2 ys[YS_SLOTS];  // Y chunk [k][column]
-  __shared__ int last;
   const int t = threadIdx.x, wave = t >> 6, l = t & 63;
   const int g = l >> 4, li = l & 15;
-  // 1-D grid, XCD-aware deal (dispatch sends workgroup b to XCD b % 8): the ksn splits of a row
-  // block are consecutive logical ids, so they run on one XCD and their partials meet in its L2
-  const int total = nt * ksn;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, qq = total >> 3, rr = total & 7;
-  const int logical = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
-  const int rb = logical / ksn;
-  const int ks = logical - rb * ksn;
+  const int rb = blockIdx.x;
+  const int ks = blockIdx.y;
   const int kc0 = ks * kper, kc1 = min(nt, kc0 + kper);
   const f64x4 zero4{0.0, 0.0, 0.0, 0.0};
   const f64x4* Cq = reinterpret_cast<const f64x4*>(Ct) + (int64_t)rb * nt * 1024;
@@ -187,7 +191,7 @@ __global__ __launch_bounds__(256) void k_cheb(const double* __restrict__ Ct, int
     if (r >= n) continue;
     const f64x4 v{acc[0][rg], acc[1][rg], acc[2][rg], acc[3][rg]};
     const int64_t o = (int64_t)r * 64 + 4 * li;
-    if (ksn > 1) {
+    if (part) {
       *reinterpret_cast<f64x4*>(part + (int64_t)ks * n * 64 + o) = v;
     } else {
       const f64x4 yv = *reinterpret_cast<const f64x4*>(Y + o);
@@ -198,40 +202,28 @@ __global__ __launch_bounds__(256) void k_cheb(const double* __restrict__ Ct, int
       *reinterpret_cast<f64x4*>(out + o) = w;
     }
   }
-  if (ksn == 1) return;
-  // split-K: the LAST workgroup of row block rb to finish (agent-scope arrival counter) sums the
-  // ksn partials in split order (deterministic) and applies the recurrence -- no k_cheb_sum
-  // launch, and the partials are read back from this XCD's L2
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __syncthreads();
-  if (t == 0) {
-    const unsigned int prev = __hip_atomic_fetch_add(cnt + rb, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    last = prev == (unsigned int)(ksn - 1);
-    if (last) __hip_atomic_store(cnt + rb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+}
+
+// out = alpha * sum_ks part[ks] + beta * Y + gamma * Z  (partials in order), double4 per thread
+__global__ __launch_bounds__(256) void k_cheb_sum(const double* __restrict__ part, int ksn, int64_t nq,
+                                                  const double* __restrict__ Y, const double* __restrict__ Z,
+                                                  double alpha, double beta, double gamma,
+                                                  double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // quad index
+  if (i >= nq) return;
+  const f64x4* P = reinterpret_cast<const f64x4*>(part);
+  f64x4 s = P[i];
+  for (int k = 1; k < ksn; ++k) {
+    const f64x4 p = P[(int64_t)k * nq + i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s[e] += p[e];
   }
-  __syncthreads();
-  if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  // 64 rows x 16 quads: 4 quads per thread, all ksn partial loads issued before the adds
+  const f64x4 yv = reinterpret_cast<const f64x4*>(Y)[i];
+  const f64x4 zv = reinterpret_cast<const f64x4*>(Z)[i];
+  f64x4 w;
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int qd = t + 256 * p;
-    const int r = rb * CB_ROWS + (qd >> 4);
-    if (r >= n) continue;
-    const int64_t o = (int64_t)r * 64 + (qd & 15) * 4;
-    f64x4 s = *reinterpret_cast<const f64x4*>(part + o);
-    for (int k = 1; k < ksn; ++k) {
-      const f64x4 pk = *reinterpret_cast<const f64x4*>(part + (int64_t)k * n * 64 + o);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) s[e] += pk[e];
-    }
-    const f64x4 yv = *reinterpret_cast<const f64x4*>(Y + o);
-    const f64x4 zv = *reinterpret_cast<const f64x4*>(Z + o);
-    f64x4 w;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) w[e] = fma(gamma, zv[e], fma(beta, yv[e], alpha * s[e]));
-    *reinterpret_cast<f64x4*>(out + o) = w;
-  }
+  for (int e = 0; e < 4; ++e) w[e] = fma(gamma, zv[e], fma(beta, yv[e], alpha * s[e]));
+  reinterpret_cast<f64x4*>(out)[i] = w;
 }
 
 // ---- small dense pieces of the iteration: Gram matrices, Cholesky QR, block rotations ----
@@ -434,11 +426,8 @@ hipError_t launch_tile_c(const double* C, int64_t ldc, int n, double* Ct, hipStr
   return hipGetLastError();
 }
 
-size_t cheb_counter_words(int n) { return (size_t)((n + 63) / 64 + 64); }
-
 hipError_t launch_cheb_step(const double* Ct, int n, const double* Y, const double* Z, int m, double alpha,
-                            double beta, double gamma, double* part, unsigned int* cnt, double* out,
-                            hipStream_t st) {
+                            double beta, double gamma, double* part, double* out, hipStream_t st) {
   if (n <= 0 || m != 64) return hipErrorInvalidValue;
   if (!Z) {
     Z = Y;
@@ -448,8 +437,17 @@ hipError_t launch_cheb_step(const double* Ct, int n, const double* Y, const doub
   const int ks = cheb_splits(n);
   const int kper = (nt + ks - 1) / ks;
   const int ksn = (nt + kper - 1) / kper;
-  hipLaunchKernelGGL(k_cheb, dim3((unsigned)(nt * ksn)), dim3(256), 0, st, Ct, nt, n, Y, Z, alpha, beta, gamma, kper,
-                     ksn, part, cnt, out);
+  const dim3 grid((unsigned)nt, (unsigned)ksn);
+  auto kern = k_cheb;
+  if (ksn == 1) {
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, Ct, nt, n, Y, Z, alpha, beta, gamma, kper, (double*)nullptr,
+                       out);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, Ct, nt, n, Y, Z, alpha, beta, gamma, kper, part, out);
+  const int64_t nq = (int64_t)n * 16;
+  hipLaunchKernelGGL(k_cheb_sum, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, part, ksn, nq, Y, Z, alpha,
+                     beta, gamma, out);
   return hipGetLastError();
 }
 
