@@ -205,9 +205,12 @@ int pods_stream_wait_marker(pods_ctx* ctx, void* stream);
 
 /* All n eigenvalues of C alone (the full spectrum POD.eigenvalues.dat and the valid-mode count
  * consume, PODFS.py:1309-1320, :1339), as a sequence of stream-ordered units that a caller can
- * spread over several calls: units 0..U-2 are the column ranges of the tridiagonalisation
- * (512 columns each, U - 1 = (n-1)/512 + 1), unit U-1 the bisection.  Each slot (0..15) has its
- * own workspace, so several matrices may be in flight at once.  n <= 4096.
+ * spread over several calls.  n <= 4096: units 0..U-2 are the column ranges of the on-chip
+ * tridiagonalisation (512 columns each, U - 1 = (n-1)/512 + 1), unit U-1 the bisection.
+ * 4096 < n <= 16384: the two-stage solver of pods_syev2 without vectors -- units of 32 stage-1
+ * panels (1024 columns reduced to band 32), then units of 512 bulge-chasing sweep groups (1024
+ * sweeps), then the bisection (n = 8192: 8 + 8 + 1 units).  Each slot (0..15) has its own
+ * workspace, so several matrices may be in flight at once.
  *   pods_eigvals_begin    starts slot on C_dev (n x n row-major, read by unit 0 only, so C may
  *                         be reused by work enqueued after this call) and runs unit 0
  *   pods_eigvals_advance  runs up to max_units more units; *remaining = units still to run

@@ -216,6 +216,13 @@ struct EigvalSlot {
   int next = 0;       // next unit: ranges 0..klast, then klast + 1 = the bisection
   bool active = false;
   pods::TrdArgs args{};
+  // n > 4096: the two-stage solver in units (stage-1 panel groups, chase sweep-group ranges,
+  // the eigenvalues); flags: 64 panel flags, 64 abort words, n sweep counters
+  bool two = false;
+  DevBuf ws2;
+  pods::SyevdPlan plan{};
+  uint32_t epoch = 0;
+  size_t flag_words = 0;
 };
 
 struct pods_ctx {
@@ -442,7 +449,7 @@ int pods_destroy(pods_ctx* c) {
   release(c->sub_cheb);
   release(c->sub_ct);
   for (EigvalSlot& sl : c->eslots)
-    for (DevBuf* b : {&sl.wm, &sl.x, &sl.flags, &sl.det, &sl.v, &sl.cnt, &sl.lam}) release(*b);
+    for (DevBuf* b : {&sl.wm, &sl.x, &sl.flags, &sl.det, &sl.v, &sl.cnt, &sl.lam, &sl.ws2}) release(*b);
   release(c->inv_lam);
   if (c->pin) {
     for (int i = 0; i < pods_ctx::kStageSlots; ++i)
@@ -999,12 +1006,45 @@ int run_sytrd(pods_ctx* c, const double* C, int n, int* R_out, int64_t* trace = 
 namespace {
 constexpr int EIGVAL_SLOTS = 16;
 
-int eigval_units(const EigvalSlot& sl) { return sl.klast + 2; }  // trd ranges + the bisection
+// two-stage units: PANEL_UNIT stage-1 panels (32 columns each) or CHASE_UNIT sweep groups (two
+// sweeps each) per unit; at n = 8192: 8 + 8 units and the eigenvalues
+constexpr int PANEL_UNIT = 32, CHASE_UNIT = 512;
+int two_panel_units(const EigvalSlot& sl) { return (sl.plan.np + PANEL_UNIT - 1) / PANEL_UNIT; }
+int two_chase_units(const EigvalSlot& sl) { return (pods::syevd2_groups(sl.n) + CHASE_UNIT - 1) / CHASE_UNIT; }
+
+int eigval_units(const EigvalSlot& sl) {
+  if (sl.two) return two_panel_units(sl) + two_chase_units(sl) + 1;
+  return sl.klast + 2;  // trd ranges + the bisection
+}
+
+// the slot's abort words: the tridiagonalisation's one, or the two-stage solver's two
+uint32_t* slot_abort(const EigvalSlot& sl) { return sl.flags.as<uint32_t>() + (sl.two ? 64 : 0); }
+int slot_abort_words(const EigvalSlot& sl) { return sl.two ? 2 : 1; }
+
+int eigval_run_two(pods_ctx* c, EigvalSlot& sl, int end) {
+  const int npu = two_panel_units(sl), ncu = two_chase_units(sl);
+  double* ws = sl.ws2.as<double>();
+  uint32_t* fl = sl.flags.as<uint32_t>();
+  for (int u = sl.next; u < end; ++u) {
+    if (u < npu) {
+      PODS_HIP(pods::syevd2_panels(sl.n, ws, sl.plan, fl, sl.epoch, u * PANEL_UNIT, (u + 1) * PANEL_UNIT, c->stream));
+      if (u == npu - 1) PODS_HIP(pods::syevd2_band(sl.n, ws, sl.plan, false, c->stream));
+    } else if (u < npu + ncu) {
+      const int q0 = (u - npu) * CHASE_UNIT;
+      PODS_HIP(pods::syevd2_chase(sl.n, ws, sl.plan, fl, q0, q0 + CHASE_UNIT, c->stream));
+    } else {
+      PODS_HIP(pods::syevd2_eigvals(sl.n, ws, sl.plan, sl.cnt.as<int>(), sl.lam.as<double>(), c->stream));
+    }
+  }
+  sl.next = end;
+  return PODS_OK;
+}
 
 // launch the slot's units [next, next + count)
 int eigval_run(pods_ctx* c, EigvalSlot& sl, int count) {
   const int total = eigval_units(sl);
   const int end = std::min(total, sl.next + count);
+  if (sl.two) return eigval_run_two(c, sl, end);
   if (sl.next <= sl.klast && end > sl.next) {
     const int ke = std::min(end - 1, sl.klast);
     PODS_HIP(pods::launch_trd_ranges(sl.args, sl.R, sl.next, ke, c->stream));
@@ -1025,14 +1065,42 @@ int pods_eigvals_begin(pods_ctx* c, int slot, const double* C, int n) {
   if (slot < 0 || slot >= EIGVAL_SLOTS || !C || n < 1) return fail(PODS_ERR_ARG, "pods_eigvals_begin: bad arguments");
   int R = 0, G = 0;
   int64_t slab = 0;
-  if (pods::trd_plan(n, &R, &G, &slab) != 0)
-    return fail(PODS_ERR_UNSUPPORTED, "pods_eigvals_begin: n = " + std::to_string(n) + " > 4096");
+  const bool two = pods::trd_plan(n, &R, &G, &slab) != 0;
+  if (two && (n < 3 || n > pods::syev2_max_n()))
+    return fail(PODS_ERR_UNSUPPORTED, "pods_eigvals_begin: n = " + std::to_string(n) + " > " +
+                                          std::to_string(pods::syev2_max_n()));
   PODS_HIP(hipSetDevice(c->device));
   PersistentLock lk(c);
   if ((int)c->eslots.size() <= slot) c->eslots.resize(slot + 1);
   EigvalSlot& sl = c->eslots[slot];
   if (sl.active && sl.next < eigval_units(sl))
     return fail(PODS_ERR_STATE, "pods_eigvals_begin: slot " + std::to_string(slot) + " still running");
+  if (two) {  // the two-stage solver, eigenvalues only, in units (stage 1, chase, eigenvalues)
+    const size_t wsd = pods::sy2sb_work_doubles(n, 0, &sl.plan);
+    PODS_HIP(ensure(sl.ws2, wsd * sizeof(double)));
+    const size_t fw = 128 + (size_t)n;
+    if (sl.flag_words < fw) {  // panel flags start zeroed; the epoch keeps their tags apart
+      PODS_HIP(ensure(sl.flags, fw * sizeof(uint32_t)));
+      PODS_HIP(hipMemsetAsync(sl.flags.p, 0, fw * sizeof(uint32_t), c->stream));
+      sl.flag_words = fw;
+      sl.epoch = 0;
+    }
+    PODS_HIP(hipMemsetAsync(sl.flags.as<uint32_t>() + 64, 0, 64 * sizeof(uint32_t), c->stream));  // abort words
+    PODS_HIP(ensure(sl.cnt, pods::tri_grid_bytes()));
+    PODS_HIP(ensure(sl.lam, (size_t)n * sizeof(double)));
+    ++sl.epoch;
+    sl.two = true;
+    sl.n = n;
+    sl.next = 0;
+    sl.active = true;
+    PODS_HIP(pods::syevd2_begin(C, n, sl.ws2.as<double>(), sl.plan, sl.flags.as<uint32_t>(), c->stream));
+    if (int e = eigval_run(c, sl, 1)) return e;  // unit 0, like the tridiagonalisation (C is copied)
+    return lk.release();
+  }
+  if (sl.two) {  // the slot held a two-stage solve before: its flag layout differs
+    sl.two = false;
+    sl.flag_words = 0;
+  }
   PODS_HIP(ensure(sl.wm, (size_t)slab * sizeof(double)));
   PODS_HIP(ensure(sl.x, (size_t)32 * n * sizeof(double)));
   PODS_HIP(ensure(sl.flags, 64));
@@ -1103,10 +1171,12 @@ int pods_eigvals_status(pods_ctx* c, int slot) {
   if (int e = check_ctx(c)) return e;
   if (slot < 0 || slot >= (int)c->eslots.size() || !c->eslots[slot].active)
     return fail(PODS_ERR_ARG, "pods_eigvals_status: no such slot");
-  uint32_t abort_word = 0;
-  PODS_HIP(hipMemcpyAsync(&abort_word, c->eslots[slot].flags.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+  const EigvalSlot& sl = c->eslots[slot];
+  uint32_t abort_word[2] = {0, 0};
+  PODS_HIP(hipMemcpyAsync(abort_word, slot_abort(sl), slot_abort_words(sl) * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                          c->stream));
   PODS_HIP(hipStreamSynchronize(c->stream));
-  if (abort_word) return fail(PODS_ERR_INTERNAL, "pods_eigvals: hand-off wait timed out (aborted)");
+  if (abort_word[0] || abort_word[1]) return fail(PODS_ERR_INTERNAL, "pods_eigvals: hand-off wait timed out (aborted)");
   return PODS_OK;
   PODS_CATCH
 }
@@ -1117,7 +1187,9 @@ int pods_eigvals_flags_async(pods_ctx* c, int slot, uint32_t* flags_dst) {
   if (slot < 0 || slot >= (int)c->eslots.size() || !c->eslots[slot].active || !flags_dst)
     return fail(PODS_ERR_ARG, "pods_eigvals_flags_async: no such slot");
   PODS_HIP(hipSetDevice(c->device));
-  PODS_HIP(hipMemcpyAsync(flags_dst, c->eslots[slot].flags.p, sizeof(uint32_t), hipMemcpyDefault, c->stream));
+  const EigvalSlot& sl = c->eslots[slot];
+  PODS_HIP(hipMemcpyAsync(flags_dst, slot_abort(sl), slot_abort_words(sl) * sizeof(uint32_t), hipMemcpyDefault,
+                          c->stream));
   return PODS_OK;
   PODS_CATCH
 }
@@ -1128,7 +1200,7 @@ int pods_eigvals_inject_abort(pods_ctx* c, int slot) {
   if (slot < 0 || slot >= (int)c->eslots.size() || !c->eslots[slot].active)
     return fail(PODS_ERR_ARG, "pods_eigvals_inject_abort: no such slot");
   PODS_HIP(hipSetDevice(c->device));
-  PODS_HIP(hipMemsetAsync(c->eslots[slot].flags.p, 1, sizeof(uint32_t), c->stream));
+  PODS_HIP(hipMemsetAsync(slot_abort(c->eslots[slot]), 1, sizeof(uint32_t), c->stream));
   return PODS_OK;
   PODS_CATCH
 }

@@ -124,6 +124,17 @@ size_t sy2sb_work_doubles(int n, int nvec, SyevdPlan* plan);
 // that grows by one per call (the panel hand-off tags); grid_cnt: tri_grid_bytes()
 hipError_t launch_syevd2(const double* C, int n, int nvec, double* ws, const SyevdPlan& p, uint32_t* flags,
                          uint32_t epoch, int* ipiv, int* grid_cnt, double* lam_desc, double* vec, hipStream_t st);
+// the same solve in stages (eigenvalues only when spread over calls: pods_eigvals_* for n > 4096):
+// begin (copies C, clears the chase counters and panel slots), stage-1 panels [pi0, pi1) (plan.np
+// panels), the band (band0 kept for the vectors), chase sweep groups [q0, q1) of syevd2_groups(n)
+// (every earlier group finished), the eigenvalues (descending)
+hipError_t syevd2_begin(const double* C, int n, double* ws, const SyevdPlan& p, uint32_t* flags, hipStream_t st);
+hipError_t syevd2_panels(int n, double* ws, const SyevdPlan& p, uint32_t* flags, uint32_t epoch, int pi0, int pi1,
+                         hipStream_t st);
+hipError_t syevd2_band(int n, double* ws, const SyevdPlan& p, bool keep_band0, hipStream_t st);
+int syevd2_groups(int n);
+hipError_t syevd2_chase(int n, double* ws, const SyevdPlan& p, uint32_t* flags, int q0, int q1, hipStream_t st);
+hipError_t syevd2_eigvals(int n, double* ws, const SyevdPlan& p, int* grid_cnt, double* lam_desc, hipStream_t st);
 size_t bt_part_bytes(int n, int nvec);
 size_t bt_w2_bytes(int nvec);
 

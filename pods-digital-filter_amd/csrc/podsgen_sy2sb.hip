@@ -744,8 +744,8 @@ struct SbWin {
 };
 
 template <int B, int G>
-__global__ __launch_bounds__(64 * (G + 3), 1) void k_sbtrd_win(double* __restrict__ band, int n, int ngroups,
-                                                                uint32_t* __restrict__ gprog,
+__global__ __launch_bounds__(64 * (G + 3), 1) void k_sbtrd_win(double* __restrict__ band, int n, int qbeg,
+                                                                int qend, uint32_t* __restrict__ gprog,
                                                                 uint32_t* __restrict__ abortw,
                                                                 double* __restrict__ scratch,
                                                                 int64_t* __restrict__ wtr, int wq0) {
@@ -775,14 +775,15 @@ __global__ __launch_bounds__(64 * (G + 3), 1) void k_sbtrd_win(double* __restric
   // element d of band column cc in the ring
   auto ri = [&](int cc, int d) -> int { return (cc % W) * LDB + d; };
   auto ntask = [&](int s) -> int { return s < n - 2 ? (n - 2 - s + B - 1) / B : 0; };
-  for (int q = blockIdx.x; q < ngroups; q += gridDim.x) {
+  // groups [qbeg, qend) of this launch; every group before qbeg finished in an earlier launch
+  for (int q = qbeg + blockIdx.x; q < qend; q += gridDim.x) {
     const int s0 = q * G;  // even: the two columns of one DMA share an even slot pair
     const int gq = min(G, n - 2 - s0);
     const int tend = ntask(s0) + 3 * (gq - 1);
     const int nblk = (n - s0 + B - 1) / B;
     auto blk_end = [&](int b) -> int { return min(n, s0 + (b + 1) * B); };
     if (t == 0) {
-      s_avail = q == 0 ? n : 0;
+      s_avail = q == qbeg ? n : 0;
       s_wread = -1;
     }
     __syncthreads();
@@ -827,7 +828,7 @@ __global__ __launch_bounds__(64 * (G + 3), 1) void k_sbtrd_win(double* __restric
     };
     auto poll_until = [&](int need) {  // poller
       need = min(need, n);
-      if (lane == 0 && q > 0) {
+      if (lane == 0 && q > qbeg) {
         int got = __hip_atomic_load(&s_avail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), spin = 0;
         while (got < need) {
           got = (int)ld_f(gprog + q - 1);
@@ -1336,23 +1337,32 @@ size_t sy2sb_work_doubles(int n, int nvec, SyevdPlan* plan) {
   return (size_t)p.off_end;
 }
 
-hipError_t launch_syevd2(const double* C, int n, int nvec, double* ws, const SyevdPlan& p, uint32_t* flags,
-                         uint32_t epoch, int* ipiv, int* grid_cnt, double* lam_desc, double* vec, hipStream_t st) {
+// ---- launch_syevd2 in stages, so a caller can spread one eigenvalues-only solve over several
+// calls (pods_eigvals_* for n > 4096): begin, panel ranges of stage 1, the band, sweep-group
+// ranges of the bulge chase, the eigenvalues.  launch_syevd2 runs them back to back.
+hipError_t syevd2_begin(const double* C, int n, double* ws, const SyevdPlan& p, uint32_t* flags, hipStream_t st) {
   constexpr int B = 32;
-  double* Aw = ws + p.off_aw;
-  hipError_t e = hipMemcpyAsync(Aw, C, (size_t)n * n * sizeof(double), hipMemcpyDeviceToDevice, st);
+  hipError_t e = hipMemcpyAsync(ws + p.off_aw, C, (size_t)n * n * sizeof(double), hipMemcpyDeviceToDevice, st);
   if (e != hipSuccess) return e;
-  uint32_t* pflags = flags;        // 64 panel-QR flags
-  uint32_t* abortw = flags + 64;   // [0] panel QR, [1] stage 2
-  uint32_t* prog = flags + 128;    // n sweep counters
-  e = hipMemsetAsync(prog, 0, (size_t)n * sizeof(uint32_t), st);
+  e = hipMemsetAsync(flags + 128, 0, (size_t)n * sizeof(uint32_t), st);  // the chase's sweep counters
   if (e != hipSuccess) return e;
   // k_pqr's tagged hand-off slots start from tag 0 (the first column's tag is 1)
-  e = hipMemsetAsync(ws + p.off_pub, 0, (size_t)2 * 64 * 2 * B * sizeof(double), st);
-  if (e != hipSuccess) return e;
+  return hipMemsetAsync(ws + p.off_pub, 0, (size_t)2 * 64 * 2 * B * sizeof(double), st);
+}
+
+// stage 1, panels [pi0, pi1) (panel pi reduces columns 32 pi .. 32 pi + 31 to the band)
+hipError_t syevd2_panels(int n, double* ws, const SyevdPlan& p, uint32_t* flags, uint32_t epoch, int pi0, int pi1,
+                         hipStream_t st) {
+  constexpr int B = 32;
+  double* Aw = ws + p.off_aw;
+  uint32_t* pflags = flags;        // 64 panel-QR flags
+  uint32_t* abortw = flags + 64;   // [0] panel QR, [1] stage 2
+  hipError_t e = hipSuccess;
   int64_t vxo = 0;
-  int pi = 0;
-  for (int c0 = 0; c0 < n - B - 1; c0 += B, ++pi) {
+  for (int r = 0; r < pi0; ++r) vxo += (int64_t)(n - r * B - B) * B;
+  pi1 = std::min(pi1, p.np);
+  for (int pi = pi0; pi < pi1; ++pi) {
+    const int c0 = pi * B;
     const int r0 = c0 + B, m = n - r0;
     double* Vx = ws + p.off_vx + vxo;
     double* T = ws + p.off_t + (int64_t)pi * B * B;
@@ -1413,81 +1423,112 @@ hipError_t launch_syevd2(const double* C, int n, int nvec, double* ws, const Sye
     if (e != hipSuccess) return e;
     vxo += (int64_t)m * B;
   }
+  return hipSuccess;
+}
+
+hipError_t syevd2_band(int n, double* ws, const SyevdPlan& p, bool keep_band0, hipStream_t st) {
+  constexpr int B = 32;
   double* band = ws + p.off_band;
-  double* band0 = ws + p.off_band0;
   const int64_t nb = (int64_t)n * 2 * B;
-  hipLaunchKernelGGL(sb::k_band<B>, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, Aw, (int64_t)n, n, band);
-  e = hipMemcpyAsync(band0, band, (size_t)nb * sizeof(double), hipMemcpyDeviceToDevice, st);
+  hipLaunchKernelGGL(sb::k_band<B>, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, ws + p.off_aw, (int64_t)n, n,
+                     band);
+  if (!keep_band0) return hipGetLastError();
+  return hipMemcpyAsync(ws + p.off_band0, band, (size_t)nb * sizeof(double), hipMemcpyDeviceToDevice, st);
+}
+
+int syevd2_groups(int n) { return n > 2 ? (n - 2 + 1) / 2 : 0; }  // sweep groups of two (GW = 2)
+
+// stage 2, sweep groups [q0, q1): one persistent launch; every group before q0 is done
+hipError_t syevd2_chase(int n, double* ws, const SyevdPlan& p, uint32_t* flags, int q0, int q1, hipStream_t st) {
+  constexpr int B = 32;
+  constexpr int GW = 2;
+  using SW = sb::SbWin<B, GW>;
+  q1 = std::min(q1, syevd2_groups(n));
+  if (q1 <= q0) return hipSuccess;
+  uint32_t* abortw = flags + 64;
+  uint32_t* prog = flags + 128;
+  int cus = 256, dev = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int P = std::max(1, std::min(q1 - q0, cus));
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sb::k_sbtrd_win<B, GW>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)SW::lds_bytes);
   if (e != hipSuccess) return e;
-  if (n > 2) {
-    constexpr int GW = 2;
-    using SW = sb::SbWin<B, GW>;
-    const int ngroups = (n - 2 + GW - 1) / GW;
-    int cus = 256, dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const int P = std::max(1, std::min(ngroups, cus));
-    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sb::k_sbtrd_win<B, GW>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)SW::lds_bytes);
+  e = check_persistent(reinterpret_cast<const void*>(&sb::k_sbtrd_win<B, GW>), SW::NT, SW::lds_bytes, P);
+  if (e != hipSuccess) return e;
+  // PODS_SBWIN_TRACE=q0: per-step timestamps of groups q0 .. q0+3 (diagnostics, stderr)
+  const char* wts = std::getenv("PODS_SBWIN_TRACE");
+  int64_t* wtr = nullptr;
+  const size_t wtn = 4 * 512 * 12;
+  if (wts) {
+    e = hipMallocAsync(reinterpret_cast<void**>(&wtr), wtn * sizeof(int64_t), st);
+    if (e == hipSuccess) e = hipMemsetAsync(wtr, 0, wtn * sizeof(int64_t), st);
     if (e != hipSuccess) return e;
-    e = check_persistent(reinterpret_cast<const void*>(&sb::k_sbtrd_win<B, GW>), SW::NT, SW::lds_bytes, P);
+  }
+  const int wq0 = wts ? std::atoi(wts) : 0;
+  hipLaunchKernelGGL((sb::k_sbtrd_win<B, GW>), dim3(P), dim3(SW::NT), SW::lds_bytes, st, ws + p.off_band, n, q0, q1,
+                     prog, abortw + 1, ws + p.off_end - 256LL * B * 2 * B, wtr, wq0);
+  if (wtr) {
+    std::vector<int64_t> h(wtn);
+    e = hipMemcpyAsync(h.data(), wtr, wtn * sizeof(int64_t), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFreeAsync(wtr, st);
     if (e != hipSuccess) return e;
-    // PODS_SBWIN_TRACE=q0: per-step timestamps of groups q0 .. q0+3 (diagnostics, stderr)
-    const char* wts = std::getenv("PODS_SBWIN_TRACE");
-    int64_t* wtr = nullptr;
-    const size_t wtn = 4 * 512 * 12;
-    if (wts) {
-      e = hipMallocAsync(reinterpret_cast<void**>(&wtr), wtn * sizeof(int64_t), st);
-      if (e == hipSuccess) e = hipMemsetAsync(wtr, 0, wtn * sizeof(int64_t), st);
-      if (e != hipSuccess) return e;
-    }
-    const int wq0 = wts ? std::atoi(wts) : 0;
-    hipLaunchKernelGGL((sb::k_sbtrd_win<B, GW>), dim3(P), dim3(SW::NT), SW::lds_bytes, st, band, n, ngroups, prog,
-                       abortw + 1, ws + p.off_end - 256LL * B * 2 * B, wtr, wq0);
-    if (wtr) {
-      std::vector<int64_t> h(wtn);
-      e = hipMemcpyAsync(h.data(), wtr, wtn * sizeof(int64_t), hipMemcpyDeviceToHost, st);
-      if (e == hipSuccess) e = hipStreamSynchronize(st);
-      (void)hipFreeAsync(wtr, st);
-      if (e != hipSuccess) return e;
-      for (int g = 0; g < 4; ++g) {
-        const int64_t* T = h.data() + (size_t)g * 512 * 12;
-        double a[6] = {0, 0, 0, 0, 0, 0};
-        int cnt = 0;
-        double ph[5] = {0, 0, 0, 0, 0};
-        int pc = 0;
-        for (int k = 0; k + 1 < 512 && T[(k + 1) * 12] != 0; ++k, ++cnt) {
-          const int64_t* R = T + k * 12;
-          a[0] += (R[1] - R[0]) * 0.01;           // loader: wait for the previous group
-          a[1] += (R[2] - R[1]) * 0.01;           // loader: wait for the writer's read
-          a[2] += (R[3] - R[2]) * 0.01;           // loader: DMA issue + landing
-          a[3] += (R[4] - R[0]) * 0.01;           // writer: store drain
-          a[4] += (R[5] - R[0]) * 0.01;           // task wave 0
-          a[5] += (T[(k + 1) * 12] - R[0]) * 0.01;  // step to step
-          if (R[6] != 0) {
-            ph[0] += (R[6] - R[0]) * 0.01;  // task start
-            for (int z = 1; z < 5; ++z) ph[z] += (R[6 + z] - R[5 + z]) * 0.01;
-            ++pc;
-          }
+    for (int g = 0; g < 4; ++g) {
+      const int64_t* T = h.data() + (size_t)g * 512 * 12;
+      double a[6] = {0, 0, 0, 0, 0, 0};
+      int cnt = 0;
+      double ph[5] = {0, 0, 0, 0, 0};
+      int pc = 0;
+      for (int k = 0; k + 1 < 512 && T[(k + 1) * 12] != 0; ++k, ++cnt) {
+        const int64_t* R = T + k * 12;
+        a[0] += (R[1] - R[0]) * 0.01;           // loader: wait for the previous group
+        a[1] += (R[2] - R[1]) * 0.01;           // loader: wait for the writer's read
+        a[2] += (R[3] - R[2]) * 0.01;           // loader: DMA issue + landing
+        a[3] += (R[4] - R[0]) * 0.01;           // writer: store drain
+        a[4] += (R[5] - R[0]) * 0.01;           // task wave 0
+        a[5] += (T[(k + 1) * 12] - R[0]) * 0.01;  // step to step
+        if (R[6] != 0) {
+          ph[0] += (R[6] - R[0]) * 0.01;  // task start
+          for (int z = 1; z < 5; ++z) ph[z] += (R[6 + z] - R[5 + z]) * 0.01;
+          ++pc;
         }
-        pc = std::max(pc, 1);
-        std::fprintf(stderr, "sbwin group %d task phases us: start %.2f loads %.2f reflector %.2f left %.2f right+w %.2f\n", wq0 + g,
-                     ph[0] / pc, ph[1] / pc, ph[2] / pc, ph[3] / pc, ph[4] / pc);
-        const double lag = g > 0 ? (T[0] - h[(size_t)(g - 1) * 512 * 12]) * 0.01 : 0.0;
-        cnt = std::max(cnt, 1);
-        std::fprintf(stderr,
-                     "sbwin group %d: %d steps, start lag %.2f us; per step us: avail %.2f wread %.2f dma %.2f "
-                     "drain %.2f task %.2f step %.2f\n",
-                     wq0 + g, cnt, lag, a[0] / cnt, a[1] / cnt, a[2] / cnt, a[3] / cnt, a[4] / cnt, a[5] / cnt);
       }
+      pc = std::max(pc, 1);
+      std::fprintf(stderr, "sbwin group %d task phases us: start %.2f loads %.2f reflector %.2f left %.2f right+w %.2f\n", wq0 + g,
+                   ph[0] / pc, ph[1] / pc, ph[2] / pc, ph[3] / pc, ph[4] / pc);
+      const double lag = g > 0 ? (T[0] - h[(size_t)(g - 1) * 512 * 12]) * 0.01 : 0.0;
+      cnt = std::max(cnt, 1);
+      std::fprintf(stderr,
+                   "sbwin group %d: %d steps, start lag %.2f us; per step us: avail %.2f wread %.2f dma %.2f "
+                   "drain %.2f task %.2f step %.2f\n",
+                   wq0 + g, cnt, lag, a[0] / cnt, a[1] / cnt, a[2] / cnt, a[3] / cnt, a[4] / cnt, a[5] / cnt);
     }
   }
+  return hipGetLastError();
+}
+
+// all n eigenvalues of the band's tridiagonal (descending)
+hipError_t syevd2_eigvals(int n, double* ws, const SyevdPlan& p, int* grid_cnt, double* lam_desc, hipStream_t st) {
+  constexpr int B = 32;
   double* D = ws + p.off_de;
   double* E = D + n;
   double* bounds = D + 2 * (int64_t)n;
-  hipLaunchKernelGGL(sb::k_tri_out<B>, dim3((n + 255) / 256), dim3(256), 0, st, band, n, D, E);
-  e = launch_tri_eigvals(D, E, n, bounds, lam_desc, grid_cnt, st, reinterpret_cast<double2*>(ws + p.off_deg));
+  hipLaunchKernelGGL(sb::k_tri_out<B>, dim3((n + 255) / 256), dim3(256), 0, st, ws + p.off_band, n, D, E);
+  return launch_tri_eigvals(D, E, n, bounds, lam_desc, grid_cnt, st, reinterpret_cast<double2*>(ws + p.off_deg));
+}
+
+hipError_t launch_syevd2(const double* C, int n, int nvec, double* ws, const SyevdPlan& p, uint32_t* flags,
+                         uint32_t epoch, int* ipiv, int* grid_cnt, double* lam_desc, double* vec, hipStream_t st) {
+  constexpr int B = 32;
+  hipError_t e = syevd2_begin(C, n, ws, p, flags, st);
+  if (e == hipSuccess) e = syevd2_panels(n, ws, p, flags, epoch, 0, p.np, st);
+  if (e == hipSuccess) e = syevd2_band(n, ws, p, nvec > 0, st);
+  if (e == hipSuccess) e = syevd2_chase(n, ws, p, flags, 0, syevd2_groups(n), st);
+  if (e == hipSuccess) e = syevd2_eigvals(n, ws, p, grid_cnt, lam_desc, st);
   if (e != hipSuccess || nvec <= 0) return e;
+  double* band0 = ws + p.off_band0;
+  double* bounds = ws + p.off_de + 2 * (int64_t)n;
   double* inv = ws + p.off_inv;
   hipLaunchKernelGGL(sb::k_band_invit<B>, dim3(nvec), dim3(256), 0, st, band0, n, lam_desc, inv, ipiv, vec, nvec);
   e = launch_orth(lam_desc, bounds, n, nvec, vec, nvec, st);

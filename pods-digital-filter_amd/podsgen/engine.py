@@ -384,8 +384,10 @@ class SpectrumQueue:
     LEAD_MS of their units while rank 0 solves (before the broadcast of its result, which
     waits for them) and the rest after their spatial modes.  drain() runs what
     is left (inside a caller's timed region); results() returns {step: eigenvalues} for the
-    steps this rank owned.  ns <= 4096; beyond that each owner solves its step at once
-    (pods_syev2, no vectors)."""
+    steps this rank owned.  4096 < ns <= 16384 (BASELINE configs 4 and 5): the same queue over
+    the two-stage solver's units (pods_eigvals_* run pods_syev2 without vectors as 32-panel
+    stage-1 groups, 1024-sweep chase ranges and the bisection: 17 units at ns = 8192), so the
+    spectrum spreads over ranks 1..N-1 instead of one owner solving a whole step at once."""
 
     # per-unit time (ms) of k_trd column ranges 0..7 and the bisection at ns = 4096
     # (profiles/r3/c3_kernel_stats.csv); used only to even out the per-step load
@@ -393,13 +395,35 @@ class SpectrumQueue:
     # rank 0's own extra work per step at ns = 4096 (leading pairs 5.0, DFT + ranking ~1 ms)
     LEAD_MS = 6.0
 
+    @staticmethod
+    def two_stage_costs(ns):
+        """Modelled per-unit cost (ms) of the two-stage units at ns > 4096 (r2/r3 profiles at
+        8192: a stage-1 panel 0.22 ms of panel QR + 0.47 (m/8192)^2 ms of updates; a chase
+        sweep group ~27 us behind the previous one plus one sweep's drain; bisection 5.2 ms x
+        (ns/8192)^2).  Only evens out the per-step load; correctness does not depend on it."""
+        B, PU, CU = 32, 32, 512
+        panels = [ns - c0 - B for c0 in range(0, ns - B - 1, B)]
+        cost = []
+        for u in range(0, len(panels), PU):
+            cost.append(sum(0.22 + 0.47 * (m / 8192.0) ** 2 for m in panels[u:u + PU]))
+        groups = (ns - 1) // 2
+        for q0 in range(0, groups, CU):
+            cost.append(0.027 * min(CU, groups - q0) + 0.65 * ns / 8192.0)
+        cost.append(5.2 * (ns / 8192.0) ** 2)
+        return cost
+
     def __init__(self, ctx, ns, rank=0, world=1, max_slots=16):
         self.ctx, self.ns, self.rank, self.world = ctx, ns, rank, world
-        self.units = (ns - 1) // 512 + 2
-        self.cost = (self.UNIT_MS if self.units == len(self.UNIT_MS)
-                     else [1.0] * self.units)
+        if ns > SYEV_MAX_N:
+            self.cost = self.two_stage_costs(ns)
+        else:
+            units = (ns - 1) // 512 + 2
+            self.cost = self.UNIT_MS if units == len(self.UNIT_MS) else [1.0] * units
+        self.units = len(self.cost)
         E = sum(self.cost)
-        lead = self.LEAD_MS * (ns / 4096.0) ** 2 * sum(self.cost) / sum(self.UNIT_MS)
+        lead = self.LEAD_MS * (ns / 4096.0) ** 2
+        if ns <= SYEV_MAX_N:
+            lead *= sum(self.cost) / sum(self.UNIT_MS)
         self.lead = lead
         if world == 1:
             self.budgets = [E]
@@ -477,18 +501,11 @@ class SpectrumQueue:
             self._reap()
             self.credit += self.budget
             if self.owner(s) == self.rank:
-                if self.ns > SYEV_MAX_N:
-                    lam_t = torch.empty(self.ns, dtype=torch.float64, device=C.device)
-                    check(lib.pods_syev2(self.ctx.h, ptr(C), self.ns, 0, ptr(lam_t), None), "pods_syev2")
-                    self._finish(s, lam_t, C, lambda w: check(lib.pods_syev2_flags_async(self.ctx.h, ptr(w)),
-                                                              "pods_syev2_flags_async"))
-                    self.credit = 0.0
-                else:
-                    slot = self._slot()
-                    check(lib.pods_eigvals_begin(self.ctx.h, slot, ptr(C), self.ns), "pods_eigvals_begin")
-                    lam = torch.empty(self.ns, dtype=torch.float64, device=C.device)
-                    self.pending.append([s, slot, 1, lam, C])
-                    self.credit -= self.cost[0]
+                slot = self._slot()
+                check(lib.pods_eigvals_begin(self.ctx.h, slot, ptr(C), self.ns), "pods_eigvals_begin")
+                lam = torch.empty(self.ns, dtype=torch.float64, device=C.device)
+                self.pending.append([s, slot, 1, lam, C])
+                self.credit -= self.cost[0]
             self._advance(limit=limit)
 
     def run(self, timer=None):

@@ -104,3 +104,56 @@ def test_syev2_structured(ctx, kind, n, nvec):
     check_against_eigh(C, lam, Y)
     if Y.shape[1]:
         assert np.max(np.abs(Y.T @ Y - np.eye(Y.shape[1]))) <= 1e-12
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("n", [4500, 8192])
+def test_eigvals_units_two_stage_equal_syev2(ctx, n):
+    """pods_eigvals_* beyond the on-chip limit: the two-stage solver without vectors in resumable
+    units (32-panel stage-1 groups, 512-group chase ranges, the bisection), advanced ONE unit
+    per call with unrelated work on the stream in between, gives pods_syev2's eigenvalues bit for
+    bit (same kernels, same order; the chase split over launches changes no arithmetic), and its
+    abort words read 0."""
+    import ctypes
+    C = pod_like(n, seed=3)
+    lam_ref, _ = solve2(ctx, C, 0)
+    lib = ctx.lib
+    slot = 2
+    podsgen.check(lib.pods_eigvals_begin(ctx.h, slot, E.ptr(C), n), "pods_eigvals_begin")
+    C2 = C.clone()
+    C.zero_()                        # begin copied C: later units must not read it
+    rem = ctypes.c_int(1)
+    units = 1
+    junk = torch.empty(1 << 20, dtype=torch.float64, device="cuda")
+    while rem.value:
+        junk.normal_()               # other work between units
+        podsgen.check(lib.pods_eigvals_advance(ctx.h, slot, 1, ctypes.byref(rem)), "pods_eigvals_advance")
+        units += 1
+    expect = E.SpectrumQueue.two_stage_costs(n)
+    assert units == len(expect), (units, len(expect))
+    lam = torch.empty(n, dtype=torch.float64, device="cuda")
+    podsgen.check(lib.pods_eigvals_fetch(ctx.h, slot, E.ptr(lam)), "pods_eigvals_fetch")
+    podsgen.check(lib.pods_eigvals_status(ctx.h, slot), "pods_eigvals_status")
+    assert np.array_equal(lam.cpu().numpy(), lam_ref)
+    lr = torch.flip(torch.linalg.eigvalsh(C2), (0,)).cpu().numpy()
+    assert np.max(np.abs(lam_ref - lr)) <= 1e-12 * lr[0]
+
+
+@pytest.mark.timeout(600)
+def test_spectrum_queue_two_stage_spreads_and_matches(ctx):
+    """SpectrumQueue at ns = 8192 (BASELINE config 4) from rank 1's view of a 3-rank run: its
+    owned steps' spectra run as two-stage units spread over the following steps and drained at
+    the end, each equal to pods_syev2's eigenvalues bit for bit."""
+    n = 8192
+    mats = [pod_like(n, seed=90 + i) for i in range(3)]
+    q = E.SpectrumQueue(ctx, n, rank=1, world=3)
+    for C in mats:
+        q.submit(C)
+    assert q.pending or q.finished
+    q.drain()
+    got = q.results()
+    owned = [s for s in range(len(mats)) if q.owner(s) == 1]
+    assert sorted(got) == owned and owned
+    for s in owned:
+        ref, _ = solve2(ctx, mats[s], 0)
+        assert np.array_equal(got[s], ref), s

@@ -376,26 +376,35 @@ def test_num_valid_modes_vectorised_matches_reference_loop():
                     assert num_valid_modes(e, ns, tol) == num_valid_modes_loop(e, ns, tol), (ns, tol, trial)
 
 
+@pytest.mark.parametrize("ns", [4096, 8192, 16384])
 @pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
-def test_spectrum_queue_ownership(world):
+def test_spectrum_queue_ownership(world, ns):
     """SpectrumQueue's owner sequence (host logic, no device): identical on every rank, shares
     of the spectra proportional to the per-step budgets, rank 0 (which carries the leading-pair
-    solve) owning less than the others and none at world 8 (C3 costs)."""
+    solve) owning less than the others and none at world 8 (C3 costs).  ns = 8192 / 16384
+    (BASELINE configs 4 / 5): the two-stage solver's units (17 / 33: stage-1 panel groups, chase
+    ranges, the bisection) are spread the same way -- no owner solves a whole step at once."""
     from podsgen import engine as E
 
     class _Ctx:
         lib = None
 
-    qs = [E.SpectrumQueue(_Ctx(), 4096, r, world) for r in range(world)]
+    qs = [E.SpectrumQueue(_Ctx(), ns, r, world) for r in range(world)]
     seq = [qs[0].owner(s) for s in range(400)]
     for q in qs[1:]:
         assert [q.owner(s) for s in range(400)] == seq
     b = qs[0].budgets
-    assert abs(sum(b) - sum(E.SpectrumQueue.UNIT_MS)) < 1e-9
+    if ns == 4096:
+        assert abs(sum(b) - sum(E.SpectrumQueue.UNIT_MS)) < 1e-9
+    else:
+        assert qs[0].units == {8192: 17, 16384: 33}[ns]
+        assert abs(sum(b) - sum(qs[0].cost)) < 1e-9
+        # the largest unit is a small share of one spectrum: units interleave with steps
+        assert max(qs[0].cost) < 0.2 * sum(qs[0].cost)
     counts = np.bincount(seq, minlength=world)
     for r in range(world):
         assert abs(counts[r] / 400 - b[r] / sum(b)) <= 0.01, (r, counts, b)
     if world > 1:
         assert b[0] < b[1]
-    if world == 8:
+    if world == 8 and ns == 4096:
         assert counts[0] == 0
