@@ -802,6 +802,10 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds_byte_addr) 
                                    16, 0, 0);
 }
 
+#ifndef PODS_SYRK_SETPRIO
+#define PODS_SYRK_SETPRIO 0  // s_setprio(1) around each K-tile's MFMA cluster (A/B switch)
+#endif
+
 // Split-K SYRK: one 128 x 128 tile of the lower triangle per 256-thread workgroup, TWO
 // workgroups per CU.  Operands are streamed by LDS-DMA (global_load_lds_dwordx4) into a
 // 2-stage ring (66.5 KB per workgroup); counted vmcnt + raw s_barrier keep the next K-tile in
@@ -904,6 +908,9 @@ __global__ __launch_bounds__(256, OCC) void k_syrk_g128(const double* __restrict
     __builtin_amdgcn_sched_barrier(0);
     if (t + NST - 1 < nt) issue(t + NST - 1);
     const char* st = smem + (t % NST) * STAGE;
+#if PODS_SYRK_SETPRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
     const double* Xs = reinterpret_cast<const double*>(st);
     const double* Ys = reinterpret_cast<const double*>(st + XB);
     const double* Ms = reinterpret_cast<const double*>(st + XB + YB + wave * KT * 8);
@@ -923,6 +930,9 @@ __global__ __launch_bounds__(256, OCC) void k_syrk_g128(const double* __restrict
         for (int n = 0; n < 4; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], bv[n], acc[m][n], 0, 0, 0);
     }
+#if PODS_SYRK_SETPRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
   }
   double* dst = work + (int64_t)sp * slab;
 #pragma unroll
@@ -1347,7 +1357,12 @@ hipError_t launch_center(double* AT, int64_t rowpad, int ns, const double* mean,
 // instead of 16) 50.7 vs 48.8 ms, K-tile 8 / 3 stages / three workgroups per CU 49.5 ms,
 // K-tile 8 / 3 stages / two per CU 49.8 ms -- the shorter K-tiles' extra barriers cost more
 // than the deeper prefetch gains.
-constexpr int SYRK_KT = 16, SYRK_NST = 2, SYRK_OCC = 2;
+#ifndef PODS_SYRK_KT  // compile-time overrides for A/B builds (tools/lib_variants.sh)
+#define PODS_SYRK_KT 16
+#define PODS_SYRK_NST 2
+#define PODS_SYRK_OCC 2
+#endif
+constexpr int SYRK_KT = PODS_SYRK_KT, SYRK_NST = PODS_SYRK_NST, SYRK_OCC = PODS_SYRK_OCC;
 
 int syrk_plan(int ns, int64_t Kdim, int64_t* ksplit) {
   constexpr int KT = 16;
