@@ -20,6 +20,8 @@ def run(name, reps):
     if r.returncode != 0:
         print(name, "FAILED", r.stderr[-2000:], flush=True)
         sys.exit(1)
+    chk = re.findall(r"check max rel err (\S+) symmetric (\S+)", r.stdout)
+    print(name, "check", chk, flush=True)
     return [float(m) for m in re.findall(r"corr ([0-9.]+) ms", r.stdout)][2:]
 
 

@@ -23,3 +23,16 @@ for r in range(reps):
     podsgen.check(ctx.lib.pods_corr(ctx.h, E.ptr(C), 1))
     torch.cuda.synchronize(); dt = time.time() - t
     print("corr %.2f ms  %.1f TFLOP/s (triangle flops)" % (dt * 1e3, flops / dt / 1e12), flush=True)
+# correctness of the last C: sampled 256 x 256 tiles against torch's A_c^T A_c / ns
+import ctypes
+def _blk(i0, i1):
+    out = torch.empty((i1 - i0, gen.rowlen), dtype=torch.float64, device="cuda")
+    podsgen.check(ctx.lib.pods_copy_snapshots(ctx.h, i0, i1, ctypes.c_void_p(out.data_ptr())), "copy")
+    return out
+cm = float(C.abs().max())
+worst = 0.0
+for bi, bj in [(0, 0), (NS // 256 - 1, 0), (NS // 512, NS // 1024)]:
+    X, Y = _blk(bi * 256, bi * 256 + 256), _blk(bj * 256, bj * 256 + 256)
+    ref = X @ Y.T / NS
+    worst = max(worst, float((C[bi * 256:bi * 256 + 256, bj * 256:bj * 256 + 256] - ref).abs().max()) / cm)
+print("check max rel err %.3e symmetric %s" % (worst, bool(torch.equal(C, C.T))), flush=True)
