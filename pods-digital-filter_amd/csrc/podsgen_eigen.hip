@@ -32,9 +32,7 @@ namespace pods {
 namespace eig {
 
 constexpr int TT = 512;  // k_trd workgroup: 8 waves
-#ifndef PODS_TRD_SKIP_MIN_K
-#define PODS_TRD_SKIP_MIN_K 0  // first column range whose dead slot-K storage is skipped
-#endif
+
 
 // ---- cross-CU hand-off primitives (MI355X_MICROARCH.md "Valid forms": sc1 payload stores,
 // ---- drained, one sc1 flag per workgroup; sc1 poll; sc1 payload loads) ------------------
@@ -431,35 +429,29 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
     // publish, where it overlaps the next column's hop.  (Updating them here mixed stores
     // into the loads, and a pending store makes every load wait a full vmcnt drain: one L2
     // round trip per row group on the critical path.)
-    // Dead storage is skipped, exactly: slot K of this wave holds columns 512K + 64 wv .. + 63,
-    // all below j once 512K + 64 wv + 63 < j -- x (v_j) is zero there and the pending update's
-    // multipliers (v_{j-1}, w_{j-1}) too, so neither the symv nor the update reads or writes
-    // them (range 0: the L2 slab slot; ranges 1-3: an LDS slot).  The test is wave-uniform.
-    const bool kalive = K < PODS_TRD_SKIP_MIN_K || TT * K + 64 * __builtin_amdgcn_readfirstlane(t >> 6) + 63 >= j;
+    // (Skipping the dead part of slot K -- this wave's columns 512K + 64 wv .. + 63 once all are
+    // below j, exact since x and the pending update's multipliers are zero there -- was
+    // bit-identical and slower, r4: the wave-uniform branches raised range 0's spills 47 -> 83
+    // VGPRs and pods_syev 36.8 -> 39.9 ms; ranges 1-7 only: 37.0 ms.)
     // slab loads run SPF row groups ahead
     constexpr int SPF = K == 0 ? 0 : 3;  // range 0: no registers to spare (depth 2 measured no faster)
     double slab[SG > 0 ? RL : 1][SG > 0 ? SG : 1];
-    if (kalive) {
 #pragma unroll
-      for (int ii = 0; ii < (SG > 0 ? SPF * RH : 0); ++ii)
+    for (int ii = 0; ii < (SG > 0 ? SPF * RH : 0); ++ii)
 #pragma unroll
-        for (int m = K; m < K + SG; ++m) slab[ii][m - K] = wm(m, I0 + ii, t);
-    }
+      for (int m = K; m < K + SG; ++m) slab[ii][m - K] = wm(m, I0 + ii, t);
 #pragma unroll
     for (int h = 0; h < RL / RH; ++h) {
-      if (kalive) {
 #pragma unroll
-        for (int ii = (h + SPF) * RH; ii < (SG > 0 ? (h + SPF + 1) * RH : 0); ++ii)
-          if (ii < RL)
+      for (int ii = (h + SPF) * RH; ii < (SG > 0 ? (h + SPF + 1) * RH : 0); ++ii)
+        if (ii < RL)
 #pragma unroll
-            for (int m = K; m < K + SG; ++m) slab[ii][m - K] = wm(m, I0 + ii, t);
-      }
+          for (int m = K; m < K + SG; ++m) slab[ii][m - K] = wm(m, I0 + ii, t);
       double acc[RH], colv[RH];
 #pragma unroll
       for (int q = 0; q < RH; ++q) acc[q] = 0.0;
 #pragma unroll
       for (int m = K; m < S; ++m) {
-        if (m == K && !kalive) continue;
 #pragma unroll
         for (int q = 0; q < RH; ++q) {
           const int ii = h * RH + q;
@@ -532,7 +524,6 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
       }
 #pragma unroll
       for (int m = K; m < S; ++m) {
-        if (m == K && !kalive) continue;
 #pragma unroll
         for (int q = 0; q < RH; ++q) {
           const int ii = h * RH + q;

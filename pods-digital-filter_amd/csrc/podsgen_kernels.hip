@@ -802,12 +802,6 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds_byte_addr) 
                                    16, 0, 0);
 }
 
-#ifndef PODS_SYRK_SETPRIO
-#define PODS_SYRK_SETPRIO 0  // s_setprio(1) around each K-tile's MFMA cluster (A/B switch)
-#endif
-#ifndef PODS_SYRK_PRIV
-#define PODS_SYRK_PRIV 0  // > 0: the wave-private k_syrk_w with that many ring stages (A/B switch)
-#endif
 
 // Split-K SYRK: one 128 x 128 tile of the lower triangle per 256-thread workgroup, TWO
 // workgroups per CU.  Operands are streamed by LDS-DMA (global_load_lds_dwordx4) into a
@@ -911,9 +905,6 @@ __global__ __launch_bounds__(256, OCC) void k_syrk_g128(const double* __restrict
     __builtin_amdgcn_sched_barrier(0);
     if (t + NST - 1 < nt) issue(t + NST - 1);
     const char* st = smem + (t % NST) * STAGE;
-#if PODS_SYRK_SETPRIO
-    __builtin_amdgcn_s_setprio(1);
-#endif
     const double* Xs = reinterpret_cast<const double*>(st);
     const double* Ys = reinterpret_cast<const double*>(st + XB);
     const double* Ms = reinterpret_cast<const double*>(st + XB + YB + wave * KT * 8);
@@ -927,108 +918,6 @@ __global__ __launch_bounds__(256, OCC) void k_syrk_g128(const double* __restrict
       for (int m = 0; m < 4; ++m) a[m] = CENTRED ? Xs[xrow + koff + m * 16 * KT] : Xs[xrow + koff + m * 16 * KT] - mk;
 #pragma unroll
       for (int n = 0; n < 4; ++n) bv[n] = CENTRED ? Ys[yrow + koff + n * 16 * KT] : Ys[yrow + koff + n * 16 * KT] - mk;
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], bv[n], acc[m][n], 0, 0, 0);
-    }
-#if PODS_SYRK_SETPRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
-  }
-  double* dst = work + (int64_t)sp * slab;
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int gi = i0 + wr * 64 + m * 16 + fk + 4 * reg;
-        const int gj = j0 + wc * 64 + n * 16 + fr;
-        if (gi < ns && gj <= gi) dst[(int64_t)gi * ldc + gj] = acc[m][n][reg];
-      }
-}
-
-// k_syrk_w<KT, NST>: the same 128 x 128 split-K tile (centred A) with NO workgroup barrier.
-// Every wave LDS-DMAs its OWN operands -- the 64 X rows and 64 Y rows of its 64 x 64 block --
-// into a private NST-stage ring and waits only on its own counted vmcnt (an LDS-DMA is ordered
-// for the issuing wave's ds_reads by that wave's covering vmcnt alone, MI355X_MICROARCH.md
-// item 7).  Two waves share each X / Y slice, so the L2 -> LDS traffic doubles; in exchange a
-// wave never idles on a sibling's barrier skew (the r3 kernel's pipe sat 12 % idle at the
-// per-K-tile vmcnt(0) + barrier).  Same row layout and XOR swizzle as SyrkCfg<KT>; the stage
-// of tile t is overwritten by tile t + NST - 1 only after this wave's MFMAs consumed it.
-template <int KT, int NST>
-__global__ __launch_bounds__(256, 2) void k_syrk_w(const double* __restrict__ AT, int ns, int64_t Kdim,
-                                                    const int4* __restrict__ items, int nitems, int64_t ksplit,
-                                                    double* __restrict__ work, int64_t ldc, int64_t slab) {
-  using Cf = SyrkCfg<KT, NST>;
-  constexpr int SLOTS = Cf::SLOTS, RPI = Cf::RPI, SWZ = Cf::SWZ, RSH = Cf::RSH;
-  constexpr int SLICE = 64 * KT * 8;  // one wave's X (or Y) rows per stage
-  constexpr int P = SLICE / 1024;     // 1 KB LDS-DMA instructions per slice
-  constexpr int WSTAGE = 2 * SLICE;
-  constexpr int Q = 2 * P;            // DMA instructions per wave per K-tile
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  const int b = blockIdx.x;
-  const int xcd = b & 7, qq = nitems >> 3, rr = nitems & 7;
-  const int logical = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
-  const int4 it = items[logical];
-  const int bi = it.x, bj = it.y, sp = it.z;
-  const int i0 = bi * 128, j0 = bj * 128;
-  const int64_t kt0 = (int64_t)sp * (ksplit / KT);
-  const int64_t kt1 = min(Kdim, (int64_t)(sp + 1) * ksplit) / KT;
-  const int nt = (int)(kt1 - kt0);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wr = wave >> 1, wc = wave & 1;
-  const uint32_t wl0 = (uint32_t)(uintptr_t)smem + (uint32_t)(wave * NST * WSTAGE);
-  const int lrow = lane / SLOTS, lslot = lane % SLOTS;
-  int64_t xsrc[P], ysrc[P];
-#pragma unroll
-  for (int q = 0; q < P; ++q) {
-    const int R = q * RPI + lrow;  // row of this wave's 64-row slice
-    const int sw = (lslot ^ ((R >> RSH) & SWZ)) << 1;
-    xsrc[q] = ((int64_t)min(i0 + wr * 64 + R, ns - 1) << 4) + sw;
-    ysrc[q] = ((int64_t)min(j0 + wc * 64 + R, ns - 1) << 4) + sw;
-  }
-  const int64_t blk = (int64_t)ns << 4;
-  auto issue = [&](int t) {
-    const int64_t kt = kt0 + t;
-    const uint32_t base = wl0 + (uint32_t)((t % NST) * WSTAGE);
-    const double* g = AT + ((kt * KT) >> 4) * blk + ((kt * KT) & 15);
-#pragma unroll
-    for (int q = 0; q < P; ++q) glds16(g + xsrc[q], base + q * 1024);
-#pragma unroll
-    for (int q = 0; q < P; ++q) glds16(g + ysrc[q], base + SLICE + q * 1024);
-  };
-  f64x4 acc[4][4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = (f64x4){0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int t = 0; t < NST - 1; ++t)
-    if (t < nt) issue(t);
-  const int fr = lane & 15, fk = lane >> 4, fs = (fr >> RSH) & SWZ;
-  const int row = fr * KT;
-  for (int t = 0; t < nt; ++t) {
-    // this wave's DMAs of tile t landed (tiles t+1 .. t+NST-2 may still fly); the stage tile
-    // t+NST-1 overwrites was read by this wave's MFMAs of tile t-1, already retired
-    if (t + NST - 2 < nt) wait_vmcnt<Q * (NST - 2)>();
-    else wait_vmcnt<0>();
-    __builtin_amdgcn_sched_barrier(0);
-    if (t + NST - 1 < nt) issue(t + NST - 1);
-    const char* st = smem + wave * NST * WSTAGE + (t % NST) * WSTAGE;
-    const double* Xs = reinterpret_cast<const double*>(st);
-    const double* Ys = reinterpret_cast<const double*>(st + SLICE);
-#pragma unroll
-    for (int kk = 0; kk < KT; kk += 4) {
-      const int k = kk + fk;
-      const int koff = ((((k >> 1) ^ fs)) << 1) + (k & 1);
-      double a[4], bv[4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) a[m] = Xs[row + koff + m * 16 * KT];
-#pragma unroll
-      for (int n = 0; n < 4; ++n) bv[n] = Ys[row + koff + n * 16 * KT];
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -1458,7 +1347,11 @@ hipError_t launch_center(double* AT, int64_t rowpad, int ns, const double* mean,
 // it (r3, tools/syrk_probe.py, same data): K-tile 8 with a 4-stage ring (prefetch distance 24
 // instead of 16) 50.7 vs 48.8 ms, K-tile 8 / 3 stages / three workgroups per CU 49.5 ms,
 // K-tile 8 / 3 stages / two per CU 49.8 ms -- the shorter K-tiles' extra barriers cost more
-// than the deeper prefetch gains.
+// than the deeper prefetch gains.  r4 (tools/syrk_ab.py, one call, 12 runs each): s_setprio(1)
+// around each K-tile's MFMA cluster 49.28 vs 48.84 ms; no workgroup barrier at all -- every wave
+// LDS-DMAs its own 64 X and 64 Y rows into a private ring (K-tile 8) and waits on its own
+// vmcnt only -- 50.13 ms with 2 stages (two workgroups per CU; the L2 -> LDS traffic doubles)
+// and 58.28 ms with 3 (one workgroup per CU).
 #ifndef PODS_SYRK_KT  // compile-time overrides for A/B builds (tools/lib_variants.sh)
 #define PODS_SYRK_KT 16
 #define PODS_SYRK_NST 2
@@ -1503,22 +1396,6 @@ hipError_t launch_syrk(const double* AT, int ns, int64_t Kdim, const double* mea
     return hipGetLastError();
   };
   constexpr int lds = SYRK_NST * SyrkCfg<SYRK_KT, SYRK_NST>::STAGE;
-#if PODS_SYRK_PRIV
-  // the wave-private ring (k_syrk_w): 4 waves x NST stages x 2 slices of 64 rows x 8 k
-  constexpr int ldsw = 4 * PODS_SYRK_PRIV * 2 * 64 * 8 * 8;
-  if (centred) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_syrk_w<8, PODS_SYRK_PRIV>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, ldsw);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_syrk_w<8, PODS_SYRK_PRIV>), dim3(nitems), dim3(256), ldsw, st, AT, ns, Kdim,
-                       reinterpret_cast<const int4*>(items), nitems, ksplit, work, ldc, slab);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_syrk_reduce, dim3(((ns + 63) / 64) * ((ns + 63) / 64 + 1) / 2), dim3(256), 0, st, work,
-                       nsplit, slab, ns, ldc, C, divide);
-    return hipGetLastError();
-  }
-#endif
   hipError_t le = centred ? launch(k_syrk_g128<1, SYRK_KT, SYRK_NST, SYRK_OCC>, lds)
                           : launch(k_syrk_g128<0, SYRK_KT, SYRK_NST, SYRK_OCC>, lds);
   if (le != hipSuccess) return le;
