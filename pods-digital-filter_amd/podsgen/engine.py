@@ -395,6 +395,11 @@ class SpectrumQueue:
     # rank 0's own extra work per step at ns = 4096 (leading pairs 5.0, DFT + ranking ~1 ms)
     LEAD_MS = 6.0
 
+    # measured per-unit times (ms) of the two-stage units (profiles/r4/eigvals_units.jsonl,
+    # tools/eigvals_units_probe.py): 204 ms per spectrum at 8192, 626 ms at 16384
+    UNIT_MS_TWO = {8192: [19.4, 16.2, 13.4, 11.1, 9.3, 8.1, 6.8, 5.9, 13.9, 13.8, 13.7, 13.6, 13.4, 13.3, 13.2, 12.6, 6.2],
+                   16384: [53.1, 47.1, 42.9, 38.1, 34.1, 30.1, 26.4, 22.7, 19.3, 16.4, 13.4, 11.1, 9.2, 7.9, 6.6, 5.7, 14.4, 14.4, 14.3, 14.2, 14.1, 14.1, 14.0, 13.9, 13.8, 13.7, 13.6, 13.5, 13.5, 13.4, 13.3, 12.6, 21.4]}
+
     @staticmethod
     def two_stage_costs(ns):
         """Modelled per-unit cost (ms) of the two-stage units at ns > 4096 (r2/r3 profiles at
@@ -415,7 +420,7 @@ class SpectrumQueue:
     def __init__(self, ctx, ns, rank=0, world=1, max_slots=16):
         self.ctx, self.ns, self.rank, self.world = ctx, ns, rank, world
         if ns > SYEV_MAX_N:
-            self.cost = self.two_stage_costs(ns)
+            self.cost = list(self.UNIT_MS_TWO.get(ns) or self.two_stage_costs(ns))
         else:
             units = (ns - 1) // 512 + 2
             self.cost = self.UNIT_MS if units == len(self.UNIT_MS) else [1.0] * units
