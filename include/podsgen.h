@@ -148,6 +148,17 @@ int pods_set_mean(pods_ctx* ctx, const double* mean_host);
  * full symmetric.  divide = 1 divides by ns (single device); multi-device callers pass 0,
  * all-reduce the partials, then call pods_divide_inplace(C, ns*ns, ns). */
 int pods_corr(pods_ctx* ctx, double* C_dev, int divide);
+/* How pods_corr forms the products (replaces numpy's BLAS dgemm behind np.dot, PODFS.py:1455):
+ *   1 (default) exact integer products on the int8 matrix cores: A - m scaled by one power of
+ *     two to integers of <= 53 bits (2^-53 of max |A - m| is the only input rounding), their
+ *     residues modulo 16 coprime moduli <= 255, one int8 SYRK per modulus, the exact 125-bit
+ *     integer C' rebuilt by the Chinese remainder theorem and rounded to double once.  Needs
+ *     16 bytes per element of residue workspace (in K chunks of PODS_CORR_BUDGET_GB, default 16)
+ *     and no pods_center (the mean is subtracted while forming the residues);
+ *   0 the fp64 MFMA SYRK (v_mfma_f64_16x16x4), rounding at every accumulation.
+ * PODS_CORR=f64 in the environment selects 0 when the context is created. */
+int pods_set_corr_mode(pods_ctx* ctx, int mode);
+int pods_get_corr_mode(pods_ctx* ctx, int* mode);
 /* x[i] = x[i] / divisor for n doubles on the device. */
 int pods_divide_inplace(pods_ctx* ctx, double* x_dev, int64_t n, double divisor);
 /* The multi-device all-reduce of the partial correlations (PODFS.py:1455 summed over row slabs)

@@ -278,6 +278,14 @@ struct pods_ctx {
   bool marker_recorded = false;
   // pods_set_shared_device: the per-device lock file persistent launches hold (-1: not shared)
   int lock_fd = -1;
+  // pods_corr: 1 = exact int8-MFMA modular products + CRT (podsgen_corr_i8.hip), 0 = fp64 MFMA
+  // SYRK; PODS_CORR=f64 selects 0 at pods_create
+  int corr_mode = 1;
+  DevBuf devmax;           // max |fl(a - mean)| (k_mean / k_absdev), the int8 path's scale
+  bool dev_valid = false;  // devmax belongs to the current snapshots and mean
+  DevBuf i8_res, i8_part, i8_items;
+  int64_t i8_key = -1;
+  pods::CorrI8Plan i8_plan{};
 };
 
 namespace {
@@ -427,6 +435,7 @@ int pods_create(pods_ctx** out, int device) {
   PODS_HIP(hipSetDevice(device));
   pods_ctx* c = new pods_ctx();
   c->device = device;
+  if (const char* cm = std::getenv("PODS_CORR")) c->corr_mode = std::string(cm) == "f64" ? 0 : 1;
   *out = c;
   return PODS_OK;
   PODS_CATCH
@@ -451,6 +460,7 @@ int pods_destroy(pods_ctx* c) {
   for (EigvalSlot& sl : c->eslots)
     for (DevBuf* b : {&sl.wm, &sl.x, &sl.flags, &sl.det, &sl.v, &sl.cnt, &sl.lam, &sl.ws2}) release(*b);
   release(c->inv_lam);
+  for (DevBuf* b : {&c->devmax, &c->i8_res, &c->i8_part, &c->i8_items}) release(*b);
   if (c->pin) {
     for (int i = 0; i < pods_ctx::kStageSlots; ++i)
       if (c->pin_ev[i]) (void)hipEventDestroy(c->pin_ev[i]);
@@ -584,6 +594,7 @@ int pods_df_configure(pods_ctx* c, const pods_df_params* prm, const double* bx, 
   c->configured = true;
   c->have_snapshots = false;
   c->mean_valid = false;
+  c->dev_valid = false;
   c->centered = false;
   return PODS_OK;
   PODS_CATCH
@@ -622,6 +633,7 @@ int pods_df_generate_parts(pods_ctx* c, int parts) {
                                     c->A.as<double>(), c->stream));
     c->have_snapshots = true;
     c->mean_valid = false;
+    c->dev_valid = false;
     c->centered = false;
   }
   return PODS_OK;
@@ -664,6 +676,7 @@ int pods_set_snapshots(pods_ctx* c, const double* at, int ns, int64_t rowlen) {
   c->configured = false;
   c->have_snapshots = true;
   c->mean_valid = false;
+  c->dev_valid = false;
   c->centered = false;
   return PODS_OK;
   PODS_CATCH
@@ -687,9 +700,11 @@ int pods_mean(pods_ctx* c, double* mean_out, int out_is_device) {
   if (int e = check_ctx(c)) return e;
   if (!c->have_snapshots) return fail(PODS_ERR_STATE, "pods_mean before snapshots exist");
   PODS_HIP(hipSetDevice(c->device));
+  PODS_HIP(ensure(c->devmax, sizeof(double)));
   PODS_HIP(pods::launch_mean(c->A.as<double>(), c->rowlen, c->p.ns, c->prog_mean.as<int>(),
-                             c->nprog_mean, c->mean.as<double>(), c->stream));
+                             c->nprog_mean, c->mean.as<double>(), c->stream, c->devmax.as<double>()));
   c->mean_valid = true;
+  c->dev_valid = true;
   if (mean_out) {
     const size_t bytes = (size_t)c->rowlen * sizeof(double);
     if (out_is_device) {
@@ -709,8 +724,36 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
   if (!c->have_snapshots || !c->mean_valid) return fail(PODS_ERR_STATE, "pods_corr needs pods_mean first");
   if (!C_dev) return fail(PODS_ERR_ARG, "C_dev is null");
   PODS_HIP(hipSetDevice(c->device));
-  int64_t ksplit = 0;
   const int ns = c->p.ns;
+  const double* mean = c->centered ? c->zero.as<double>() : c->mean.as<double>();
+  if (c->corr_mode == 1) {
+    const char* bud = std::getenv("PODS_CORR_BUDGET_GB");
+    const int64_t budget = (int64_t)((bud ? std::atof(bud) : 16.0) * (double)(1LL << 30));
+    const char* fsp = std::getenv("PODS_CORR_SPLITS");  // tests: a fixed number of K splits
+    const int force = fsp ? std::max(0, std::atoi(fsp)) : 0;
+    const int64_t key = ((int64_t)ns << 40) ^ (c->rowpad << 4) ^ (budget >> 20) ^ ((int64_t)force << 58);
+    if (c->i8_key != key) {
+      if (pods::corr_i8_plan(ns, c->rowlen, c->rowpad, budget, &c->i8_plan, force) != 0)
+        return fail(PODS_ERR_UNSUPPORTED, "pods_corr: K too large for the int8 correlation (PODS_CORR=f64)");
+      const std::vector<int> items = pods::corr_i8_items(ns, c->i8_plan);
+      PODS_HIP(ensure(c->i8_items, items.size() * sizeof(int)));
+      PODS_HIP(hipMemcpy(c->i8_items.p, items.data(), items.size() * sizeof(int), hipMemcpyHostToDevice));
+      c->i8_key = key;
+    }
+    PODS_HIP(ensure(c->i8_res, (size_t)c->i8_plan.r_bytes));
+    PODS_HIP(ensure(c->i8_part, (size_t)c->i8_plan.p_bytes));
+    PODS_HIP(ensure(c->devmax, sizeof(double)));
+    if (!c->dev_valid) {
+      PODS_HIP(pods::launch_absdev(c->A.as<double>(), ns, c->rowlen, c->rowpad, mean, c->devmax.as<double>(),
+                                   c->stream));
+      c->dev_valid = true;
+    }
+    PODS_HIP(pods::launch_corr_i8(c->A.as<double>(), ns, c->rowlen, c->rowpad, mean, c->devmax.as<double>(),
+                                  c->i8_plan, c->i8_items.as<int>(), c->i8_res.as<int8_t>(),
+                                  c->i8_part.as<uint8_t>(), C_dev, ns, divide, c->stream));
+    return PODS_OK;
+  }
+  int64_t ksplit = 0;
   const int nsplit = pods::syrk_plan(ns, c->rowpad, &ksplit);
   PODS_HIP(ensure(c->cwork, (size_t)nsplit * ns * ns * sizeof(double)));
   const int64_t key = ((int64_t)ns << 20) | nsplit;
@@ -721,12 +764,24 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
     c->nitems = (int)items.size() / 4;
     c->items_key = key;
   }
-  PODS_HIP(pods::launch_syrk(c->A.as<double>(), ns, c->rowpad,
-                             c->centered ? c->zero.as<double>() : c->mean.as<double>(),
-                             c->items.as<int>(), c->nitems, nsplit, ksplit, C_dev, ns, divide,
-                             c->cwork.as<double>(), c->centered ? 1 : 0, c->stream));
+  PODS_HIP(pods::launch_syrk(c->A.as<double>(), ns, c->rowpad, mean, c->items.as<int>(), c->nitems, nsplit,
+                             ksplit, C_dev, ns, divide, c->cwork.as<double>(), c->centered ? 1 : 0, c->stream));
   return PODS_OK;
   PODS_CATCH
+}
+
+int pods_set_corr_mode(pods_ctx* c, int mode) {
+  if (int e = check_ctx(c)) return e;
+  if (mode != 0 && mode != 1) return fail(PODS_ERR_ARG, "corr mode must be 0 (fp64) or 1 (int8 CRT)");
+  c->corr_mode = mode;
+  return PODS_OK;
+}
+
+int pods_get_corr_mode(pods_ctx* c, int* mode) {
+  if (int e = check_ctx(c)) return e;
+  if (!mode) return fail(PODS_ERR_ARG, "mode is null");
+  *mode = c->corr_mode;
+  return PODS_OK;
 }
 
 int pods_center(pods_ctx* c) {
@@ -755,6 +810,7 @@ int pods_set_mean(pods_ctx* c, const double* mean_host) {
     PODS_HIP(hipStreamSynchronize(c->stream));
   }
   c->mean_valid = true;
+  c->dev_valid = false;
   c->centered = false;  // an explicit mean is subtracted by the consumers again
   return PODS_OK;
   PODS_CATCH

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 namespace pods {
 
@@ -34,8 +35,29 @@ hipError_t launch_filter_yz(int NY, const double* T1, const double* by, const do
 int filter_yz_max_K(int Kp);
 hipError_t launch_lund_apply(double* yu, double* yv, double* yw, int64_t P, const double* lund,
                              int lund_mode, const double* rot, int rotate, hipStream_t st);
+// devmax (nullable): also max |fl(a - mean)| over the matrix, as a double (zeroed here)
 hipError_t launch_mean(const double* AT, int64_t rowlen, int ns, const int* prog, int nprog,
-                       double* mean, hipStream_t st);
+                       double* mean, hipStream_t st, double* devmax = nullptr);
+// The correlation by exact int8-MFMA modular products + CRT (podsgen_corr_i8.hip).
+struct CorrI8Plan {
+  int bbits;       // scaled elements are integers with |a'| <= 2^bbits
+  int nlaunch;     // residue + SYRK launches (K chunks of the residue buffer)
+  int nsplit;      // K splits per launch
+  int kcs;         // 64-row K chunks per split
+  int64_t chunks;  // K chunks per launch (nsplit * kcs)
+  int64_t nkc;     // K chunks of the matrix
+  int nitems;      // work items per modulus per launch
+  int64_t r_bytes; // residue buffer
+  int64_t p_bytes; // per-modulus partial buffer
+};
+int corr_i8_nmod();
+int corr_i8_plan(int ns, int64_t rowlen, int64_t rowpad, int64_t budget_bytes, CorrI8Plan* out, int force_split = 0);
+std::vector<int> corr_i8_items(int ns, const CorrI8Plan& p);
+hipError_t launch_absdev(const double* AT, int ns, int64_t rowlen, int64_t rowpad, const double* mean,
+                         double* devmax, hipStream_t st);
+hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowpad, const double* mean,
+                          const double* devmax, const CorrI8Plan& p, const int* items, int8_t* R, uint8_t* P,
+                          double* C, int64_t ldc, int divide, hipStream_t st);
 // Split-K SYRK (k_syrk_g128 + k_syrk_reduce).  Plan: returns the number of K splits (work
 // slabs of ns*ns doubles).
 int syrk_plan(int ns, int64_t Kdim, int64_t* ksplit);

@@ -736,44 +736,67 @@ hipError_t launch_lund_apply(double* yu, double* yv, double* yw, int64_t P, cons
 // -----------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_mean(const double* __restrict__ AT, int64_t rowlen,
                                               int ns, const int* __restrict__ prog, int nprog,
-                                              double* __restrict__ mean) {
+                                              double* __restrict__ mean,
+                                              unsigned long long* __restrict__ devmax) {
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (r >= rowlen) return;
-  double stk[40];
-  int sp = 0;
-  for (int op = 0; op < nprog; ++op) {
-    const int s = prog[2 * op], n = prog[2 * op + 1];
-    if (s < 0) {
-      const double bsum = stk[--sp];
-      stk[sp - 1] = stk[sp - 1] + bsum;
-      continue;
-    }
-    const double* a = AT + at_off(r, s, ns);  // consecutive snapshots are 16 doubles apart
-    double res;
-    if (n < 8) {
-      res = 0.0;
-      for (int i = 0; i < n; ++i) res = res + a[(int64_t)i * 16];
-    } else {
-      double r0 = a[0], r1 = a[16], r2 = a[32], r3 = a[48];
-      double r4 = a[64], r5 = a[80], r6 = a[96], r7 = a[112];
-      int i = 8;
-      for (; i < n - (n % 8); i += 8) {
-        const double* b = a + (int64_t)i * 16;
-        r0 = r0 + b[0];
-        r1 = r1 + b[16];
-        r2 = r2 + b[32];
-        r3 = r3 + b[48];
-        r4 = r4 + b[64];
-        r5 = r5 + b[80];
-        r6 = r6 + b[96];
-        r7 = r7 + b[112];
+  const bool valid = r < rowlen;
+  // devmax: the largest |fl(a - mean)| (the int8 correlation's scale, podsgen_corr_i8.hip) from
+  // the row's extremes -- rounding is monotonic, so fl(max - mean) bounds every fl(a - mean)
+  double mx = -__builtin_huge_val(), mn = __builtin_huge_val(), dev = 0.0;
+  if (valid) {
+    double stk[40];
+    int sp = 0;
+    for (int op = 0; op < nprog; ++op) {
+      const int s = prog[2 * op], n = prog[2 * op + 1];
+      if (s < 0) {
+        const double bsum = stk[--sp];
+        stk[sp - 1] = stk[sp - 1] + bsum;
+        continue;
       }
-      res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-      for (; i < n; ++i) res = res + a[(int64_t)i * 16];
+      const double* a = AT + at_off(r, s, ns);  // consecutive snapshots are 16 doubles apart
+      auto ld = [&](int64_t k) -> double {
+        const double x = a[k];
+        mx = fmax(mx, x);
+        mn = fmin(mn, x);
+        return x;
+      };
+      double res;
+      if (n < 8) {
+        res = 0.0;
+        for (int i = 0; i < n; ++i) res = res + ld((int64_t)i * 16);
+      } else {
+        double r0 = ld(0), r1 = ld(16), r2 = ld(32), r3 = ld(48);
+        double r4 = ld(64), r5 = ld(80), r6 = ld(96), r7 = ld(112);
+        int i = 8;
+        for (; i < n - (n % 8); i += 8) {
+          const int64_t b = (int64_t)i * 16;
+          r0 = r0 + ld(b);
+          r1 = r1 + ld(b + 16);
+          r2 = r2 + ld(b + 32);
+          r3 = r3 + ld(b + 48);
+          r4 = r4 + ld(b + 64);
+          r5 = r5 + ld(b + 80);
+          r6 = r6 + ld(b + 96);
+          r7 = r7 + ld(b + 112);
+        }
+        res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+        for (; i < n; ++i) res = res + ld((int64_t)i * 16);
+      }
+      stk[sp++] = res;
     }
-    stk[sp++] = res;
+    const double mu = (0.0 + stk[0]) / (double)ns;
+    mean[r] = mu;
+    dev = fmax(mx - mu, mu - mn);
   }
-  mean[r] = (0.0 + stk[0]) / (double)ns;
+  if (devmax) {
+    unsigned long long u = (unsigned long long)__double_as_longlong(dev > 0.0 ? dev : 0.0);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long v = __shfl_xor(u, o);
+      u = v > u ? v : u;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(devmax, u);
+  }
 }
 
 // main() :1492-1495 (A[:, j] = A[:, j] - mean_field) in place on the K-tiled snapshot matrix:
@@ -1328,9 +1351,13 @@ int filter_yz_max_K(int Kp) {
 }
 
 hipError_t launch_mean(const double* AT, int64_t rowlen, int ns, const int* prog, int nprog,
-                       double* mean, hipStream_t st) {
+                       double* mean, hipStream_t st, double* devmax) {
+  if (devmax) {
+    const hipError_t e = hipMemsetAsync(devmax, 0, sizeof(double), st);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(k_mean, dim3((unsigned)((rowlen + 255) / 256)), dim3(256), 0, st, AT, rowlen, ns,
-                     prog, nprog, mean);
+                     prog, nprog, mean, reinterpret_cast<unsigned long long*>(devmax));
   return hipGetLastError();
 }
 

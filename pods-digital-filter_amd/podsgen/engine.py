@@ -80,6 +80,15 @@ class Context:
             check(self.lib.pods_set_shared_device(self.h, 1), "pods_set_shared_device")
         self._side = None
 
+    def corr_mode(self):
+        """pods_corr's product arithmetic: 1 = exact int8 modular products + CRT, 0 = fp64 SYRK."""
+        m = ctypes.c_int(-1)
+        check(self.lib.pods_get_corr_mode(self.h, ctypes.byref(m)), "pods_get_corr_mode")
+        return m.value
+
+    def set_corr_mode(self, mode):
+        check(self.lib.pods_set_corr_mode(self.h, int(mode)), "pods_set_corr_mode")
+
     def side_stream(self):
         """A second stream on the device for work that may overlap the main stream's."""
         if self._side is None:
@@ -746,8 +755,9 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
     mean = torch.empty(snap.rowlen, dtype=torch.float64, device=dev)
     with tm("mean"):
         check(lib.pods_mean(ctx.h, ptr(mean), 1), "pods_mean")
-    with tm("center"):  # main() :1493-1495, in place
-        check(lib.pods_center(ctx.h), "pods_center")
+    if ctx.corr_mode() == 0:   # the fp64 SYRK reads A centred in place (main() :1493-1495); the
+        with tm("center"):     # int8 correlation subtracts the mean while forming its residues
+            check(lib.pods_center(ctx.h), "pods_center")
     C = torch.empty((ns, ns), dtype=torch.float64, device=dev)
     with tm("corr"):
         check(lib.pods_corr(ctx.h, ptr(C), 1 if world == 1 else 0), "pods_corr")
