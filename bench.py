@@ -5,8 +5,8 @@
 
 One "step" is the whole hot path over one synthetic problem (BASELINE.json config 3,
 256 x 256 inlet x 4096 snapshots): MT19937 random field -> 3 separable Gaussian filter
-passes -> Lund transform -> snapshot matrix -> mean -> fp64 correlation (MFMA SYRK,
-RCCL all-reduce when N > 1) -> eigensolve -> temporal/spatial modes -> Fourier
+passes -> Lund transform -> snapshot matrix -> mean -> correlation (exact int8-MFMA
+residue SYRKs + CRT to fp64, RCCL all-reduce when N > 1) -> eigensolve -> temporal/spatial modes -> Fourier
 coefficients ranked and counted (the arrays PODFS.pod2prf / HDF5.write_HDF5 consume).
 File writing is outside the step.  A point is one inlet (j, k) at one step (3 fp64
 components); value = J*K*ns*steps / wall(max over ranks) / 1e6.
@@ -15,11 +15,12 @@ N > 1 runs one process per GPU under torch.distributed.run; the inlet rows are s
 into N slabs (strong scaling: the same 256^2 x 4096 problem at every N).
 
 Extra JSON objects (rank 0):
-  roofline      the dominant kernel (pods_corr: k_syrk_g128 + k_syrk_reduce), fp64 MFMA
-                bound; achieved = 3*P*ns*(ns+1) algorithmic flops per launch / mean launch
-                time from HIP events recorded around it on its stream inside the timed
-                steps; traffic from the committed rocprofv3 PMC summary (profiles/) when
-                one exists for this config.
+  roofline      the dominant kernel, k_syrk_i8 (pods_corr's 16 residue SYRKs), int8 MFMA
+                bound; achieved = 16 * 3P * ns * (ns+1) algorithmic int ops per launch / mean
+                launch time from HIP events the library records around it on its stream
+                inside the timed steps (pods_corr_timing); traffic from the committed
+                rocprofv3 PMC summary (profiles/) when one exists for this config.  With
+                PODS_CORR=f64: the fp64 SYRK, 3P*ns*(ns+1) flops / the corr stage time.
   cpu_baseline  the oracle (faithful numpy/scipy restatement of the reference, incl. its
                 Python loops) on a bounded sample of the same workload, extrapolated to the
                 full job (N = 1, rank 0 only).
@@ -80,6 +81,10 @@ def make_setup(podsgen, config, seed):
         return podsgen.DFSetup(jma=J, kma=K, ns=ns, seed=seed, dt=dt1 / 2.0, prf=prf)
     return podsgen.DFSetup(jma=J, kma=K, ns=ns, seed=seed)
 FP64_MFMA_PEAK_TFLOPS = 78.6  # MI355X dense FP64 matrix (spec); measured 70-76 by tools/mfma_bench.hip
+# MI355X dense int8 matrix: v_mfma_i32_16x16x64_i8 = 32768 ops per 16 cycles per SIMD
+# (MI355X_MICROARCH.md: I8 = 2x BF16 per clock), 1024 SIMDs at 2.4 GHz
+I8_MFMA_PEAK_TOPS = 2048 * 1024 * 2.4e9 / 1e12
+CORR_NMOD = 16  # residue SYRKs per correlation (podsgen_corr_i8.hip NMOD)
 
 
 def parse():
@@ -194,9 +199,9 @@ def cpu_baseline(J, K, ns, nm=20, budget=20.0):
             "stages_s": {k: round(v, 3) for k, v in est.items()}, "stage_basis": how}
 
 
-def load_traffic(config, ns, rank):
-    """HBM bytes per pods_corr launch from the committed PMC summary (profiles/)."""
-    path = os.path.join(ROOT, "profiles", "pmc_syrk_%s.json" % config)
+def load_traffic(config, corr_mode):
+    """HBM bytes per launch of the roofline kernel from the committed PMC summary (profiles/)."""
+    path = os.path.join(ROOT, "profiles", ("pmc_corr_i8_%s.json" if corr_mode == 1 else "pmc_syrk_%s.json") % config)
     if not os.path.exists(path):
         return None
     try:
@@ -286,6 +291,8 @@ def main():
     # each step's host-side Fourier results (copies, FC rows) finish during the next step's
     # SYRK (E.FourierBacklog); the last one, and the last steps' spectra, inside the timed region
     backlog = E.FourierBacklog()
+    corr_mode = gen.ctx.corr_mode()
+    podsgen.check(gen.ctx.lib.pods_corr_timing(gen.ctx.h, 1), "pods_corr_timing")
     t0 = time.perf_counter()
     for s in range(args.steps):
         _, pod, _ = step(timer=tm_run, backlog=backlog, ahead=s < args.steps - 1)
@@ -308,6 +315,11 @@ def main():
 
     # stage split and the roofline of the dominant kernel, from the timed steps' events
     stages = {k: v / args.steps for k, v in tm_run.summary().items()}
+    import ctypes
+    k_ms, k_n = ctypes.c_double(0.0), ctypes.c_int(0)
+    podsgen.check(gen.ctx.lib.pods_corr_kernel_ms(gen.ctx.h, ctypes.byref(k_ms), ctypes.byref(k_n)),
+                  "pods_corr_kernel_ms")
+    podsgen.check(gen.ctx.lib.pods_corr_timing(gen.ctx.h, 0), "pods_corr_timing")
 
     # one job on its own (after the timed region): generation to the FC arrays with no
     # cross-step overlap -- no prefetched jump-ahead or planes, the Fourier results finished in
@@ -329,10 +341,28 @@ def main():
     corr_ms = stages["corr"]
     P_local = (gen.j1 - gen.j0) * K
     flops = 3.0 * P_local * ns * (ns + 1)
-    achieved = flops / (corr_ms * 1e-3) / 1e12
     # the committed PMC summary is for the one-GPU launch; a rank's launch at N > 1 covers
     # only its row slab, so no measured figure applies there
-    traffic = load_traffic(args.config, ns, rank) if world == 1 else None
+    traffic = load_traffic(args.config, corr_mode) if world == 1 else None
+    if corr_mode == 1 and k_n.value > 0:
+        # the int8 SYRK: CORR_NMOD residue SYRKs of the 3 P x ns matrix, timed alone by HIP events
+        kern_ms = k_ms.value / k_n.value
+        ops = 2.0 * CORR_NMOD * 3 * P_local * ns * (ns + 1) / 2
+        achieved = ops / (kern_ms * 1e-3) / 1e12
+        roofline = {"kernel": "k_syrk_i8 (pods_corr's %d residue SYRKs on int8 MFMA), rank 0" % CORR_NMOD,
+                    "bound": "mfma", "dtype": "i8", "achieved": round(achieved, 1), "peak": round(I8_MFMA_PEAK_TOPS, 1),
+                    "unit": "TOP/s", "frac": round(achieved / I8_MFMA_PEAK_TOPS, 4), "traffic": traffic,
+                    "launch_ms": round(kern_ms, 3), "ops_per_launch": ops, "launches": k_n.value,
+                    "corr_stage_ms": round(corr_ms, 3),
+                    "corr_fp64_equiv_tflops": round(flops / (corr_ms * 1e-3) / 1e12, 2)}
+    else:
+        achieved = flops / (corr_ms * 1e-3) / 1e12
+        roofline = {"kernel": "pods_corr (k_syrk_g128 + k_syrk_reduce), rank 0",
+                    "bound": "mfma", "dtype": "f64", "achieved": round(achieved, 3),
+                    "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / FP64_MFMA_PEAK_TFLOPS, 4),
+                    "traffic": traffic, "launch_ms": round(corr_ms, 3),
+                    "flops_per_launch": flops}
     num_valid = pod.num_valid
     if spectrum is not None:   # from the last full spectrum (whichever rank owned it)
         done = spectrum.results()
@@ -366,12 +396,10 @@ def main():
             "config": {"workload": desc, "jma": J, "kma": K, "ns": ns, "nm": setup.nm,
                        "nf": [setup.nfx, setup.nfy, setup.nfz], "parallelism": "row-slab dp%d" % world,
                        "backend": args.backend if world > 1 else None, "dist_world_size": observed_world},
-            "roofline": {"kernel": "pods_corr (k_syrk_g128 + k_syrk_reduce), rank 0",
-                         "bound": "mfma", "achieved": round(achieved, 3),
-                         "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / FP64_MFMA_PEAK_TFLOPS, 4),
-                         "traffic": traffic, "launch_ms": round(corr_ms, 3),
-                         "flops_per_launch": flops},
+            "roofline": roofline,
+            "corr_arithmetic": ("exact: int8-MFMA residue products mod 16 pairwise-coprime moduli + CRT, one "
+                                "rounding to f64 (pods_corr mode 1)" if corr_mode == 1 else
+                                "fp64 MFMA SYRK (pods_corr mode 0)"),
             "stages_ms": {k: round(v, 3) for k, v in stages.items()},
             "setup_ms": {k: round(v, 1) for k, v in setup_ms.items()},
             "one_shot_ms": round(one_shot * 1e3, 3),

@@ -159,6 +159,12 @@ int pods_corr(pods_ctx* ctx, double* C_dev, int divide);
  * PODS_CORR=f64 in the environment selects 0 when the context is created. */
 int pods_set_corr_mode(pods_ctx* ctx, int mode);
 int pods_get_corr_mode(pods_ctx* ctx, int* mode);
+/* Measurement: with timing on, every mode-1 pods_corr records HIP events around its int8 SYRK
+ * launch on the context's stream; pods_corr_kernel_ms waits for them, returns the summed
+ * milliseconds and the number of launches, and starts a new count.  (With the residue buffer
+ * cut into several launches the events bracket all of them, residue passes included.) */
+int pods_corr_timing(pods_ctx* ctx, int enable);
+int pods_corr_kernel_ms(pods_ctx* ctx, double* total_ms, int* count);
 /* x[i] = x[i] / divisor for n doubles on the device. */
 int pods_divide_inplace(pods_ctx* ctx, double* x_dev, int64_t n, double divisor);
 /* The multi-device all-reduce of the partial correlations (PODFS.py:1455 summed over row slabs)

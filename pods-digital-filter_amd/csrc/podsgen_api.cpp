@@ -286,6 +286,11 @@ struct pods_ctx {
   DevBuf i8_res, i8_part, i8_items;
   int64_t i8_key = -1;
   pods::CorrI8Plan i8_plan{};
+  // pods_corr_timing: HIP events around each int8 SYRK launch (the roofline kernel), read back
+  // by pods_corr_kernel_ms
+  bool corr_timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> corr_ev;
+  size_t corr_ev_used = 0;
 };
 
 namespace {
@@ -461,6 +466,10 @@ int pods_destroy(pods_ctx* c) {
     for (DevBuf* b : {&sl.wm, &sl.x, &sl.flags, &sl.det, &sl.v, &sl.cnt, &sl.lam, &sl.ws2}) release(*b);
   release(c->inv_lam);
   for (DevBuf* b : {&c->devmax, &c->i8_res, &c->i8_part, &c->i8_items}) release(*b);
+  for (auto& ev : c->corr_ev) {
+    (void)hipEventDestroy(ev.first);
+    (void)hipEventDestroy(ev.second);
+  }
   if (c->pin) {
     for (int i = 0; i < pods_ctx::kStageSlots; ++i)
       if (c->pin_ev[i]) (void)hipEventDestroy(c->pin_ev[i]);
@@ -731,7 +740,9 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
     const int64_t budget = (int64_t)((bud ? std::atof(bud) : 16.0) * (double)(1LL << 30));
     const char* fsp = std::getenv("PODS_CORR_SPLITS");  // tests: a fixed number of K splits
     const int force = fsp ? std::max(0, std::atoi(fsp)) : 0;
-    const int64_t key = ((int64_t)ns << 40) ^ (c->rowpad << 4) ^ (budget >> 20) ^ ((int64_t)force << 58);
+    const char* ord = std::getenv("PODS_CORR_ORDER");
+    const int64_t key = ((int64_t)ns << 40) ^ (c->rowpad << 4) ^ (budget >> 20) ^ ((int64_t)force << 58) ^
+                        ((int64_t)(ord ? ord[0] : 0) << 50);
     if (c->i8_key != key) {
       if (pods::corr_i8_plan(ns, c->rowlen, c->rowpad, budget, &c->i8_plan, force) != 0)
         return fail(PODS_ERR_UNSUPPORTED, "pods_corr: K too large for the int8 correlation (PODS_CORR=f64)");
@@ -748,9 +759,21 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
                                    c->stream));
       c->dev_valid = true;
     }
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (c->corr_timing) {
+      if (c->corr_ev_used == c->corr_ev.size()) {
+        std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+        PODS_HIP(hipEventCreate(&ev.first));
+        PODS_HIP(hipEventCreate(&ev.second));
+        c->corr_ev.push_back(ev);
+      }
+      e0 = c->corr_ev[c->corr_ev_used].first;
+      e1 = c->corr_ev[c->corr_ev_used].second;
+      ++c->corr_ev_used;
+    }
     PODS_HIP(pods::launch_corr_i8(c->A.as<double>(), ns, c->rowlen, c->rowpad, mean, c->devmax.as<double>(),
                                   c->i8_plan, c->i8_items.as<int>(), c->i8_res.as<int8_t>(),
-                                  c->i8_part.as<uint8_t>(), C_dev, ns, divide, c->stream));
+                                  c->i8_part.as<uint8_t>(), C_dev, ns, divide, c->stream, e0, e1));
     return PODS_OK;
   }
   int64_t ksplit = 0;
@@ -775,6 +798,31 @@ int pods_set_corr_mode(pods_ctx* c, int mode) {
   if (mode != 0 && mode != 1) return fail(PODS_ERR_ARG, "corr mode must be 0 (fp64) or 1 (int8 CRT)");
   c->corr_mode = mode;
   return PODS_OK;
+}
+
+int pods_corr_timing(pods_ctx* c, int enable) {
+  if (int e = check_ctx(c)) return e;
+  c->corr_timing = enable != 0;
+  c->corr_ev_used = 0;
+  return PODS_OK;
+}
+
+int pods_corr_kernel_ms(pods_ctx* c, double* total_ms, int* count) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!total_ms || !count) return fail(PODS_ERR_ARG, "null output");
+  double t = 0.0;
+  for (size_t k = 0; k < c->corr_ev_used; ++k) {
+    PODS_HIP(hipEventSynchronize(c->corr_ev[k].second));
+    float ms = 0.0f;
+    PODS_HIP(hipEventElapsedTime(&ms, c->corr_ev[k].first, c->corr_ev[k].second));
+    t += ms;
+  }
+  *total_ms = t;
+  *count = (int)c->corr_ev_used;
+  c->corr_ev_used = 0;
+  return PODS_OK;
+  PODS_CATCH
 }
 
 int pods_get_corr_mode(pods_ctx* c, int* mode) {

@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <type_traits>
 #include <vector>
 
@@ -37,6 +38,7 @@ struct ModTables {
   int m[NMOD];
   int p18[NMOD], p36[NMOD];  // 2^18, 2^36 mod m
   int off[NMOD];             // -(2^52) mod m
+  int p11[NMOD][5];          // 2^(11 k) mod m
   int inv[NMOD][NMOD];       // inv[k][l] = m_k^-1 mod m_l (k != l)
 };
 constexpr int pow2mod(int e, int m) {
@@ -59,6 +61,7 @@ constexpr ModTables make_tables() {
     t.p18[l] = pow2mod(18, mm[l]);
     t.p36[l] = pow2mod(36, mm[l]);
     t.off[l] = (mm[l] - pow2mod(52, mm[l])) % mm[l];
+    for (int k = 0; k < 5; ++k) t.p11[l][k] = pow2mod(11 * k, mm[l]);
   }
   for (int l = 0; l < NMOD; ++l)
     for (int k = 0; k < NMOD; ++k) t.inv[k][l] = k == l ? 0 : invmod(mm[k], mm[l]);
@@ -89,6 +92,9 @@ __device__ __forceinline__ int modulus(int l) {
     if (k == l) r = kT.m[k];
   return r;
 }
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int I, int N, class F>
 __device__ __forceinline__ void sfor(F&& f) {
@@ -153,37 +159,50 @@ __global__ __launch_bounds__(256) void k_residues(const double* __restrict__ AT,
     for (int e = 0; e < 16; ++e) a[e] = 0.0;
   }
   const int sg = scale_exp(*devmax, bbits);
-  // z = a' + 2^52 in [0, 2^53] as three limbs of 18 bits (all steps exact)
-  uint32_t z0[16], z1[16], z2[16];
+  // z = a' + 2^52 in [0, 2^53] as five 11-bit limbs z_k, held as exact f32
+  f32x2 F[5][8];
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const double z = rint(ldexp(a[e], sg)) + 0x1p52;
-    const double h2 = floor(z * 0x1p-36);
-    const double rem = __builtin_fma(-h2, 0x1p36, z);
-    const double h1 = floor(rem * 0x1p-18);
-    const double h0 = __builtin_fma(-h1, 0x1p18, rem);
-    z2[e] = (uint32_t)h2;
-    z1[e] = (uint32_t)h1;
-    z0[e] = (uint32_t)h0;
+    const double h = floor(z * 0x1p-32);
+    const uint32_t lo = (uint32_t)__builtin_fma(-h, 0x1p32, z), hi = (uint32_t)h;
+    const uint32_t zk[5] = {lo & 0x7FFu, (lo >> 11) & 0x7FFu, __builtin_amdgcn_alignbit(hi, lo, 22) & 0x7FFu,
+                            (hi >> 1) & 0x7FFu, hi >> 12};
+#pragma unroll
+    for (int k = 0; k < 5; ++k) F[k][e >> 1][e & 1] = (float)zk[k];
   }
-  int8_t* dst = R + (kcl * ns + i) * 64 + q * 16;
+  const uint32_t doff = (uint32_t)((kcl * ns + i) * 64 + q * 16);  // < lstride < 4 GB
+  // per modulus m: s = sum_k z_k (2^11k mod m) + (-2^52 mod m) < 2^21.4, exact in f32; the f32
+  // quotient s * fl(1/m) is within 2^-23 * 2^13.9 < 1/(2m) of s / m, and s / m (m odd) is never
+  // within 1/(2m) of a half-integer, so rint gives the balanced residue s - m rint(s/m) exactly
   sfor<0, NMOD>([&](auto L) {
     constexpr int l = decltype(L)::value;
-    constexpr uint32_t m = kT.m[l], c1 = kT.p18[l], c2 = kT.p36[l], o = kT.off[l];
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    constexpr float m = (float)kT.m[l], inv = 1.0f / (float)kT.m[l], o = (float)kT.off[l];
+    constexpr float c1 = (float)kT.p11[l][1], c2 = (float)kT.p11[l][2], c3 = (float)kT.p11[l][3],
+                    c4 = (float)kT.p11[l][4];
+    uint32_t w[4];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const uint32_t s = z2[e] * c2 + z1[e] * c1 + z0[e] + o;  // < 2^27
-      int v = (int)(s % m);
-      if (v > (int)(m / 2)) v -= (int)m;
-      w[e >> 2] |= ((uint32_t)v & 255u) << (8 * (e & 3));
+    for (int pq = 0; pq < 4; ++pq) {
+      uint32_t half[2];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int pr = pq * 2 + h2;
+        f32x2 sv = __builtin_elementwise_fma(F[1][pr], (f32x2){c1, c1}, F[0][pr]);
+        sv = __builtin_elementwise_fma(F[2][pr], (f32x2){c2, c2}, sv);
+        sv = __builtin_elementwise_fma(F[3][pr], (f32x2){c3, c3}, sv);
+        sv = __builtin_elementwise_fma(F[4][pr], (f32x2){c4, c4}, sv) + (f32x2){o, o};
+        const f32x2 qv = __builtin_elementwise_roundeven(sv * (f32x2){inv, inv});
+        const f32x2 rv = __builtin_elementwise_fma(-qv, (f32x2){m, m}, sv);
+        half[h2] = __builtin_amdgcn_perm((uint32_t)(int)rv[1], (uint32_t)(int)rv[0], 0x0C0C0400u);
+      }
+      w[pq] = half[0] | (half[1] << 16);
     }
-    *reinterpret_cast<uint4*>(dst + (int64_t)l * lstride) = make_uint4(w[0], w[1], w[2], w[3]);
+    int8_t* base = R + (int64_t)l * lstride;  // uniform: a scalar base + 32-bit offset store
+    *reinterpret_cast<uint4*>(base + doff) = make_uint4(w[0], w[1], w[2], w[3]);
   });
 }
 
 // ---- the int8 SYRK -----------------------------------------------------------------------
-typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 template <int N>
 __device__ __forceinline__ void wait_vm() {
@@ -199,47 +218,47 @@ constexpr int TB = 256;            // tile rows / columns
 constexpr int KC = 64;             // K bytes per chunk (one MFMA K step)
 constexpr int PANEL = TB * KC;     // 16 KB: one chunk of 256 rows
 constexpr int FOLD = 2048;         // K steps between the mod-m reductions of the accumulators
+__device__ __forceinline__ int swz(int quartet) { return (0x78 >> (2 * quartet)) & 3; }
 
 // One 256 x 256 tile of one modulus' residue SYRK over one K split.  8 waves as 2 x 4, each
 // 128 x 64 = 8 x 4 blocks of v_mfma_i32_16x16x64_i8 (lane l: A[l&15][16(l>>4)+j],
 // B[16(l>>4)+j][l&15]; D[4(l>>4)+r][l&15]).  Both operands are rows of the same K-tiled residue
-// matrix, so a fragment is 16 consecutive 64-B rows = 1 KB contiguous in LDS (conflict-free
-// ds_read_b128, no swizzle).  Operands stream by LDS-DMA into an NST-stage ring of KSUB chunks
-// per stage (counted vmcnt + barrier, as k_syrk_g128).  items: {bi, bj, split, -} (bi < 0: an
-// empty slot that keeps the item count a multiple of 8).
-template <int NST, int KSUB>
-__global__ __launch_bounds__(512, 1) void k_syrk_i8(const int8_t* __restrict__ R, int ns, int64_t lstride, int kcs,
-                                                    const int4* __restrict__ items, int nitems, int nsplit,
-                                                    uint8_t* __restrict__ P, int64_t pslab, int accumulate) {
-  constexpr int STG = KSUB * 2 * PANEL;
-  constexpr int Q = KSUB * 4;  // DMA instructions per wave per stage
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  const int l = blockIdx.x / nitems;
-  const int4 it = items[blockIdx.x - l * nitems];
-  if (it.x < 0) return;
-  const int bi = it.x, bj = it.y, sp = it.z;
-  const int i0 = bi * TB, j0 = bj * TB;
-  const int nt = kcs / KSUB;
+// matrix, so a fragment is 16 consecutive 64-B rows of one K chunk.  Operands stream by LDS-DMA
+// into an NST-stage ring (counted vmcnt + one barrier per K step); the fragments of step t+1
+// are read between the two halves of step t's MFMAs.  A diagonal tile (SAME) loads one panel and
+// reads it as both operands.  items: {bi, bj, split, -} (bi < 0: an empty slot that keeps the
+// item count a multiple of 8).  DIAG (measurement only): 1 = no MFMAs, 2 = no operand traffic.
+template <int NST, int DIAG, bool SAME>
+__device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int ns, int nt, int i0, int j0, int m,
+                                          char* smem, uint8_t* __restrict__ dst, int ldp, int accumulate) {
+  constexpr int STG = 2 * PANEL;
+  constexpr int Q = SAME ? 2 : 4;  // DMA instructions per wave per stage
+  constexpr int D = NST - 2;       // DMA lead in K steps beyond the one being read
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int8_t* base = R + (int64_t)l * lstride + (int64_t)sp * kcs * ns * KC;
+  // LDS rows are 64 B (four 16-B slots); row R keeps logical slot s at physical slot
+  // s ^ g((R >> 2) & 3), g = {0, 2, 3, 1}: ds_read_b128 serves a wave in the lane groups
+  // {0-3, 12-15, 20-27}, {4-11, 16-19, 28-31} (+32), and with this g the four 4-row quartets
+  // of every group land on four different 16-B bank columns (conflict-free).  The DMA writes
+  // each wave-instruction's 1 KB linearly, so the swizzle is applied to the source address.
   int64_t xo[2], yo[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int rw = (wave * 2 + q) * 16 + (lane >> 2);
-    xo[q] = (int64_t)min(i0 + rw, ns - 1) * KC + (lane & 3) * 16;
-    yo[q] = (int64_t)min(j0 + rw, ns - 1) * KC + (lane & 3) * 16;
+    const int ls = (lane & 3) ^ swz((rw >> 2) & 3);
+    xo[q] = (int64_t)min(i0 + rw, ns - 1) * KC + ls * 16;
+    yo[q] = (int64_t)min(j0 + rw, ns - 1) * KC + ls * 16;
   }
   const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
   const int64_t cstride = (int64_t)ns * KC;
   auto issue = [&](int t) {
+    if constexpr (DIAG == 2) return;
     const uint32_t sb = lds0 + (uint32_t)((t % NST) * STG);
+    const int8_t* g = base + (int64_t)t * cstride;
 #pragma unroll
-    for (int ks = 0; ks < KSUB; ++ks) {
-      const int8_t* g = base + (int64_t)(t * KSUB + ks) * cstride;
+    for (int q = 0; q < 2; ++q) dma16(g + xo[q], sb + (wave * 2 + q) * 1024);
+    if constexpr (!SAME) {
 #pragma unroll
-      for (int q = 0; q < 2; ++q) dma16(g + xo[q], sb + (ks * 2) * PANEL + (wave * 2 + q) * 1024);
-#pragma unroll
-      for (int q = 0; q < 2; ++q) dma16(g + yo[q], sb + (ks * 2 + 1) * PANEL + (wave * 2 + q) * 1024);
+      for (int q = 0; q < 2; ++q) dma16(g + yo[q], sb + PANEL + (wave * 2 + q) * 1024);
     }
   };
   i32x4 acc[8][4];
@@ -247,34 +266,30 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8(const int8_t* __restrict__ R
   for (int a = 0; a < 8; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = (i32x4){0, 0, 0, 0};
-#pragma unroll
-  for (int t = 0; t < NST - 1; ++t)
-    if (t < nt) issue(t);
-  const int m = modulus(l);
   const int wr = wave >> 2, wc = wave & 3;
-  const int fo = (lane & 15) * KC + (lane >> 4) * 16;
-  for (int t = 0; t < nt; ++t) {
-    if (t + NST - 2 < nt) wait_vm<Q * (NST - 2)>();
-    else wait_vm<0>();
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (t + NST - 1 < nt) issue(t + NST - 1);
+  const int fo = (lane & 15) * KC + (((lane >> 4) ^ swz((lane >> 2) & 3)) * 16);  // row lane&15, slot lane>>4
+  auto read = [&](int t, i32x4 (&av)[8], i32x4 (&bv)[4]) {
     const char* st = smem + (t % NST) * STG;
+    const char* X = st + wr * 128 * KC + fo;
+    const char* Y = st + (SAME ? 0 : PANEL) + wc * 64 * KC + fo;
 #pragma unroll
-    for (int ks = 0; ks < KSUB; ++ks) {
-      const char* X = st + ks * 2 * PANEL + wr * 128 * KC + fo;
-      const char* Y = st + (ks * 2 + 1) * PANEL + wc * 64 * KC + fo;
-      i32x4 av[8], bv[4];
+    for (int a = 0; a < 8; ++a) av[a] = *reinterpret_cast<const i32x4*>(X + a * 16 * KC);
 #pragma unroll
-      for (int a = 0; a < 8; ++a) av[a] = *reinterpret_cast<const i32x4*>(X + a * 16 * KC);
+    for (int b = 0; b < 4; ++b) bv[b] = *reinterpret_cast<const i32x4*>(Y + b * 16 * KC);
+  };
+  auto mma_rows = [&](const i32x4 (&av)[8], const i32x4 (&bv)[4], int a0) {
 #pragma unroll
-      for (int b = 0; b < 4; ++b) bv[b] = *reinterpret_cast<const i32x4*>(Y + b * 16 * KC);
-#pragma unroll
-      for (int a = 0; a < 8; ++a)
+    for (int a = a0; a < a0 + 4; ++a) {
+      if constexpr (DIAG == 1) {
+        acc[a][0] += av[a] ^ bv[a & 3];
+      } else {
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[a], bv[b], acc[a][b], 0, 0, 0);
+      }
     }
-    if (((t + 1) * KSUB) % FOLD == 0 && t + 1 < nt) {
+  };
+  auto fold = [&](int t) {
+    if ((t + 1) % FOLD == 0 && t + 1 < nt) {
       // |acc| stays < m + 2048 * 64 * 127^2 < 2^31
 #pragma unroll
       for (int a = 0; a < 8; ++a)
@@ -283,8 +298,41 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8(const int8_t* __restrict__ R
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[a][b][r] %= m;
     }
+  };
+  // step t: every wave waits for stage t+1, one barrier, the DMA of stage t + D + 1 into the
+  // slot of step t - 1 (read during step t - 1's MFMAs, consumed by them), then step t's MFMAs
+  // with the reads of step t+1 between their halves -- the wait the compiler puts at the loop
+  // head (lgkmcnt(0)) then finds those reads long complete
+#pragma unroll
+  for (int t = 0; t <= D; ++t)
+    if (t < nt) issue(t);
+  if (D < nt) wait_vm<Q * D>();
+  else wait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  i32x4 a0[8], b0[4], a1[8], b1[4];
+  read(0, a0, b0);
+  auto step = [&](int t, const i32x4 (&ac)[8], const i32x4 (&bc)[4], i32x4 (&an)[8], i32x4 (&bn)[4]) {
+    if (t + 1 < nt) {
+      if (t + D < nt) wait_vm<Q * (D - 1)>();
+      else wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + D + 1 < nt) issue(t + D + 1);
+    }
+    mma_rows(ac, bc, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < nt) read(t + 1, an, bn);
+    __builtin_amdgcn_sched_barrier(0);
+    mma_rows(ac, bc, 4);
+    fold(t);
+  };
+  int t = 0;
+  for (; t + 1 < nt; t += 2) {
+    step(t, a0, b0, a1, b1);
+    step(t + 1, a1, b1, a0, b0);
   }
-  uint8_t* dst = P + (int64_t)(l * nsplit + sp) * pslab;
+  if (t < nt) step(t, a0, b0, a1, b1);
   const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll
   for (int a = 0; a < 8; ++a)
@@ -297,7 +345,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8(const int8_t* __restrict__ R
         if (gi < ns && gj <= gi) {
           int v = acc[a][b][r] % m;
           if (v < 0) v += m;
-          uint8_t* p = dst + (int64_t)gi * ns + gj;
+          uint8_t* p = dst + (int64_t)gi * ldp + gj;
           if (accumulate) {
             v += *p;
             if (v >= m) v -= m;
@@ -305,6 +353,30 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8(const int8_t* __restrict__ R
           *p = (uint8_t)v;
         }
       }
+}
+
+template <int NST, int DIAG = 0>
+__global__ __launch_bounds__(512, 1) void k_syrk_i8(const int8_t* __restrict__ R, int ns, int64_t lstride, int kcs,
+                                                    const int4* __restrict__ items, int nitems, int nsplit,
+                                                    uint8_t* __restrict__ P, int64_t pslab, int ldp, int accumulate,
+                                                    int xcd_ranges) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  int b = blockIdx.x;
+  if (xcd_ranges) {  // block b runs on XCD b % 8: give each XCD a contiguous range of the work
+    const int nb = gridDim.x, xcd = b & 7, q = nb >> 3, rr = nb & 7;
+    b = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (b >> 3);
+  }
+  const int l = b / nitems;
+  const int4 it = items[b - l * nitems];
+  if (it.x < 0) return;
+  const int bi = it.x, bj = it.y, sp = it.z;
+  const int8_t* base = R + (int64_t)l * lstride + (int64_t)sp * kcs * ns * KC;
+  uint8_t* dst = P + (int64_t)(l * nsplit + sp) * pslab;
+  const int m = modulus(l);
+  if (bi == bj)
+    syrk_tile<NST, DIAG, true>(base, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
+  else
+    syrk_tile<NST, DIAG, false>(base, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
 }
 
 // ---- CRT reconstruction ----------------------------------------------------------------------
@@ -339,41 +411,65 @@ __device__ __forceinline__ double crt_value(const int (&c)[NMOD]) {
   return neg ? -d : d;
 }
 
-// C[i][j] (lower 64 x 64 tiles, mirrored through LDS as k_syrk_reduce) from the partials
-__global__ __launch_bounds__(256) void k_crt(const uint8_t* __restrict__ P, int nsplit, int64_t pslab, int ns,
-                                             const double* __restrict__ devmax, int bbits, double* __restrict__ C,
-                                             int64_t ldc, int divide) {
+// C[i][j] (lower 64 x 64 tiles, mirrored through LDS as k_syrk_reduce) from the partials:
+// thread (row r, column quad) loads each modulus' / split's 4 residues of its row as one u32
+// (P rows padded to ldp, a multiple of 64)
+__global__ __launch_bounds__(256) void k_crt(const uint8_t* __restrict__ P, int nsplit, int64_t pslab, int ldp,
+                                             int ns, const double* __restrict__ devmax, int bbits,
+                                             double* __restrict__ C, int64_t ldc, int divide) {
   __shared__ double tile[64][65];
   const int L = blockIdx.x;
   int ti = (int)((sqrt(8.0 * (double)L + 1.0) - 1.0) * 0.5);
   while ((ti + 1) * (ti + 2) / 2 <= L) ++ti;
   while (ti * (ti + 1) / 2 > L) --ti;
   const int tj = L - ti * (ti + 1) / 2;
-  const int c = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+  const int cq = threadIdx.x & 15, rq = threadIdx.x >> 4;
   const int sg = scale_exp(*devmax, bbits);
   const double dn = (double)ns;
 #pragma unroll 1
-  for (int q = 0; q < 16; ++q) {
-    const int r = r0 + 4 * q;
-    const int i = ti * 64 + r, j = tj * 64 + c;
-    const bool ok = i < ns && j < ns && (ti > tj || c <= r);
-    double val = 0.0;
-    if (ok) {
-      int cr[NMOD];
-      const int64_t off = (int64_t)i * ns + j;
-      sfor<0, NMOD>([&](auto Lm) {
-        constexpr int l = decltype(Lm)::value;
-        int s = 0;
-        for (int sp = 0; sp < nsplit; ++sp) s += P[(int64_t)(l * nsplit + sp) * pslab + off];
-        cr[l] = s % kT.m[l];
-      });
-      val = ldexp(crt_value(cr), -2 * sg);
-      if (divide) val = val / dn;
-      C[(int64_t)i * ldc + j] = val;
+  for (int it = 0; it < 4; ++it) {
+    const int r = rq + 16 * it;
+    const int i = ti * 64 + r, jb = tj * 64 + 4 * cq;
+    double val[4] = {0.0, 0.0, 0.0, 0.0};
+    if (i < ns) {
+      // the splits' bytes summed in 16-bit fields: even bytes (entries 0, 2), odd (1, 3)
+      uint32_t ev[NMOD], od[NMOD];
+      const uint8_t* src = P + (int64_t)i * ldp + jb;
+#pragma unroll
+      for (int l = 0; l < NMOD; ++l) {
+        const uint32_t v = *reinterpret_cast<const uint32_t*>(src + (int64_t)(l * nsplit) * pslab);
+        ev[l] = v & 0x00FF00FFu;
+        od[l] = (v >> 8) & 0x00FF00FFu;
+      }
+      for (int sp = 1; sp < nsplit; ++sp)
+#pragma unroll
+        for (int l = 0; l < NMOD; ++l) {
+          const uint32_t v = *reinterpret_cast<const uint32_t*>(src + (int64_t)(l * nsplit + sp) * pslab);
+          ev[l] += v & 0x00FF00FFu;
+          od[l] += (v >> 8) & 0x00FF00FFu;
+        }
+#pragma unroll 1
+      for (int k = 0; k < 4; ++k) {
+        const int j = jb + k;
+        if (j < ns && (ti > tj || j <= i)) {
+          int cr[NMOD];
+          const int sh = 16 * (k >> 1);
+          sfor<0, NMOD>([&](auto Lm) {
+            constexpr int l = decltype(Lm)::value;
+            cr[l] = (int)((((k & 1) ? od[l] : ev[l]) >> sh) & 0xFFFFu) % kT.m[l];
+          });
+          double v = ldexp(crt_value(cr), -2 * sg);
+          if (divide) v = v / dn;
+          C[(int64_t)i * ldc + j] = v;
+          val[k] = v;
+        }
+      }
     }
-    tile[r][c] = val;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tile[r][4 * cq + k] = val[k];
   }
   __syncthreads();
+  const int c = threadIdx.x & 63, r0 = threadIdx.x >> 6;
 #pragma unroll 4
   for (int r = r0; r < 64; r += 4) {
     const int i = tj * 64 + r, j = ti * 64 + c;
@@ -386,7 +482,7 @@ __global__ __launch_bounds__(256) void k_crt(const uint8_t* __restrict__ P, int 
 
 // ---- host ------------------------------------------------------------------------------------
 namespace {
-constexpr int I8_NST = 4, I8_KSUB = 1;
+constexpr int I8_KSUB = 1;  // K chunks per split are a multiple of this
 }
 
 int corr_i8_nmod() { return i8::NMOD; }
@@ -425,7 +521,7 @@ int corr_i8_plan(int ns, int64_t rowlen, int64_t rowpad, int64_t budget_bytes, C
   p.nkc = nkc;
   p.nitems = tiles8 * p.nsplit;
   p.r_bytes = (int64_t)i8::NMOD * p.chunks * ns * i8::KC;
-  p.p_bytes = (int64_t)i8::NMOD * p.nsplit * ns * ns;
+  p.p_bytes = (int64_t)i8::NMOD * p.nsplit * ns * ((ns + 63) / 64 * 64);
   *out = p;
   return 0;
 }
@@ -444,6 +540,25 @@ std::vector<int> corr_i8_items(int ns, const CorrI8Plan& p) {
     }
   std::sort(t.begin(), t.end());
   const int tiles = (int)t.size(), per = (tiles + 7) / 8;
+  // PODS_CORR_ORDER (A/B runs): "m" = plain Morton order, no XCD groups; "x" = plain Morton order
+  // with every XCD given a contiguous range of the whole grid (kernel-side remap)
+  const char* ord = std::getenv("PODS_CORR_ORDER");
+  if (ord && (ord[0] == 'm' || ord[0] == 'x')) {
+    std::vector<int> out;
+    for (int s = 0; s < p.nsplit; ++s)
+      for (int k = 0; k < per * 8; ++k) {
+        if (k < tiles) {
+          out.push_back(t[k].second.first);
+          out.push_back(t[k].second.second);
+        } else {
+          out.push_back(-1);
+          out.push_back(-1);
+        }
+        out.push_back(s);
+        out.push_back(0);
+      }
+    return out;
+  }
   std::vector<int> out;
   out.reserve((size_t)p.nitems * 4);
   for (int s = 0; s < p.nsplit; ++s)
@@ -475,15 +590,28 @@ hipError_t launch_absdev(const double* AT, int ns, int64_t rowlen, int64_t rowpa
 
 hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowpad, const double* mean,
                           const double* devmax, const CorrI8Plan& p, const int* items, int8_t* R, uint8_t* P,
-                          double* C, int64_t ldc, int divide, hipStream_t st) {
+                          double* C, int64_t ldc, int divide, hipStream_t st, hipEvent_t syrk_begin,
+                          hipEvent_t syrk_end) {
   using namespace i8;
-  constexpr size_t lds = (size_t)I8_NST * I8_KSUB * 2 * PANEL;
-  static_assert(lds <= 160 * 1024, "LDS");
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_syrk_i8<I8_NST, I8_KSUB>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  // PODS_SYRK_I8 (A/B runs): "4" / "5" ring stages (default 4); "9m" / "9d": the 4-stage kernel
+  // without MFMAs / without operand traffic (measurement only, wrong results)
+  int variant = 4;
+  if (const char* v = std::getenv("PODS_SYRK_I8")) {
+    if (v[0] == '5') variant = 5;
+    if (v[0] == '9') variant = v[1] == 'm' ? 91 : 92;
+  }
+  const void* fn = variant == 5 ? reinterpret_cast<const void*>(&k_syrk_i8<5>)
+                 : variant == 91 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 1>)
+                 : variant == 92 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 2>)
+                                 : reinterpret_cast<const void*>(&k_syrk_i8<4>);
+  const size_t lds = (size_t)(variant == 5 ? 5 : 4) * 2 * PANEL;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   const int64_t lstride = p.chunks * ns * KC;
-  const int64_t pslab = (int64_t)ns * ns;
+  const int ldp = (ns + 63) / 64 * 64;
+  const int64_t pslab = (int64_t)ns * ldp;
+  if (syrk_begin && p.nlaunch > 1) e = hipEventRecord(syrk_begin, st);
+  if (e != hipSuccess) return e;
   for (int li = 0; li < p.nlaunch; ++li) {
     const int64_t kc0 = (int64_t)li * p.chunks;
     const int64_t thr = p.chunks * ns * 4;
@@ -491,15 +619,29 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
                        mean, devmax, p.bbits, kc0, p.chunks, R, lstride);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_syrk_i8<I8_NST, I8_KSUB>), dim3((unsigned)(NMOD * p.nitems)), dim3(512), lds, st, R, ns,
-                       lstride, p.kcs, reinterpret_cast<const int4*>(items), p.nitems, p.nsplit, P, pslab,
-                       li > 0 ? 1 : 0);
+    // the events bracket the SYRK launch (with several launches: the first residue pass to the last SYRK)
+    if (syrk_begin && p.nlaunch == 1) e = hipEventRecord(syrk_begin, st);
+    if (e != hipSuccess) return e;
+    {
+      const int ldp_ = ldp;
+      const int acc_ = li > 0 ? 1 : 0;
+      const char* ord = std::getenv("PODS_CORR_ORDER");
+      int xr_ = ord && ord[0] == 'x' ? 1 : 0;
+      const int4* it_ = reinterpret_cast<const int4*>(items);
+      void* args[] = {&R, const_cast<int*>(&ns), const_cast<int64_t*>(&lstride), const_cast<int*>(&p.kcs),
+                      &it_, const_cast<int*>(&p.nitems), const_cast<int*>(&p.nsplit), &P,
+                      const_cast<int64_t*>(&pslab), const_cast<int*>(&ldp_), const_cast<int*>(&acc_), &xr_};
+      e = hipLaunchKernel(fn, dim3((unsigned)(NMOD * p.nitems)), dim3(512), args, lds, st);
+      if (e != hipSuccess) return e;
+    }
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
+  if (syrk_end) e = hipEventRecord(syrk_end, st);
+  if (e != hipSuccess) return e;
   const int nt = (ns + 63) / 64;
-  hipLaunchKernelGGL(k_crt, dim3((unsigned)(nt * (nt + 1) / 2)), dim3(256), 0, st, P, p.nsplit, pslab, ns, devmax,
-                     p.bbits, C, ldc, divide);
+  hipLaunchKernelGGL(k_crt, dim3((unsigned)(nt * (nt + 1) / 2)), dim3(256), 0, st, P, p.nsplit, pslab, ldp, ns,
+                     devmax, p.bbits, C, ldc, divide);
   return hipGetLastError();
 }
 

@@ -57,7 +57,8 @@ hipError_t launch_absdev(const double* AT, int ns, int64_t rowlen, int64_t rowpa
                          double* devmax, hipStream_t st);
 hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowpad, const double* mean,
                           const double* devmax, const CorrI8Plan& p, const int* items, int8_t* R, uint8_t* P,
-                          double* C, int64_t ldc, int divide, hipStream_t st);
+                          double* C, int64_t ldc, int divide, hipStream_t st, hipEvent_t syrk_begin = nullptr,
+                          hipEvent_t syrk_end = nullptr);
 // Split-K SYRK (k_syrk_g128 + k_syrk_reduce).  Plan: returns the number of K splits (work
 // slabs of ns*ns doubles).
 int syrk_plan(int ns, int64_t Kdim, int64_t* ksplit);
