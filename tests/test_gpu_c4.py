@@ -63,6 +63,9 @@ def c4():
     cols = {i: snap_block(gen, i, i + 1)[0].cpu().numpy() for i in STEPS}
     raw_rows = sample_rows(gen, rows)
     pod = E.run_pod(snap, s.nm, keep_C=True)
+    # the default (int8) correlation subtracts the mean while forming its residues and leaves A as
+    # generated; centre it in place now (pods_center, main() :1493-1495) for the checks below
+    podsgen.check(gen.ctx.lib.pods_center(gen.ctx.h), "pods_center")
     torch.cuda.synchronize()
     cen_rows = sample_rows(gen, rows)
     fo = E.run_fourier(gen.ctx, pod.T, pod.nm, s.ns, s.dt_eff, s.et)

@@ -53,6 +53,9 @@ def c3():
 
     A_raw = device_copy()
     pod = E.run_pod(snap, s.nm, keep_C=True)
+    # the default (int8) correlation subtracts the mean while forming its residues and leaves A as
+    # generated; centre it in place now (pods_center, main() :1493-1495) for the checks below
+    podsgen.check(gen.ctx.lib.pods_center(gen.ctx.h), "pods_center")
     A_c = device_copy()
     fo = E.run_fourier(gen.ctx, pod.T, pod.nm, s.ns, s.dt_eff, s.et)
     torch.cuda.synchronize()
