@@ -543,6 +543,17 @@ std::vector<int> corr_i8_items(int ns, const CorrI8Plan& p) {
   // PODS_CORR_ORDER (A/B runs): "m" = plain Morton order, no XCD groups; "x" = plain Morton order
   // with every XCD given a contiguous range of the whole grid (kernel-side remap)
   const char* ord = std::getenv("PODS_CORR_ORDER");
+  if (ord && ord[0] == 's') {  // measurement only (wrong results): every item is tile (1, 0)
+    std::vector<int> out;
+    for (int s = 0; s < p.nsplit; ++s)
+      for (int k = 0; k < per * 8; ++k) {
+        out.push_back(nb > 1 ? 1 : 0);
+        out.push_back(0);
+        out.push_back(s);
+        out.push_back(0);
+      }
+    return out;
+  }
   if (ord && (ord[0] == 'm' || ord[0] == 'x')) {
     std::vector<int> out;
     for (int s = 0; s < p.nsplit; ++s)
