@@ -136,8 +136,10 @@ int pods_mean(pods_ctx* ctx, double* mean_out, int out_is_device);
 
 /* Centre the snapshots in place, A[:, j] = A[:, j] - mean (main() :1493-1495), after
  * pods_mean.  pods_corr and pods_spatial_modes then read A as it stands instead of
- * subtracting the mean at every fragment read (same values, so the same results; the
- * SYRK runs 7 % faster).  Irreversible until the snapshots are regenerated or reloaded. */
+ * subtracting the mean themselves (same values, so the same results).  Worth it for the fp64
+ * SYRK (pods_corr mode 0, 7 % faster on a centred A); the default int8 correlation subtracts
+ * the mean while forming its residues and needs no centring.  Irreversible until the
+ * snapshots are regenerated or reloaded. */
 int pods_center(pods_ctx* ctx);
 
 /* Set the mean the correlation / spatial-mode kernels subtract (mean_host: row_len doubles,
