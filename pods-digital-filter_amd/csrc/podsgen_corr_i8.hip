@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256) void k_absdev(const double* __restrict__ AT, i
 // Thread (chunk kc, snapshot i, quarter q) converts the 16 rows r = 64 kc + 16 q + e of snapshot
 // i (one 128-B run of the K-tiled fp64 A) and writes 16 bytes per modulus at
 // R_l[kc][i][16 q ..]: a wave covers 16 snapshots x 64 rows = 1 KB contiguous per modulus.
-__global__ __launch_bounds__(256) void k_residues(const double* __restrict__ AT, int ns, int64_t rowlen,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) void k_residues(const double* __restrict__ AT, int ns, int64_t rowlen,
                                                   int64_t rowpad, const double* __restrict__ mean,
                                                   const double* __restrict__ devmax, int bbits, int64_t kc0,
                                                   int64_t nkc, int8_t* __restrict__ R, int64_t lstride) {
@@ -160,42 +160,63 @@ __global__ __launch_bounds__(256) void k_residues(const double* __restrict__ AT,
   }
   const int sg = scale_exp(*devmax, bbits);
   // z = a' + 2^52 in [0, 2^53] as five 11-bit limbs z_k, held as exact f32
-  f32x2 F[5][8];
+  float Fs[5][16];
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const double z = rint(ldexp(a[e], sg)) + 0x1p52;
     const double h = floor(z * 0x1p-32);
     const uint32_t lo = (uint32_t)__builtin_fma(-h, 0x1p32, z), hi = (uint32_t)h;
-    const uint32_t zk[5] = {lo & 0x7FFu, (lo >> 11) & 0x7FFu, __builtin_amdgcn_alignbit(hi, lo, 22) & 0x7FFu,
-                            (hi >> 1) & 0x7FFu, hi >> 12};
-#pragma unroll
-    for (int k = 0; k < 5; ++k) F[k][e >> 1][e & 1] = (float)zk[k];
+    Fs[0][e] = (float)(lo & 0x7FFu);
+    Fs[1][e] = (float)((lo >> 11) & 0x7FFu);
+    Fs[2][e] = (float)(((lo >> 22) | (hi << 10)) & 0x7FFu);
+    Fs[3][e] = (float)((hi >> 1) & 0x7FFu);
+    Fs[4][e] = (float)(hi >> 12);
   }
+  f32x2 F[5][8];
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+#pragma unroll
+    for (int pr = 0; pr < 8; ++pr) F[k][pr] = (f32x2){Fs[k][2 * pr], Fs[k][2 * pr + 1]};
   const uint32_t doff = (uint32_t)((kcl * ns + i) * 64 + q * 16);  // < lstride < 4 GB
-  // per modulus m: s = sum_k z_k (2^11k mod m) + (-2^52 mod m) < 2^21.4, exact in f32; the f32
-  // quotient s * fl(1/m) is within 2^-23 * 2^13.9 < 1/(2m) of s / m, and s / m (m odd) is never
-  // within 1/(2m) of a half-integer, so rint gives the balanced residue s - m rint(s/m) exactly
+  // per modulus m: s = sum_k z_k (2^11k mod m) + (-2^52 mod m) < 2^21.4, exact in f32.  The
+  // quotient q = rint(s / m) comes from one fma, s * fl(1/m) + 1.5 * 2^23, rounded once to an
+  // integer: |s fl(1/m) - s/m| <= (s/m) 2^-24 < 2^-10 < 1/(2m), and s/m (m odd) is never within
+  // 1/(2m) of a half-integer, so it is exact; r = s - q m is the balanced residue, and
+  // r + 1.5 * 2^23 holds r's two's-complement byte in its low mantissa bits (|r| <= 127)
   sfor<0, NMOD>([&](auto L) {
     constexpr int l = decltype(L)::value;
     constexpr float m = (float)kT.m[l], inv = 1.0f / (float)kT.m[l], o = (float)kT.off[l];
     constexpr float c1 = (float)kT.p11[l][1], c2 = (float)kT.p11[l][2], c3 = (float)kT.p11[l][3],
                     c4 = (float)kT.p11[l][4];
+    constexpr float MAG = 12582912.0f;  // 1.5 * 2^23
+    // stage by stage over the 8 element pairs: independent packed ops back to back (no nops)
+    f32x2 sv[8];
+#pragma unroll
+    for (int pr = 0; pr < 8; ++pr) sv[pr] = __builtin_elementwise_fma(F[1][pr], (f32x2){c1, c1}, F[0][pr]);
+#pragma unroll
+    for (int pr = 0; pr < 8; ++pr) sv[pr] = __builtin_elementwise_fma(F[2][pr], (f32x2){c2, c2}, sv[pr]);
+#pragma unroll
+    for (int pr = 0; pr < 8; ++pr) sv[pr] = __builtin_elementwise_fma(F[3][pr], (f32x2){c3, c3}, sv[pr]);
+#pragma unroll
+    for (int pr = 0; pr < 8; ++pr) sv[pr] = __builtin_elementwise_fma(F[4][pr], (f32x2){c4, c4}, sv[pr]);
+#pragma unroll
+    for (int pr = 0; pr < 8; ++pr) sv[pr] = sv[pr] + (f32x2){o, o};
+    f32x2 qv[8];
+#pragma unroll
+    for (int pr = 0; pr < 8; ++pr) qv[pr] = __builtin_elementwise_fma(sv[pr], (f32x2){inv, inv}, (f32x2){MAG, MAG});
+#pragma unroll
+    for (int pr = 0; pr < 8; ++pr) qv[pr] = qv[pr] - (f32x2){MAG, MAG};
+#pragma unroll
+    for (int pr = 0; pr < 8; ++pr) sv[pr] = __builtin_elementwise_fma(-qv[pr], (f32x2){m, m}, sv[pr]);
+#pragma unroll
+    for (int pr = 0; pr < 8; ++pr) sv[pr] = sv[pr] + (f32x2){MAG, MAG};
     uint32_t w[4];
 #pragma unroll
     for (int pq = 0; pq < 4; ++pq) {
-      uint32_t half[2];
-#pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {
-        const int pr = pq * 2 + h2;
-        f32x2 sv = __builtin_elementwise_fma(F[1][pr], (f32x2){c1, c1}, F[0][pr]);
-        sv = __builtin_elementwise_fma(F[2][pr], (f32x2){c2, c2}, sv);
-        sv = __builtin_elementwise_fma(F[3][pr], (f32x2){c3, c3}, sv);
-        sv = __builtin_elementwise_fma(F[4][pr], (f32x2){c4, c4}, sv) + (f32x2){o, o};
-        const f32x2 qv = __builtin_elementwise_roundeven(sv * (f32x2){inv, inv});
-        const f32x2 rv = __builtin_elementwise_fma(-qv, (f32x2){m, m}, sv);
-        half[h2] = __builtin_amdgcn_perm((uint32_t)(int)rv[1], (uint32_t)(int)rv[0], 0x0C0C0400u);
-      }
-      w[pq] = half[0] | (half[1] << 16);
+      const f32x2 u = sv[2 * pq], v = sv[2 * pq + 1];
+      const uint32_t h0 = __builtin_amdgcn_perm(__float_as_uint(u.y), __float_as_uint(u.x), 0x0C0C0400u);
+      const uint32_t h1 = __builtin_amdgcn_perm(__float_as_uint(v.y), __float_as_uint(v.x), 0x0C0C0400u);
+      w[pq] = h0 | (h1 << 16);
     }
     int8_t* base = R + (int64_t)l * lstride;  // uniform: a scalar base + 32-bit offset store
     *reinterpret_cast<uint4*>(base + doff) = make_uint4(w[0], w[1], w[2], w[3]);
@@ -267,6 +288,9 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int n
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = (i32x4){0, 0, 0, 0};
   const int wr = wave >> 2, wc = wave & 3;
+  // a diagonal tile's waves (0, 2) and (0, 3) hold rows 0-127 x columns 128-255: strictly upper,
+  // never stored -- they only load their share of the panel
+  const bool idle = SAME && wr == 0 && wc >= 2;
   const int fo = (lane & 15) * KC + (((lane >> 4) ^ swz((lane >> 2) & 3)) * 16);  // row lane&15, slot lane>>4
   auto read = [&](int t, i32x4 (&av)[8], i32x4 (&bv)[4]) {
     const char* st = smem + (t % NST) * STG;
@@ -311,7 +335,7 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int n
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   i32x4 a0[8], b0[4], a1[8], b1[4];
-  read(0, a0, b0);
+  if (!idle) read(0, a0, b0);
   auto step = [&](int t, const i32x4 (&ac)[8], const i32x4 (&bc)[4], i32x4 (&an)[8], i32x4 (&bn)[4]) {
     if (t + 1 < nt) {
       if (t + D < nt) wait_vm<Q * (D - 1)>();
@@ -320,6 +344,7 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int n
       __builtin_amdgcn_sched_barrier(0);
       if (t + D + 1 < nt) issue(t + D + 1);
     }
+    if (idle) return;
     mma_rows(ac, bc, 0);
     __builtin_amdgcn_sched_barrier(0);
     if (t + 1 < nt) read(t + 1, an, bn);
