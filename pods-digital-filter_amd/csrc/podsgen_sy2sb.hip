@@ -1450,7 +1450,8 @@ hipError_t syevd2_chase(int n, double* ws, const SyevdPlan& p, uint32_t* flags, 
   int cus = 256, dev = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const int P = std::max(1, std::min(q1 - q0, cus));
+  int P = std::max(1, std::min(q1 - q0, cus));
+  if (const char* cp = std::getenv("PODS_CHASE_P")) P = std::max(1, std::min(P, std::atoi(cp)));  // A/B runs
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sb::k_sbtrd_win<B, GW>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)SW::lds_bytes);
   if (e != hipSuccess) return e;
