@@ -18,6 +18,7 @@
 //
 // FMA is requested explicitly (the file is built with -ffp-contract=off like the others).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <mutex>
 #include <vector>
@@ -1321,7 +1322,7 @@ static hipError_t launch_trd_t(const TrdArgs& a, hipStream_t st) {
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_trd<R, S, K, SG, SL>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  e = check_persistent(reinterpret_cast<const void*>(&k_trd<R, S, K, SG, SL>), TT, lds, a.G);
+  e = check_persistent(reinterpret_cast<const void*>(&k_trd<R, S, K, SG, SL>), TT, lds, a.G, st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_trd<R, S, K, SG, SL>), dim3(a.G), dim3(TT), lds, st, a);
   return hipGetLastError();
@@ -1333,7 +1334,21 @@ bool persistent_grid_fits(int blocks_per_cu, int cus, int64_t grid) {
   return blocks_per_cu > 0 && cus > 0 && grid <= (int64_t)blocks_per_cu * cus;
 }
 
-hipError_t check_persistent(const void* fn, int block, size_t lds, int64_t grid) {
+// CUs a stream may use: the popcount of its CU mask (a stream made by
+// hipExtStreamCreateWithCUMask), else the device's CU count
+int stream_cus(hipStream_t st) {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  if (!st) return cus;
+  uint32_t m[16] = {};
+  int n = 0;
+  if (hipExtStreamGetCUMask(st, 16, m) == hipSuccess)
+    for (int i = 0; i < 16; ++i) n += __builtin_popcount(m[i]);
+  return (n > 0 && n < cus) ? n : cus;
+}
+
+hipError_t check_persistent(const void* fn, int block, size_t lds, int64_t grid, hipStream_t st) {
   struct Key {
     const void* fn;
     int block;
@@ -1363,6 +1378,7 @@ hipError_t check_persistent(const void* fn, int block, size_t lds, int64_t grid)
     std::lock_guard<std::mutex> g(mu);
     cache.push_back(Key{fn, block, lds, dev, per, cus});
   }
+  if (st) cus = std::min(cus, stream_cus(st));
   return persistent_grid_fits(per, cus, grid) ? hipSuccess : hipErrorCooperativeLaunchTooLarge;
 }
 
@@ -1522,7 +1538,7 @@ hipError_t launch_back_transform(const double* V, int64_t ldv, const double* tau
                             : reinterpret_cast<const void*>(&eig::k_bt_fused<64>);
   e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  e = check_persistent(fn, 256, lds, G);
+  e = check_persistent(fn, 256, lds, G, st);
   if (e != hipSuccess) return e;
   if (CR == 16)
     hipLaunchKernelGGL(eig::k_bt_fused<16>, dim3(G), dim3(256), lds, st, V, ldv, (const double*)Tg, n,

@@ -11,7 +11,10 @@ namespace pods {
 // resident at once.  check_persistent asks the occupancy API (cached per kernel and LDS size)
 // and returns hipErrorCooperativeLaunchTooLarge when grid > blocks per CU x CUs, before launch.
 bool persistent_grid_fits(int blocks_per_cu, int cus, int64_t grid);
-hipError_t check_persistent(const void* fn, int block, size_t lds, int64_t grid);
+// st: the stream the grid goes to -- a stream created with a CU mask (hipExtStreamCreateWithCUMask)
+// offers only its masked CUs (stream_cus)
+hipError_t check_persistent(const void* fn, int block, size_t lds, int64_t grid, hipStream_t st = nullptr);
+int stream_cus(hipStream_t st);
 
 hipError_t launch_mt_jump(const uint32_t* src, const int* src_idx, const uint32_t* polys,
                           const int* poly_idx, uint32_t* dst, const int* dst_idx, int njobs,

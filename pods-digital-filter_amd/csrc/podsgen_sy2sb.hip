@@ -1377,7 +1377,7 @@ hipError_t syevd2_panels(int n, double* ws, const SyevdPlan& p, uint32_t* flags,
       if (e == hipSuccess) e = hipMemsetAsync(ptrace, 0, (B * 8 + 1) * sizeof(int64_t), st);
       if (e != hipSuccess) return e;
     }
-    e = check_persistent(reinterpret_cast<const void*>(&sb::k_pqr<B>), 256, 0, NW);
+    e = check_persistent(reinterpret_cast<const void*>(&sb::k_pqr<B>), 256, 0, NW, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(sb::k_pqr<B>, dim3(NW), dim3(256), 0, st, Aw, (int64_t)n, r0, c0, m, RP, NW,
                        ws + p.off_pub, pflags, epoch * 1024u + (uint32_t)pi, 16u * (uint32_t)pi + 1u, abortw, Vx,
@@ -1447,15 +1447,13 @@ hipError_t syevd2_chase(int n, double* ws, const SyevdPlan& p, uint32_t* flags, 
   if (q1 <= q0) return hipSuccess;
   uint32_t* abortw = flags + 64;
   uint32_t* prog = flags + 128;
-  int cus = 256, dev = 0;
-  (void)hipGetDevice(&dev);
-  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int cus = std::max(1, stream_cus(st));  // a CU-masked stream offers only its CUs
   int P = std::max(1, std::min(q1 - q0, cus));
   if (const char* cp = std::getenv("PODS_CHASE_P")) P = std::max(1, std::min(P, std::atoi(cp)));  // A/B runs
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sb::k_sbtrd_win<B, GW>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)SW::lds_bytes);
   if (e != hipSuccess) return e;
-  e = check_persistent(reinterpret_cast<const void*>(&sb::k_sbtrd_win<B, GW>), SW::NT, SW::lds_bytes, P);
+  e = check_persistent(reinterpret_cast<const void*>(&sb::k_sbtrd_win<B, GW>), SW::NT, SW::lds_bytes, P, st);
   if (e != hipSuccess) return e;
   // PODS_SBWIN_TRACE=q0: per-step timestamps of groups q0 .. q0+3 (diagnostics, stderr)
   const char* wts = std::getenv("PODS_SBWIN_TRACE");
