@@ -274,7 +274,7 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int n
   auto issue = [&](int t) {
     if constexpr (DIAG == 2) return;
     const uint32_t sb = lds0 + (uint32_t)((t % NST) * STG);
-    const int8_t* g = base + (int64_t)t * cstride;
+    const int8_t* g = base + (int64_t)(DIAG >= 3 ? (t & 7) : t) * cstride;  // DIAG 3/4: an L2-resident K window
 #pragma unroll
     for (int q = 0; q < 2; ++q) dma16(g + xo[q], sb + (wave * 2 + q) * 1024);
     if constexpr (!SAME) {
@@ -304,7 +304,7 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int n
   auto mma_rows = [&](const i32x4 (&av)[8], const i32x4 (&bv)[4], int a0) {
 #pragma unroll
     for (int a = a0; a < a0 + 4; ++a) {
-      if constexpr (DIAG == 1) {
+      if constexpr (DIAG == 1 || DIAG == 4) {
         acc[a][0] += av[a] ^ bv[a & 3];
       } else {
 #pragma unroll
@@ -634,11 +634,13 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
   int variant = 4;
   if (const char* v = std::getenv("PODS_SYRK_I8")) {
     if (v[0] == '5') variant = 5;
-    if (v[0] == '9') variant = v[1] == 'm' ? 91 : 92;
+    if (v[0] == '9') variant = v[1] == 'm' ? 91 : v[1] == 'w' ? 93 : v[1] == 'x' ? 94 : 92;
   }
   const void* fn = variant == 5 ? reinterpret_cast<const void*>(&k_syrk_i8<5>)
                  : variant == 91 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 1>)
                  : variant == 92 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 2>)
+                 : variant == 93 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 3>)
+                 : variant == 94 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 4>)
                                  : reinterpret_cast<const void*>(&k_syrk_i8<4>);
   const size_t lds = (size_t)(variant == 5 ? 5 : 4) * 2 * PANEL;
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
