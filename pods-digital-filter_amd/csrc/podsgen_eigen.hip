@@ -437,17 +437,30 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
     // slab loads run SPF row groups ahead
     constexpr int SPF = K == 0 ? 0 : 3;  // range 0: no registers to spare (depth 2 measured no faster)
     double slab[SG > 0 ? RL : 1][SG > 0 ? SG : 1];
+    // slab slots (L2): a wave whose 64 columns of slot m all lie below j holds nothing live
+    // there any more (x, p and v_{j-1} are zero on them), so its slab loads and stores go out of
+    // the buffer's range (a buffer load then returns 0 and a store is dropped, with no memory
+    // access and no branch) -- exact, and range 0 moves half its slab traffic on average
+    const __amdgpu_buffer_rsrc_t rwm = __builtin_amdgcn_make_buffer_rsrc(Wg, 0, S * R * TT * 8, 0x00020000);
+    // per slot: the lane's byte offset (out of range when dead) in a VGPR, the (slot, row) part
+    // as the instruction's scalar offset
+    int soff[SG > 0 ? SG : 1];
+#pragma unroll
+    for (int m = 0; m < (SG > 0 ? SG : 1); ++m) soff[m] = TT * (K + m) + 64 * wv + 63 < j ? 0x40000000 : t * 8;
+    auto slab_ld = [&](int m, int i) -> double {
+      return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rwm, soff[m - K], (m * R + i) * TT * 8, 0));
+    };
 #pragma unroll
     for (int ii = 0; ii < (SG > 0 ? SPF * RH : 0); ++ii)
 #pragma unroll
-      for (int m = K; m < K + SG; ++m) slab[ii][m - K] = wm(m, I0 + ii, t);
+      for (int m = K; m < K + SG; ++m) slab[ii][m - K] = slab_ld(m, I0 + ii);
 #pragma unroll
     for (int h = 0; h < RL / RH; ++h) {
 #pragma unroll
       for (int ii = (h + SPF) * RH; ii < (SG > 0 ? (h + SPF + 1) * RH : 0); ++ii)
         if (ii < RL)
 #pragma unroll
-          for (int m = K; m < K + SG; ++m) slab[ii][m - K] = wm(m, I0 + ii, t);
+          for (int m = K; m < K + SG; ++m) slab[ii][m - K] = slab_ld(m, I0 + ii);
       double acc[RH], colv[RH];
 #pragma unroll
       for (int q = 0; q < RH; ++q) acc[q] = 0.0;
@@ -529,8 +542,11 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
         for (int q = 0; q < RH; ++q) {
           const int ii = h * RH + q;
           if (m < K + SG) {
-            double& ref = wm(m, I0 + ii, t);
-            ref = __builtin_fma(-vr[q], p[m], __builtin_fma(-wr[q], vp[m], ref));
+            const int so = (m * R + I0 + ii) * TT * 8;
+            const double ref = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rwm, soff[m - K], so, 0));
+            const double nv = __builtin_fma(-vr[q], p[m], __builtin_fma(-wr[q], vp[m], ref));
+            __builtin_amdgcn_raw_buffer_store_b64(
+                __builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(rwm, 0, 0, 0)), nv), rwm, soff[m - K], so, 0);
           } else if (m < K + SG + SL) {
             double& ref = Al[((m - K - SG) * RL + ii) * TT + t];
             ref = __builtin_fma(-vr[q], p[m], __builtin_fma(-wr[q], vp[m], ref));
