@@ -1420,7 +1420,9 @@ int trd_plan(int n, int* R, int* G, int64_t* slab_doubles) {
 // one slot stays in the (L2-resident) slab there; later ranges hold everything on chip.
 // Range 1 (14 rows x 7 slots) keeps all of it in VGPRs + LDS even though the compiler then
 // spills ~100 VGPRs of loop-invariant state: 5.43 ms against 6.25 ms with a slab slot,
-// whose mixed load/store traffic serialises every row group on a full vmcnt drain.
+// whose mixed load/store traffic serialises every row group on a full vmcnt drain (r4, with
+// the slab through buffer ops and its dead columns skipped: 6.44 against 5.49 ms, spills
+// 104 -> 48; range 0 gained from the same change, 8.07 -> 7.62 ms).
 hipError_t launch_trd(const TrdArgs& a, int R, hipStream_t st) { return launch_trd_ranges(a, R, 0, 7, st); }
 
 // Column ranges kb..ke (inclusive, clipped to klast) of the tridiagonalisation: each range is
