@@ -354,7 +354,10 @@ def main():
                     "unit": "TOP/s", "frac": round(achieved / I8_MFMA_PEAK_TOPS, 4), "traffic": traffic,
                     "launch_ms": round(kern_ms, 3), "ops_per_launch": ops, "launches": k_n.value,
                     "corr_stage_ms": round(corr_ms, 3),
-                    "corr_fp64_equiv_tflops": round(flops / (corr_ms * 1e-3) / 1e12, 2)}
+                    "corr_fp64_equiv_tflops": round(flops / (corr_ms * 1e-3) / 1e12, 2),
+                    "bound_note": ("the int8 pipe is fed by LDS-DMA: 214 GB L2->LDS per launch at C3; measured "
+                                   "floors (DESIGN.md s3): MFMAs alone 16.9 ms (the chip holds ~1.94 GHz under "
+                                   "this load), operand traffic alone 16.3 ms from an L2-resident window")}
     else:
         achieved = flops / (corr_ms * 1e-3) / 1e12
         roofline = {"kernel": "pods_corr (k_syrk_g128 + k_syrk_reduce), rank 0",
