@@ -56,8 +56,18 @@ def write(f, arrays, nm, period, num_points):
 if __name__ == "__main__":
     src, dst = sys.argv[1], sys.argv[2]
     meta = np.load(os.path.join(src, "meta.npy"))
+    lazy = os.path.exists(os.path.join(src, "spatial.npy"))
+    if lazy:  # modes assembled one at a time from the grid points and the spatial modes
+        points = np.load(os.path.join(src, "points.npy"), mmap_mode="r")
+        spatial = np.load(os.path.join(src, "spatial.npy"), mmap_mode="r")
 
     def arrays(name, i=None):
+        if name == "mode" and lazy:
+            P = points.shape[0]
+            m = np.empty((P, 6), dtype=np.float64)
+            m[:, 0:3] = points
+            m[:, 3:] = np.asarray(spatial[:, i]).reshape((P, 3), order="F")
+            return m
         fn = name + ("_%04d" % i if i is not None else "") + ".npy"
         return np.load(os.path.join(src, fn), mmap_mode="r")
     with h5py.File(dst, "w") as f:
@@ -83,13 +93,15 @@ def _h5py_python():
 def write_HDF5(i_d, filename="PODFS/PODFS.hdf5"):
     """HDF5.py:11-64.  With h5py in this interpreter the datasets are written directly, one
     after the other; otherwise each array goes to its own .npy file and a Python with h5py
-    memory-maps them and writes dataset by dataset (the modes stream through one at a time,
-    nothing holds the whole payload twice -- config 5 writes 20 modes of 6 x 1 M doubles)."""
+    memory-maps them and writes dataset by dataset.  The modes stream through one at a time:
+    i_d.modes (PODFS.ModeStack) builds mode i from the grid points and the spatial modes on
+    demand, and the writer does the same from points.npy + spatial.npy, so neither side holds
+    the (nm, P, 6) array (1 GB at config 5: 20 modes of 6 x 1 M doubles)."""
     d = os.path.dirname(filename)
     if d:
         os.makedirs(d, exist_ok=True)
     nm, P = int(i_d.nm), int(i_d.num_points)
-    modes = np.asarray(i_d.modes, dtype=np.float64)
+    modes = i_d.modes  # indexed one mode at a time: a PODFS.ModeStack is never materialised whole
     try:
         import h5py
     except ImportError:
@@ -100,7 +112,8 @@ def write_HDF5(i_d, filename="PODFS/PODFS.hdf5"):
         src = dict(N_FC=np.asarray(i_d.N_FC), FC=np.asarray(i_d.FC, dtype=np.float64),
                    mean=np.asarray(i_d.mean, dtype=np.float64))
         with h5py.File(filename, "w") as f:
-            ns_["write"](f, lambda name, i=None: modes[i] if name == "mode" else src[name], nm, i_d.period, P)
+            ns_["write"](f, lambda name, i=None: np.asarray(modes[i], dtype=np.float64) if name == "mode" else src[name],
+                         nm, i_d.period, P)
         return filename
     exe = _h5py_python()
     if exe is None:
@@ -111,8 +124,13 @@ def write_HDF5(i_d, filename="PODFS/PODFS.hdf5"):
         np.save(os.path.join(tmp, "N_FC.npy"), np.asarray(i_d.N_FC))
         np.save(os.path.join(tmp, "FC.npy"), np.asarray(i_d.FC, dtype=np.float64))
         np.save(os.path.join(tmp, "mean.npy"), np.asarray(i_d.mean, dtype=np.float64))
-        for i in range(nm):
-            np.save(os.path.join(tmp, "mode_%04d.npy" % i), modes[i])
+        if hasattr(modes, "spatial") and hasattr(modes, "points"):
+            # the writer assembles each mode from these two (no (nm, P, 6) copy on either side)
+            np.save(os.path.join(tmp, "points.npy"), modes.points)
+            np.save(os.path.join(tmp, "spatial.npy"), np.asarray(modes.spatial, dtype=np.float64))
+        else:
+            for i in range(nm):
+                np.save(os.path.join(tmp, "mode_%04d.npy" % i), np.asarray(modes[i], dtype=np.float64))
         script = os.path.join(tmp, "writer.py")
         with open(script, "w") as f:
             f.write(_WRITER)

@@ -338,6 +338,40 @@ def _prf_rows(points, u):
                    for j in range(points.shape[0]))
 
 
+class ModeStack:
+    """i_d.modes of the reference (mode i = [x y z | u v w] per point, PODFS.py:1745-1747) without
+    the (nm, P, 6) array: mode i is built from the grid points and column i of the spatial modes
+    when asked for.  np.asarray(stack) still gives the whole array."""
+
+    def __init__(self, points, spatial_modes, nm):
+        self.points = np.asarray(points, dtype=np.float64)
+        self.spatial = spatial_modes
+        self.nm = int(nm)
+
+    def __len__(self):
+        return self.nm
+
+    @property
+    def shape(self):
+        return (self.nm, self.points.shape[0], 6)
+
+    def __getitem__(self, i):
+        if not isinstance(i, (int, np.integer)):
+            return np.asarray(self)[i]
+        if not -self.nm <= i < self.nm:
+            raise IndexError(i)
+        i = int(i) % self.nm
+        P = self.points.shape[0]
+        m = np.empty((P, 6), dtype=np.float64)
+        m[:, 0:3] = self.points
+        m[:, 3:] = np.asarray(self.spatial[:, i]).reshape((P, 3), order="F")
+        return m
+
+    def __array__(self, dtype=None, copy=None):
+        a = np.stack([self[i] for i in range(self.nm)]) if self.nm else np.zeros(self.shape)
+        return a if dtype is None else a.astype(dtype, copy=False)
+
+
 def pod2prf(i_d):
     """PODFS_mean.prf and PODFS_mode_####.prf; i_d.mean / i_d.modes for the HDF5 writer."""
     rdir = "./PODFS/"
@@ -349,7 +383,9 @@ def pod2prf(i_d):
     points = i_d.grid.points
     if i_d.hdf5:
         i_d.mean = np.zeros((num_points, 6), dtype=np.float64)
-        i_d.modes = np.zeros((num_modes, num_points, 6), dtype=np.float64)
+        # the reference fills a (nm, P, 6) array here (PODFS.py:1671-1672, 1 GB at C5); the
+        # writer only ever needs one mode at a time, so the modes are assembled on demand
+        i_d.modes = ModeStack(points, i_d.spatial_modes, num_modes)
     u = np.asarray(i_d.mean_field).reshape((num_points, 3), order="F")
     if i_d.hdf5:
         i_d.mean[:, 0:3] = points
@@ -364,9 +400,6 @@ def pod2prf(i_d):
     for i in range(num_modes):
         counter = "%4.4i" % (i + 1)
         um = i_d.spatial_modes[:, i].reshape((num_points, 3), order="F")
-        if i_d.hdf5:
-            i_d.modes[i, :, 0:3] = points
-            i_d.modes[i, :, 3:] = um
         with open(rdir + "PODFS_mode_" + counter + ".prf", "w") as f:
             f.write(_prf_header("PODFS_mode_" + counter, n, 0 * n[0] + 0 * n[1] + 0 * n[2]))
             f.write(_prf_rows(points, um))

@@ -285,6 +285,61 @@ def test_hdf5_layout(tmp_path):
     assert out[2].startswith("['mode_0001', 'mode_0002']")
 
 
+def test_mode_stack_matches_reference_fill():
+    """PODFS.ModeStack gives the array the reference fills (PODFS.py:1671-1672, :1745-1747)."""
+    import PODFS
+    rng = np.random.default_rng(2)
+    P, nm = 7, 3
+    points = rng.standard_normal((P, 3))
+    spatial = rng.standard_normal((3 * P, nm))
+    want = np.zeros((nm, P, 6))
+    for i in range(nm):
+        want[i, :, 0:3] = points
+        want[i, :, 3:] = spatial[:, i].reshape((P, 3), order="F")
+    st = PODFS.ModeStack(points, spatial, nm)
+    assert len(st) == nm and st.shape == want.shape
+    for i in range(nm):
+        assert np.array_equal(st[i], want[i])
+    assert np.array_equal(st[-1], want[-1]) and np.array_equal(np.asarray(st), want)
+    with pytest.raises(IndexError):
+        st[nm]
+
+
+@pytest.mark.skipif(_h5py_python() is None, reason="no interpreter with h5py")
+def test_hdf5_streamed_modes_identical(tmp_path):
+    """The writer fed a ModeStack (modes rebuilt per mode from points + spatial modes) writes the
+    same datasets as from the materialised (nm, P, 6) array."""
+    import HDF5
+    import PODFS
+    rng = np.random.default_rng(4)
+    P, nm = 11, 3
+    points = rng.standard_normal((P, 3))
+    spatial = rng.standard_normal((3 * P, nm))
+
+    class I:
+        pass
+    files = []
+    for lazy in (True, False):
+        i_d = I()
+        i_d.nm, i_d.period, i_d.num_points = nm, 0.25, P
+        i_d.N_FC = np.array([1, 2, 1])
+        i_d.FC = rng.standard_normal((4, 3)) if lazy else files_fc
+        files_fc = i_d.FC
+        i_d.mean = np.arange(6 * P, dtype=np.float64).reshape(P, 6)
+        st = PODFS.ModeStack(points, spatial, nm)
+        i_d.modes = st if lazy else np.asarray(st)
+        fn = str(tmp_path / ("lazy.h5" if lazy else "full.h5"))
+        HDF5.write_HDF5(i_d, fn)
+        files.append(fn)
+    reader = ("import h5py, numpy as np, sys\n"
+              "a, b = (h5py.File(x, 'r')['main'] for x in sys.argv[1:3])\n"
+              "ok = all(np.array_equal(a['modes'][k][:], b['modes'][k][:]) for k in b['modes'])\n"
+              "ok = ok and sorted(a['modes']) == sorted(b['modes']) and np.array_equal(a['FC'][:], b['FC'][:])\n"
+              "print('same' if ok else 'differ', len(a['modes']))\n")
+    out = subprocess.run([_h5py_python(), "-c", reader] + files, capture_output=True, text=True)
+    assert out.stdout.split() == ["same", str(nm)], out.stderr
+
+
 def _gloo_worker(rank, world, port, A, out):
     """One rank of the product's multi-GPU host path on gloo/CPU tensors:
     engine.allreduce_correlation (packed lower-triangle all-reduce, divide, mirror) and
