@@ -747,6 +747,7 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
       if (pods::corr_i8_plan(ns, c->rowlen, c->rowpad, budget, &c->i8_plan, force) != 0)
         return fail(PODS_ERR_UNSUPPORTED, "pods_corr: K too large for the int8 correlation (PODS_CORR=f64)");
       const std::vector<int> items = pods::corr_i8_items(ns, c->i8_plan);
+      c->i8_plan.nitems = (int)(items.size() / 4);  // the order decides the (padded) item count
       PODS_HIP(ensure(c->i8_items, items.size() * sizeof(int)));
       PODS_HIP(hipMemcpy(c->i8_items.p, items.data(), items.size() * sizeof(int), hipMemcpyHostToDevice));
       c->i8_key = key;

@@ -405,25 +405,36 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8(const int8_t* __restrict__ R
 }
 
 // ---- CRT reconstruction ----------------------------------------------------------------------
-// 16 residues c_l in [0, m_l) -> the integer X in (-M/2, M/2) with X = c_l mod m_l, as a double
+// 16 residues 0 <= c_l < 2^16 -> the integer X in [-(M-1)/2, (M-1)/2] with X = c_l mod m_l, as a double
 __device__ __forceinline__ double crt_value(const int (&c)[NMOD]) {
-  int v[NMOD];
+  // Garner's digits kept balanced, v_l in [-(m_l-1)/2, (m_l-1)/2], in f32: every operand is
+  // an integer below 2^17, the quotient rint(x/m) is one fma with 1.5*2^23 (error <= 2^-15,
+  // far below 1/(2m); the argument of k_residues), so each step is exact.  With balanced
+  // digits Horner gives the signed X directly (|X| <= (M-1)/2).
+  constexpr float MAG = 12582912.0f;
+  float v[NMOD];
   sfor<0, NMOD>([&](auto L) {
     constexpr int l = decltype(L)::value;
-    constexpr int ml = kT.m[l];
-    int t = c[l];
+    constexpr float ml = (float)kT.m[l], rm = 1.0f / (float)kT.m[l];
+    float t = (float)c[l];
+    {  // balance c_l itself
+      const float q = __builtin_fmaf(t, rm, MAG) - MAG;
+      t = __builtin_fmaf(-q, ml, t);
+    }
     sfor<0, l>([&](auto K) {
       constexpr int k = decltype(K)::value;
-      constexpr int ik = kT.inv[k][l];
-      t = ((t + ml - v[k] % ml) * ik) % ml;
+      constexpr float ik = (float)kT.inv[k][l];
+      const float x = (t - v[k]) * ik;  // |x| < 2^16.1, exact
+      const float q = __builtin_fmaf(x, rm, MAG) - MAG;
+      t = __builtin_fmaf(-q, ml, x);
     });
     v[l] = t;
   });
-  unsigned __int128 X = (unsigned)v[NMOD - 1];
+  __int128 X = (__int128)(int)v[NMOD - 1];
 #pragma unroll
-  for (int l = NMOD - 2; l >= 0; --l) X = X * (unsigned)kT.m[l] + (unsigned)v[l];
-  const bool neg = X > (kM >> 1);
-  const unsigned __int128 mag = neg ? kM - X : X;
+  for (int l = NMOD - 2; l >= 0; --l) X = X * kT.m[l] + (int)v[l];
+  const bool neg = X < 0;
+  const unsigned __int128 mag = neg ? (unsigned __int128)(-X) : (unsigned __int128)X;
   const uint64_t hi = (uint64_t)(mag >> 64), lo = (uint64_t)mag;
   double d;
   if (hi == 0) {
@@ -481,7 +492,7 @@ __global__ __launch_bounds__(256) void k_crt(const uint8_t* __restrict__ P, int 
           const int sh = 16 * (k >> 1);
           sfor<0, NMOD>([&](auto Lm) {
             constexpr int l = decltype(Lm)::value;
-            cr[l] = (int)((((k & 1) ? od[l] : ev[l]) >> sh) & 0xFFFFu) % kT.m[l];
+            cr[l] = (int)((((k & 1) ? od[l] : ev[l]) >> sh) & 0xFFFFu);  // < 2^16: crt_value reduces
           });
           double v = ldexp(crt_value(cr), -2 * sg);
           if (divide) v = v / dn;
@@ -568,6 +579,30 @@ std::vector<int> corr_i8_items(int ns, const CorrI8Plan& p) {
   // PODS_CORR_ORDER (A/B runs): "m" = plain Morton order, no XCD groups; "x" = plain Morton order
   // with every XCD given a contiguous range of the whole grid (kernel-side remap)
   const char* ord = std::getenv("PODS_CORR_ORDER");
+  if (!ord || ord[0] == 'g') {
+    // default: XCD lane x (grid position 8k + x; nitems is a multiple of 8) takes split x % S
+    // and Morton group x / S of the 8 / S groups, so an XCD's concurrent workgroups all read one
+    // K range of one modulus, on a compact block of tiles (S in {1, 2, 4, 8})
+    if (8 % p.nsplit == 0) {
+      const int ngrp = 8 / p.nsplit, gsz = (tiles + ngrp - 1) / ngrp;
+      std::vector<int> out;
+      out.reserve((size_t)8 * gsz * 4);
+      for (int k = 0; k < gsz; ++k)
+        for (int x = 0; x < 8; ++x) {
+          const int sp = x % p.nsplit, grp = x / p.nsplit, idx = grp * gsz + k;
+          if (idx < tiles && k < gsz) {
+            out.push_back(t[idx].second.first);
+            out.push_back(t[idx].second.second);
+          } else {
+            out.push_back(-1);
+            out.push_back(-1);
+          }
+          out.push_back(sp);
+          out.push_back(0);
+        }
+      return out;
+    }
+  }
   if (ord && ord[0] == 's') {  // measurement only (wrong results): every item is tile (1, 0)
     std::vector<int> out;
     for (int s = 0; s < p.nsplit; ++s)

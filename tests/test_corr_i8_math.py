@@ -77,24 +77,35 @@ def test_residue_arithmetic_exact():
 
 
 def crt_like_kernel(c):
-    """c: 16 residues in [0, m_l) -> the integer X in (-M/2, M/2] (Garner + Horner, as k_crt)."""
+    """c: 16 residues -> the integer X in [-(M-1)/2, (M-1)/2], k_crt's way: Garner's digits kept
+    balanced and computed in f32 (x = (t - v_k) * inv, q = fl32(x * fl32(1/m) + 1.5 * 2^23) - 1.5 * 2^23,
+    t = x - q m; every operand an integer below 2^17, so each step is exact), then a signed Horner."""
     v = []
     for l, ml in enumerate(MODULI):
-        t = c[l]
+        rm = f32(1.0 / ml)
+
+        def bal(x):
+            q = float(f32(float(x) * float(rm) + MAG)) - MAG   # fma: exact product, one rounding
+            assert q == round(x / ml)
+            return int(x - q * ml)
+
+        t = bal(c[l])
         for k in range(l):
-            t = ((t + ml - v[k] % ml) * pow(MODULI[k], -1, ml)) % ml
+            x = (t - v[k]) * pow(MODULI[k], -1, ml)
+            assert abs(x) < 2 ** 17
+            t = bal(x)
+        assert abs(t) <= (ml - 1) // 2
         v.append(t)
     X = v[-1]
     for l in range(14, -1, -1):
         X = X * MODULI[l] + v[l]
-    M = math.prod(MODULI)
-    return X - M if X > M // 2 else X
+    return X
 
 
 def test_crt_roundtrip():
     rng = np.random.default_rng(5)
     M = math.prod(MODULI)
-    vals = [0, 1, -1, M // 2, -(M // 2) + 1, 2 ** 123, -(2 ** 123)]
+    vals = [0, 1, -1, (M - 1) // 2, -((M - 1) // 2), 2 ** 123, -(2 ** 123)]
     vals += [int(x) * (2 ** 70) + int(y) for x, y in zip(rng.integers(-2 ** 53, 2 ** 53, 300),
                                                          rng.integers(0, 2 ** 62, 300))]
     for X in vals:
