@@ -249,7 +249,7 @@ __device__ __forceinline__ int swz(int quartet) { return (0x78 >> (2 * quartet))
 // are read between the two halves of step t's MFMAs.  A diagonal tile (SAME) loads one panel and
 // reads it as both operands.  items: {bi, bj, split, -} (bi < 0: an empty slot that keeps the
 // item count a multiple of 8).  DIAG (measurement only): 1 = no MFMAs, 2 = no operand traffic.
-template <int NST, int DIAG, bool SAME>
+template <int NST, int DIAG, bool SAME, int ILV>
 __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int ns, int nt, int i0, int j0, int m,
                                           char* smem, uint8_t* __restrict__ dst, int ldp, int accumulate) {
   constexpr int STG = 2 * PANEL;
@@ -271,16 +271,17 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int n
   }
   const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
   const int64_t cstride = (int64_t)ns * KC;
-  auto issue = [&](int t) {
+  // piece q of step t's DMA (q < 2: the row panel, 2-3: the column panel)
+  auto piece = [&](int t, int q) {
     if constexpr (DIAG == 2) return;
     const uint32_t sb = lds0 + (uint32_t)((t % NST) * STG);
     const int8_t* g = base + (int64_t)(DIAG >= 3 ? (t & 7) : t) * cstride;  // DIAG 3/4: an L2-resident K window
+    if (q < 2) dma16(g + xo[q], sb + (wave * 2 + q) * 1024);
+    else dma16(g + yo[q - 2], sb + PANEL + (wave * 2 + q - 2) * 1024);
+  };
+  auto issue = [&](int t) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) dma16(g + xo[q], sb + (wave * 2 + q) * 1024);
-    if constexpr (!SAME) {
-#pragma unroll
-      for (int q = 0; q < 2; ++q) dma16(g + yo[q], sb + PANEL + (wave * 2 + q) * 1024);
-    }
+    for (int q = 0; q < Q; ++q) piece(t, q);
   };
   i32x4 acc[8][4];
 #pragma unroll
@@ -301,7 +302,10 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int n
 #pragma unroll
     for (int b = 0; b < 4; ++b) bv[b] = *reinterpret_cast<const i32x4*>(Y + b * 16 * KC);
   };
-  auto mma_rows = [&](const i32x4 (&av)[8], const i32x4 (&bv)[4], int a0) {
+  // the MFMA rows a0 .. a0+3; with dt >= 0, DMA piece qb + k / qs of step dt after row a0 + k for
+  // every k that is a multiple of qs (ILV variants: the pieces go among the MFMAs instead of back
+  // to back after the barrier, where every wave of the CU would issue them at once)
+  auto mma_rows = [&](const i32x4 (&av)[8], const i32x4 (&bv)[4], int a0, int dt, int qb, int qs) {
 #pragma unroll
     for (int a = a0; a < a0 + 4; ++a) {
       if constexpr (DIAG == 1 || DIAG == 4) {
@@ -309,6 +313,14 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int n
       } else {
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[a], bv[b], acc[a][b], 0, 0, 0);
+      }
+      if constexpr (ILV != 0) {
+        const int k = a - a0;
+        if (dt >= 0 && k % qs == 0 && qb + k / qs < Q) {
+          __builtin_amdgcn_sched_barrier(0);
+          piece(dt, qb + k / qs);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
     }
   };
@@ -326,7 +338,9 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int n
   // step t: every wave waits for stage t+1, one barrier, the DMA of stage t + D + 1 into the
   // slot of step t - 1 (read during step t - 1's MFMAs, consumed by them), then step t's MFMAs
   // with the reads of step t+1 between their halves -- the wait the compiler puts at the loop
-  // head (lgkmcnt(0)) then finds those reads long complete
+  // head (lgkmcnt(0)) then finds those reads long complete.  With ILV the DMA pieces go among
+  // the MFMA rows: issued back to back right after the barrier, all 8 waves of the CU stall on
+  // them at once (an LDS-DMA issue costs ~60-185 cycles) while the MFMA pipes idle
 #pragma unroll
   for (int t = 0; t <= D; ++t)
     if (t < nt) issue(t);
@@ -336,20 +350,25 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int n
   __builtin_amdgcn_sched_barrier(0);
   i32x4 a0[8], b0[4], a1[8], b1[4];
   if (!idle) read(0, a0, b0);
+  // ILV: 0 = the DMA pieces of step t + D + 1 back to back after the barrier; 1 = one after each
+  // of the first Q MFMA rows; 2 = after every second row over both halves; 4 = after the rows of
+  // the second half (behind the reads of step t + 1)
   auto step = [&](int t, const i32x4 (&ac)[8], const i32x4 (&bc)[4], i32x4 (&an)[8], i32x4 (&bn)[4]) {
     if (t + 1 < nt) {
       if (t + D < nt) wait_vm<Q * (D - 1)>();
       else wait_vm<0>();
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      if (t + D + 1 < nt) issue(t + D + 1);
+      if (ILV == 0 || idle)
+        if (t + D + 1 < nt) issue(t + D + 1);
     }
     if (idle) return;
-    mma_rows(ac, bc, 0);
+    const int dt = ILV != 0 && t + D + 1 < nt ? t + D + 1 : -1;
+    mma_rows(ac, bc, 0, ILV == 4 ? -1 : dt, 0, ILV == 2 ? 2 : 1);
     __builtin_amdgcn_sched_barrier(0);
     if (t + 1 < nt) read(t + 1, an, bn);
     __builtin_amdgcn_sched_barrier(0);
-    mma_rows(ac, bc, 4);
+    mma_rows(ac, bc, 4, ILV == 2 || ILV == 4 ? dt : -1, ILV == 2 ? 2 : 0, ILV == 2 ? 2 : 1);
     fold(t);
   };
   int t = 0;
@@ -380,7 +399,7 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int n
       }
 }
 
-template <int NST, int DIAG = 0>
+template <int NST, int DIAG = 0, int ILV = 0>
 __global__ __launch_bounds__(512, 1) void k_syrk_i8(const int8_t* __restrict__ R, int ns, int64_t lstride, int kcs,
                                                     const int4* __restrict__ items, int nitems, int nsplit,
                                                     uint8_t* __restrict__ P, int64_t pslab, int ldp, int accumulate,
@@ -399,9 +418,9 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8(const int8_t* __restrict__ R
   uint8_t* dst = P + (int64_t)(l * nsplit + sp) * pslab;
   const int m = modulus(l);
   if (bi == bj)
-    syrk_tile<NST, DIAG, true>(base, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
+    syrk_tile<NST, DIAG, true, ILV>(base, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
   else
-    syrk_tile<NST, DIAG, false>(base, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
+    syrk_tile<NST, DIAG, false, ILV>(base, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
 }
 
 // ---- CRT reconstruction ----------------------------------------------------------------------
@@ -664,20 +683,33 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
                           double* C, int64_t ldc, int divide, hipStream_t st, hipEvent_t syrk_begin,
                           hipEvent_t syrk_end) {
   using namespace i8;
-  // PODS_SYRK_I8 (A/B runs): "4" / "5" ring stages (default 4); "9m" / "9d": the 4-stage kernel
-  // without MFMAs / without operand traffic (measurement only, wrong results)
-  int variant = 4;
+  // default: 5 ring stages, each wave's DMA pieces one after each of its first MFMA rows (ILV 1;
+  // 22.0-22.8 ms at C3 against 24.0 for the pieces back to back after the barrier,
+  // profiles/r4/corr_i8_ilv_ab.log).  PODS_SYRK_I8 (A/B runs): "4" / "5" ring stages with the
+  // pieces after the barrier; "i1" / "i2" / "i4": 4 stages, ILV 1 / 2 / 4; "i6" / "i7": 5 stages,
+  // ILV 2 / 4; "9m" / "9d" / "9w" / "9x" / "9y": measurement only (wrong results): no MFMAs / no
+  // operand traffic / an L2-resident K window / both / the window with ILV 1
+  int variant = 45;
   if (const char* v = std::getenv("PODS_SYRK_I8")) {
+    if (v[0] == '4') variant = 4;
     if (v[0] == '5') variant = 5;
-    if (v[0] == '9') variant = v[1] == 'm' ? 91 : v[1] == 'w' ? 93 : v[1] == 'x' ? 94 : 92;
+    if (v[0] == 'i') variant = 40 + (v[1] ? v[1] - '0' : 1);
+    if (v[0] == '9') variant = v[1] == 'm' ? 91 : v[1] == 'w' ? 93 : v[1] == 'x' ? 94 : v[1] == 'y' ? 95 : 92;
   }
   const void* fn = variant == 5 ? reinterpret_cast<const void*>(&k_syrk_i8<5>)
                  : variant == 91 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 1>)
                  : variant == 92 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 2>)
                  : variant == 93 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 3>)
                  : variant == 94 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 4>)
+                 : variant == 41 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 0, 1>)
+                 : variant == 42 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 0, 2>)
+                 : variant == 44 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 0, 4>)
+                 : variant == 95 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 3, 1>)
+                 : variant == 45 ? reinterpret_cast<const void*>(&k_syrk_i8<5, 0, 1>)
+                 : variant == 46 ? reinterpret_cast<const void*>(&k_syrk_i8<5, 0, 2>)
+                 : variant == 47 ? reinterpret_cast<const void*>(&k_syrk_i8<5, 0, 4>)
                                  : reinterpret_cast<const void*>(&k_syrk_i8<4>);
-  const size_t lds = (size_t)(variant == 5 ? 5 : 4) * 2 * PANEL;
+  const size_t lds = (size_t)(variant == 5 || variant >= 45 && variant <= 47 ? 5 : 4) * 2 * PANEL;
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   const int64_t lstride = p.chunks * ns * KC;
