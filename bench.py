@@ -90,7 +90,7 @@ CORR_NMOD = 16  # residue SYRKs per correlation (podsgen_corr_i8.hip NMOD)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--seed", type=int, default=12345)

@@ -39,6 +39,7 @@ struct ModTables {
   int p18[NMOD], p36[NMOD];  // 2^18, 2^36 mod m
   int off[NMOD];             // -(2^52) mod m
   int p11[NMOD][5];          // 2^(11 k) mod m
+  int p14[NMOD][4];          // 2^(14 k) mod m, balanced to [-(m-1)/2, (m-1)/2]
   int inv[NMOD][NMOD];       // inv[k][l] = m_k^-1 mod m_l (k != l)
 };
 constexpr int pow2mod(int e, int m) {
@@ -62,6 +63,10 @@ constexpr ModTables make_tables() {
     t.p36[l] = pow2mod(36, mm[l]);
     t.off[l] = (mm[l] - pow2mod(52, mm[l])) % mm[l];
     for (int k = 0; k < 5; ++k) t.p11[l][k] = pow2mod(11 * k, mm[l]);
+    for (int k = 0; k < 4; ++k) {
+      const int c = pow2mod(14 * k, mm[l]);
+      t.p14[l][k] = c > mm[l] / 2 ? c - mm[l] : c;
+    }
   }
   for (int l = 0; l < NMOD; ++l)
     for (int k = 0; k < NMOD; ++k) t.inv[k][l] = k == l ? 0 : invmod(mm[k], mm[l]);
@@ -132,10 +137,14 @@ __global__ __launch_bounds__(256) void k_absdev(const double* __restrict__ AT, i
 // Thread (chunk kc, snapshot i, quarter q) converts the 16 rows r = 64 kc + 16 q + e of snapshot
 // i (one 128-B run of the K-tiled fp64 A) and writes 16 bytes per modulus at
 // R_l[kc][i][16 q ..]: a wave covers 16 snapshots x 64 rows = 1 KB contiguous per modulus.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) void k_residues(const double* __restrict__ AT, int ns, int64_t rowlen,
-                                                  int64_t rowpad, const double* __restrict__ mean,
-                                                  const double* __restrict__ devmax, int bbits, int64_t kc0,
-                                                  int64_t nkc, int8_t* __restrict__ R, int64_t lstride) {
+// V: 0 = unsigned 11-bit limbs, 1 = signed 14-bit limbs (two packed ops fewer per element pair
+// and modulus, measured the same: 4.4 ms either way at C3, whatever the occupancy cap or with
+// nontemporal stores -- the kernel is bound by its 19.3 GB of mostly-write HBM traffic, 4.4 TB/s)
+template <int V>
+__device__ __forceinline__ void residues_body(const double* __restrict__ AT, int ns, int64_t rowlen,
+                                              int64_t rowpad, const double* __restrict__ mean,
+                                              const double* __restrict__ devmax, int bbits, int64_t kc0,
+                                              int64_t nkc, int8_t* __restrict__ R, int64_t lstride) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int q = (int)(t & 3);
   const int64_t rest = t >> 2;
@@ -159,6 +168,71 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) voi
     for (int e = 0; e < 16; ++e) a[e] = 0.0;
   }
   const int sg = scale_exp(*devmax, bbits);
+  const uint32_t doff = (uint32_t)((kcl * ns + i) * 64 + q * 16);  // < lstride < 4 GB
+  // the byte of r + 1.5 * 2^23 (|r| <= 127) is r's two's-complement byte: pack 16 of them
+  auto store16 = [&](const f32x2 (&sv)[8], int l) {
+    uint32_t w[4];
+#pragma unroll
+    for (int pq = 0; pq < 4; ++pq) {
+      const f32x2 u = sv[2 * pq], v = sv[2 * pq + 1];
+      const uint32_t h0 = __builtin_amdgcn_perm(__float_as_uint(u.y), __float_as_uint(u.x), 0x0C0C0400u);
+      const uint32_t h1 = __builtin_amdgcn_perm(__float_as_uint(v.y), __float_as_uint(v.x), 0x0C0C0400u);
+      w[pq] = h0 | (h1 << 16);
+    }
+    int8_t* base = R + (int64_t)l * lstride;  // uniform: a scalar base + 32-bit offset store
+    *reinterpret_cast<uint4*>(base + doff) = make_uint4(w[0], w[1], w[2], w[3]);
+  };
+  constexpr float MAG = 12582912.0f;  // 1.5 * 2^23
+  if constexpr (V == 1) {
+    // a' as four SIGNED 14-bit limbs, split in fp64 (every step exact): h = rint(a' 2^-28),
+    // lo = a' - h 2^28 (|lo| <= 2^27), d3 = rint(h 2^-14), d2 = h - d3 2^14, d1 = rint(lo 2^-14),
+    // d0 = lo - d1 2^14: |d0|, |d1|, |d2| <= 2^13, |d3| <= 2^10.  Per modulus, with the balanced
+    // c_k = 2^14k mod m (|c_k| <= 127): s = d0 + c1 d1 + c2 d2 + c3 d3, |s| < 2^21.1, exact in
+    // f32; q = rint(s / m) by one fma with 1.5 * 2^23 (|s fl(1/m) - s/m| <= 2^21.1 / 181 * 2^-24
+    // < 2^-10.3 < 1/(2m), and s/m is never within 1/(2m) of a half-integer), r = s - q m.  Seven
+    // packed ops per element pair and modulus (nine with unsigned 11-bit limbs + the offset).
+    f32x2 F[4][8];
+#pragma unroll
+    for (int e = 0; e < 16; e += 2) {
+      float d[4][2];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const double ap = rint(ldexp(a[e + h2], sg));
+        const double hh = rint(ap * 0x1p-28);
+        const double lo = __builtin_fma(-hh, 0x1p28, ap);
+        const double d3 = rint(hh * 0x1p-14), d1 = rint(lo * 0x1p-14);
+        d[3][h2] = (float)d3;
+        d[2][h2] = (float)__builtin_fma(-d3, 0x1p14, hh);
+        d[1][h2] = (float)d1;
+        d[0][h2] = (float)__builtin_fma(-d1, 0x1p14, lo);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) F[k][e / 2] = (f32x2){d[k][0], d[k][1]};
+    }
+    sfor<0, NMOD>([&](auto L) {
+      constexpr int l = decltype(L)::value;
+      constexpr float m = (float)kT.m[l], inv = 1.0f / (float)kT.m[l];
+      constexpr float c1 = (float)kT.p14[l][1], c2 = (float)kT.p14[l][2], c3 = (float)kT.p14[l][3];
+      f32x2 sv[8];
+#pragma unroll
+      for (int pr = 0; pr < 8; ++pr) sv[pr] = __builtin_elementwise_fma(F[1][pr], (f32x2){c1, c1}, F[0][pr]);
+#pragma unroll
+      for (int pr = 0; pr < 8; ++pr) sv[pr] = __builtin_elementwise_fma(F[2][pr], (f32x2){c2, c2}, sv[pr]);
+#pragma unroll
+      for (int pr = 0; pr < 8; ++pr) sv[pr] = __builtin_elementwise_fma(F[3][pr], (f32x2){c3, c3}, sv[pr]);
+      f32x2 qv[8];
+#pragma unroll
+      for (int pr = 0; pr < 8; ++pr) qv[pr] = __builtin_elementwise_fma(sv[pr], (f32x2){inv, inv}, (f32x2){MAG, MAG});
+#pragma unroll
+      for (int pr = 0; pr < 8; ++pr) qv[pr] = qv[pr] - (f32x2){MAG, MAG};
+#pragma unroll
+      for (int pr = 0; pr < 8; ++pr) sv[pr] = __builtin_elementwise_fma(-qv[pr], (f32x2){m, m}, sv[pr]);
+#pragma unroll
+      for (int pr = 0; pr < 8; ++pr) sv[pr] = sv[pr] + (f32x2){MAG, MAG};
+      store16(sv, l);
+    });
+    return;
+  }
   // z = a' + 2^52 in [0, 2^53] as five 11-bit limbs z_k, held as exact f32
   float Fs[5][16];
 #pragma unroll
@@ -177,7 +251,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) voi
   for (int k = 0; k < 5; ++k)
 #pragma unroll
     for (int pr = 0; pr < 8; ++pr) F[k][pr] = (f32x2){Fs[k][2 * pr], Fs[k][2 * pr + 1]};
-  const uint32_t doff = (uint32_t)((kcl * ns + i) * 64 + q * 16);  // < lstride < 4 GB
   // per modulus m: s = sum_k z_k (2^11k mod m) + (-2^52 mod m) < 2^21.4, exact in f32.  The
   // quotient q = rint(s / m) comes from one fma, s * fl(1/m) + 1.5 * 2^23, rounded once to an
   // integer: |s fl(1/m) - s/m| <= (s/m) 2^-24 < 2^-10 < 1/(2m), and s/m (m odd) is never within
@@ -188,7 +261,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) voi
     constexpr float m = (float)kT.m[l], inv = 1.0f / (float)kT.m[l], o = (float)kT.off[l];
     constexpr float c1 = (float)kT.p11[l][1], c2 = (float)kT.p11[l][2], c3 = (float)kT.p11[l][3],
                     c4 = (float)kT.p11[l][4];
-    constexpr float MAG = 12582912.0f;  // 1.5 * 2^23
     // stage by stage over the 8 element pairs: independent packed ops back to back (no nops)
     f32x2 sv[8];
 #pragma unroll
@@ -210,18 +282,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) voi
     for (int pr = 0; pr < 8; ++pr) sv[pr] = __builtin_elementwise_fma(-qv[pr], (f32x2){m, m}, sv[pr]);
 #pragma unroll
     for (int pr = 0; pr < 8; ++pr) sv[pr] = sv[pr] + (f32x2){MAG, MAG};
-    uint32_t w[4];
-#pragma unroll
-    for (int pq = 0; pq < 4; ++pq) {
-      const f32x2 u = sv[2 * pq], v = sv[2 * pq + 1];
-      const uint32_t h0 = __builtin_amdgcn_perm(__float_as_uint(u.y), __float_as_uint(u.x), 0x0C0C0400u);
-      const uint32_t h1 = __builtin_amdgcn_perm(__float_as_uint(v.y), __float_as_uint(v.x), 0x0C0C0400u);
-      w[pq] = h0 | (h1 << 16);
-    }
-    int8_t* base = R + (int64_t)l * lstride;  // uniform: a scalar base + 32-bit offset store
-    *reinterpret_cast<uint4*>(base + doff) = make_uint4(w[0], w[1], w[2], w[3]);
+    store16(sv, l);
   });
 }
+
+#define PODS_RES_ARGS const double* __restrict__ AT, int ns, int64_t rowlen, int64_t rowpad, \
+    const double* __restrict__ mean, const double* __restrict__ devmax, int bbits, int64_t kc0, int64_t nkc, \
+    int8_t* __restrict__ R, int64_t lstride
+#define PODS_RES_PASS AT, ns, rowlen, rowpad, mean, devmax, bbits, kc0, nkc, R, lstride
+template <int V>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) void k_residues(PODS_RES_ARGS) {
+  residues_body<V>(PODS_RES_PASS);
+}
+#undef PODS_RES_ARGS
+#undef PODS_RES_PASS
 
 // ---- the int8 SYRK -----------------------------------------------------------------------
 
@@ -720,8 +794,22 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
   for (int li = 0; li < p.nlaunch; ++li) {
     const int64_t kc0 = (int64_t)li * p.chunks;
     const int64_t thr = p.chunks * ns * 4;
-    hipLaunchKernelGGL(k_residues, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, st, AT, ns, rowlen, rowpad,
-                       mean, devmax, p.bbits, kc0, p.chunks, R, lstride);
+    // PODS_RES_I8=1 (A/B runs): the signed 14-bit-limb residues (measured the same)
+    const char* rv = std::getenv("PODS_RES_I8");
+    const void* rk = rv && rv[0] == '1' ? reinterpret_cast<const void*>(&k_residues<1>)
+                                        : reinterpret_cast<const void*>(&k_residues<0>);
+    {
+      const double* AT_ = AT;
+      const double* mean_ = mean;
+      const double* dm_ = devmax;
+      int bb_ = p.bbits;
+      int64_t kc_ = kc0, nk_ = p.chunks, ls_ = lstride, rl_ = rowlen, rp_ = rowpad;
+      int ns_ = ns;
+      int8_t* R_ = R;
+      void* rargs[] = {&AT_, &ns_, &rl_, &rp_, &mean_, &dm_, &bb_, &kc_, &nk_, &R_, &ls_};
+      e = hipLaunchKernel(rk, dim3((unsigned)((thr + 255) / 256)), dim3(256), rargs, 0, st);
+      if (e != hipSuccess) return e;
+    }
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     // the events bracket the SYRK launch (with several launches: the first residue pass to the last SYRK)

@@ -4,7 +4,8 @@ tests/test_gpu_corr_i8.py):
 
   * the 16 moduli are pairwise coprime, their product M lies in [2^124, 2^125), and the
     precision b the plan picks keeps 2 K 2^2b < M for every BASELINE K (C3, C4, C5 slabs);
-  * k_residues' f32 arithmetic: five 11-bit limbs of z = a' + 2^52, s = sum z_k (2^11k mod m)
+  * k_residues' f32 arithmetic (k_residues<1>: four signed 14-bit limbs split in fp64 and balanced
+    coefficients, see residues_signed_limbs_like_kernel; k_residues<0>): five 11-bit limbs of z = a' + 2^52, s = sum z_k (2^11k mod m)
     + (-2^52 mod m) < 2^24, q = fl32(s * fl32(1/m) + 1.5 * 2^23) - 1.5 * 2^23 = rint(s / m)
     exactly, and the low byte of fl32(s - q m + 1.5 * 2^23) is the balanced residue;
   * k_crt: Garner's mixed-radix digits and Horner give back any integer |X| < M / 2 from its
@@ -63,6 +64,46 @@ def residues_like_kernel(a):
         rb = (r + f32(MAG)).astype(np.float32)
         out[li] = (rb.view(np.uint32) & 0xFF).astype(np.uint8).view(np.int8)
     return out
+
+
+def residues_signed_limbs_like_kernel(a):
+    """k_residues<1>: a' (|a'| <= 2^52) as four signed 14-bit limbs split in fp64, balanced
+    c_k = 2^14k mod m, s = d0 + c1 d1 + c2 d2 + c3 d3 in f32, the same quotient / byte steps."""
+    ap = a.astype(np.float64)
+    hh = np.rint(ap * 2.0 ** -28)
+    lo = ap - hh * 2.0 ** 28            # exact (fma in the kernel; here every term fits in 53 bits)
+    d3 = np.rint(hh * 2.0 ** -14)
+    d1 = np.rint(lo * 2.0 ** -14)
+    d = [lo - d1 * 2.0 ** 14, d1, hh - d3 * 2.0 ** 14, d3]
+    assert max(float(np.max(np.abs(x))) for x in d[:3]) <= 2 ** 13 and float(np.max(np.abs(d3))) <= 2 ** 10
+    F = [x.astype(np.float32) for x in d]
+    out = np.empty((16, a.size), dtype=np.int8)
+    for li, m in enumerate(MODULI):
+        c = [pow(2, 14 * k, m) for k in range(4)]
+        c = [x - m if x > m // 2 else x for x in c]
+        s = F[0]
+        for k in range(1, 4):
+            s = (s.astype(np.float64) + F[k].astype(np.float64) * c[k]).astype(np.float32)  # exact
+        assert float(np.max(np.abs(s))) < 2 ** 21.1
+        inv = f32(1.0 / m)
+        q = (s.astype(np.float64) * np.float64(inv) + MAG).astype(np.float32) - f32(MAG)
+        assert np.array_equal(q.astype(np.float64), np.rint(s.astype(np.float64) / m))
+        r = (s.astype(np.float64) - q.astype(np.float64) * m).astype(np.float32)
+        rb = (r + f32(MAG)).astype(np.float32)
+        out[li] = (rb.view(np.uint32) & 0xFF).astype(np.uint8).view(np.int8)
+    return out
+
+
+def test_residue_signed_limbs_exact():
+    rng = np.random.default_rng(9)
+    a = np.concatenate([rng.integers(-(1 << 52), (1 << 52) + 1, 200000, dtype=np.int64),
+                        np.array([0, 1, -1, 1 << 52, -(1 << 52), (1 << 27) + 8191, -(1 << 41) - 1],
+                                 dtype=np.int64)])
+    got = residues_signed_limbs_like_kernel(a)
+    for li, m in enumerate(MODULI):
+        want = np.array([int(x) % m for x in a], dtype=np.int64)
+        want = np.where(want > m // 2, want - m, want)
+        assert np.array_equal(got[li].astype(np.int64), want), m
 
 
 def test_residue_arithmetic_exact():
