@@ -356,8 +356,9 @@ def main():
                     "corr_stage_ms": round(corr_ms, 3),
                     "corr_fp64_equiv_tflops": round(flops / (corr_ms * 1e-3) / 1e12, 2),
                     "bound_note": ("the int8 pipe is fed by LDS-DMA: 214 GB L2->LDS per launch at C3; measured "
-                                   "floors (DESIGN.md s3): MFMAs alone 16.9 ms (the chip holds ~1.94 GHz under "
-                                   "this load), operand traffic alone 16.3 ms from an L2-resident window")}
+                                   "(DESIGN.md s3): MFMAs alone 16.9 ms (the chip holds ~1.7-1.94 GHz under "
+                                   "this load), the kernel with an L2-resident K window 19.3 ms; MFMA pipe "
+                                   "busy 66 % of the real kernel")}
     else:
         achieved = flops / (corr_ms * 1e-3) / 1e12
         roofline = {"kernel": "pods_corr (k_syrk_g128 + k_syrk_reduce), rank 0",
