@@ -415,7 +415,7 @@ __global__ __launch_bounds__(256) void k_filter_x(const double* __restrict__ R,
 // that enters the window at step i is loaded PD steps ahead (a register queue), so each wave
 // keeps PD loads in flight instead of waiting for one load per step (the compiler issued the
 // step's load and then drained vmcnt(0) before its last tap).
-template <int NX, int PD>
+template <int NX, int PD, bool NT = false>
 __global__ __launch_bounds__(256) void k_filter_x2(const double* __restrict__ R,
                                                    const double* __restrict__ bx, int ns,
                                                    int64_t Sl, int steps_per_chunk,
@@ -436,25 +436,37 @@ __global__ __launch_bounds__(256) void k_filter_x2(const double* __restrict__ R,
   const double2* R2 = reinterpret_cast<const double2*>(R);
   double2* T2 = reinterpret_cast<double2*>(T1);
   double2 w[NX];
+  // NT (A/B): nontemporal plane loads and T1 stores (each byte is touched once here)
+  typedef double f64x2_nt __attribute__((ext_vector_type(2)));
+  auto ldR = [&](int64_t idx) -> double2 {
+    if constexpr (NT) {
+      const f64x2_nt v = __builtin_nontemporal_load(reinterpret_cast<const f64x2_nt*>(R2 + idx));
+      return make_double2(v.x, v.y);
+    } else {
+      return R2[idx];
+    }
+  };
 #pragma unroll
-  for (int a = 0; a < NX - 1; ++a) w[a] = R2[stream_plane(c, i0 + a, NX) * Sl2 + pp];
+  for (int a = 0; a < NX - 1; ++a) w[a] = ldR(stream_plane(c, i0 + a, NX) * Sl2 + pp);
   // pf[d] = the plane entering the window at step i + d (planes up to i1 + NX - 2 exist)
   double2 pf[PD];
 #pragma unroll
   for (int d = 0; d < PD; ++d)
-    pf[d] = i0 + d < i1 ? R2[stream_plane(c, i0 + d + NX - 1, NX) * Sl2 + pp] : make_double2(0.0, 0.0);
+    pf[d] = i0 + d < i1 ? ldR(stream_plane(c, i0 + d + NX - 1, NX) * Sl2 + pp) : make_double2(0.0, 0.0);
   for (int i = i0; i < i1; ++i) {
     w[NX - 1] = pf[0];
 #pragma unroll
     for (int d = 0; d < PD - 1; ++d) pf[d] = pf[d + 1];
-    if (i + PD < i1) pf[PD - 1] = R2[stream_plane(c, i + PD + NX - 1, NX) * Sl2 + pp];
+    if (i + PD < i1) pf[PD - 1] = ldR(stream_plane(c, i + PD + NX - 1, NX) * Sl2 + pp);
     double ax = 0.0, ay = 0.0;
 #pragma unroll
     for (int a = 0; a < NX; ++a) {
       ax = ax + w[a].x * b[a];
       ay = ay + w[a].y * b[a];
     }
-    T2[((int64_t)c * ns + i) * Sl2 + pp] = make_double2(ax, ay);
+    if constexpr (NT)
+      __builtin_nontemporal_store((f64x2_nt){ax, ay}, reinterpret_cast<f64x2_nt*>(T2 + ((int64_t)c * ns + i) * Sl2 + pp));
+    else T2[((int64_t)c * ns + i) * Sl2 + pp] = make_double2(ax, ay);
 #pragma unroll
     for (int a = 0; a < NX - 1; ++a) w[a] = w[a + 1];
   }
@@ -1259,8 +1271,18 @@ static hipError_t launch_fx(const double* R, const double* bx, int ns, int64_t S
     const int nch = (ns + chunk2 - 1) / chunk2;
     const int64_t nvb = bx_ * ncomp * nch;
     const int64_t grid = nvb;
-    hipLaunchKernelGGL((k_filter_x2<NX, 8>), dim3((unsigned)grid), dim3(256), 0, st, R, bx, ns, Sl, chunk2, T1,
-                       (int)bx_, ncomp, nch);
+    // nontemporal plane loads / T1 stores: 8.15 vs 8.22 ms of main-stream generation at C3
+    // (bench A/B, r4); PODS_X_NT=0 turns them off
+    static const bool nt = [] {
+      const char* v = std::getenv("PODS_X_NT");
+      return !(v && v[0] == '0');
+    }();
+    if (nt)
+      hipLaunchKernelGGL((k_filter_x2<NX, 8, true>), dim3((unsigned)grid), dim3(256), 0, st, R, bx, ns, Sl, chunk2,
+                         T1, (int)bx_, ncomp, nch);
+    else
+      hipLaunchKernelGGL((k_filter_x2<NX, 8>), dim3((unsigned)grid), dim3(256), 0, st, R, bx, ns, Sl, chunk2, T1,
+                         (int)bx_, ncomp, nch);
     return hipGetLastError();
   }
   const int nch = (ns + chunk - 1) / chunk;
