@@ -783,7 +783,7 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
                  : variant == 46 ? reinterpret_cast<const void*>(&k_syrk_i8<5, 0, 2>)
                  : variant == 47 ? reinterpret_cast<const void*>(&k_syrk_i8<5, 0, 4>)
                                  : reinterpret_cast<const void*>(&k_syrk_i8<4>);
-  const size_t lds = (size_t)(variant == 5 || variant >= 45 && variant <= 47 ? 5 : 4) * 2 * PANEL;
+  const size_t lds = (size_t)(variant == 5 || (variant >= 45 && variant <= 47) ? 5 : 4) * 2 * PANEL;
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   const int64_t lstride = p.chunks * ns * KC;
