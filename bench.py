@@ -186,15 +186,19 @@ def cpu_baseline(J, K, ns, nm=20, budget=20.0):
     est["reconstruct"] = per_it * ns * (0.3 * ns) * nm
     how["reconstruct"] = "%d iterations, x ns * 0.3 ns * nm" % reps
     total = sum(est.values())
-    sample = ("oracle (numpy %s / scipy, reference-faithful Python loops) on %d host cores: generation %s; "
+    used = blas_threads or 1
+    sample = ("oracle (numpy %s / scipy, reference-faithful Python loops) on %d BLAS threads: generation %s; "
               "mean, SYRK np.dot(A.T, A) (%dx%d), dgeev n=%d, spatial modes, DFT of %d modes in full; "
               "reconstruction loop %s; measured in %.1f s"
-              % (np.__version__, cores, how["generate"], P3, ns, ns, nm, how["reconstruct"],
+              % (np.__version__, used, how["generate"], P3, ns, ns, nm, how["reconstruct"],
                  time.perf_counter() - t_all))
-    return {"value": J * K * ns / total / 1e6, "unit": "Mpoints/s", "cores": cores, "kind": "port",
-            "blas_threads": blas_threads,
+    # `cores` = the threads that actually ran: numpy's BLAS/LAPACK pool (the SYRK, dgeev and spatial
+    # stages; OMP_NUM_THREADS caps it at the box's CPU share), the Python loops on one of them
+    return {"value": J * K * ns / total / 1e6, "unit": "Mpoints/s", "cores": used, "kind": "port",
+            "affinity_cores": cores, "blas_threads": blas_threads,
             "threads_note": "Python loops (generation, reconstruction) run on one core; numpy BLAS/LAPACK "
-                            "(SYRK, dgeev, spatial) on its thread pool",
+                            "(SYRK, dgeev, spatial) on its %d-thread pool (%d cores in the affinity mask)"
+                            % (used, cores),
             "sample": sample, "seconds_full_job": round(total, 2),
             "stages_s": {k: round(v, 3) for k, v in est.items()}, "stage_basis": how}
 
@@ -210,6 +214,40 @@ def load_traffic(config, corr_mode):
         return d.get("hbm_bytes_per_launch")
     except Exception:
         return None
+
+
+HBM_PEAK_TBS = 8.0             # MI355X HBM3E (MI355X_MICROARCH.md)
+SURVEY_C3_COMBINED = 6130.0    # the C3 combined roofline with the fp64 SYRK floor (Mpoints/s)
+
+
+def combined_roofline(J, K, ns, ms_per_step, world, corr_mode):
+    """The whole step against the floor of the arithmetic it runs, per stage:
+    generation 24 B/unit (A written once), mean 24 B (A read), residues 72 B (A read, 16 int8
+    residues of 3 components written), spatial modes 24 B (A read) at the HBM peak, and the 16
+    residue SYRKs' int8 ops at the int8 MFMA peak (the fp64 SYRK's flops at the fp64 peak with
+    PODS_CORR=f64, plus the centring's 48 B).  The eigensolve is latency-bound (a per-column
+    cross-CU hop) and has no roofline term; it is excluded, so this floor is optimistic.  A unit is
+    one inlet point at one step (3 fp64 components)."""
+    units = float(J * K * ns)
+    hbm = lambda b: b * units / (HBM_PEAK_TBS * 1e12) * 1e3   # noqa: E731
+    floors = {"generate": hbm(24), "mean": hbm(24), "spatial": hbm(24)}
+    if corr_mode == 1:
+        floors["residues"] = hbm(72)
+        floors["syrk_i8"] = 2.0 * CORR_NMOD * 3 * J * K * ns * (ns + 1) / 2 / (I8_MFMA_PEAK_TOPS * 1e12) * 1e3
+    else:
+        floors["center"] = hbm(48)
+        floors["syrk_f64"] = 3.0 * J * K * ns * (ns + 1) / (FP64_MFMA_PEAK_TFLOPS * 1e12) * 1e3
+    floor_ms = sum(floors.values()) / world
+    value = units / (ms_per_step * 1e-3) / 1e6
+    out = {"floor_ms": round(floor_ms, 3), "floor_mpoints_s": round(units / (floor_ms * 1e-3) / 1e6, 1),
+           "stage_floors_ms": {k: round(v / world, 3) for k, v in floors.items()},
+           "frac": round(floor_ms / ms_per_step, 4),
+           "note": "floor of the arithmetic run (excl. the latency-bound eigensolve) / ms_per_step"}
+    if (J, K, ns) == (256, 256, 4096):
+        out["survey_frac"] = round(value / SURVEY_C3_COMBINED, 4)
+        out["survey_note"] = ("value / SURVEY.md 8(d)'s %.0f Mpoints/s C3 roofline (priced with the fp64 SYRK "
+                              "floor of 42 ms)" % SURVEY_C3_COMBINED)
+    return out
 
 
 def metric_name(config):
@@ -354,7 +392,10 @@ def main():
                     "unit": "TOP/s", "frac": round(achieved / I8_MFMA_PEAK_TOPS, 4), "traffic": traffic,
                     "launch_ms": round(kern_ms, 3), "ops_per_launch": ops, "launches": k_n.value,
                     "corr_stage_ms": round(corr_ms, 3),
-                    "corr_fp64_equiv_tflops": round(flops / (corr_ms * 1e-3) / 1e12, 2),
+                    "corr_fp64_emulated_tflops": round(flops / (corr_ms * 1e-3) / 1e12, 2),
+                    "corr_fp64_emulated_note": ("3P ns (ns+1) fp64-equivalent flop / the corr stage time: the "
+                                                "rate of an exact integer emulation on the int8 pipe, above the "
+                                                "%.1f TFLOP/s fp64 MFMA peak by construction" % FP64_MFMA_PEAK_TFLOPS),
                     "bound_note": ("the int8 pipe is fed by LDS-DMA: 214 GB L2->LDS per launch at C3; measured "
                                    "(DESIGN.md s3): MFMAs alone 16.9 ms (the chip holds ~1.7-1.94 GHz under "
                                    "this load), the kernel with an L2-resident K window 19.3 ms; MFMA pipe "
@@ -401,6 +442,7 @@ def main():
                        "nf": [setup.nfx, setup.nfy, setup.nfz], "parallelism": "row-slab dp%d" % world,
                        "backend": args.backend if world > 1 else None, "dist_world_size": observed_world},
             "roofline": roofline,
+            "combined_roofline": combined_roofline(J, K, ns, ms, world, corr_mode),
             "corr_arithmetic": ("exact: int8-MFMA residue products mod 16 pairwise-coprime moduli + CRT, one "
                                 "rounding to f64 (pods_corr mode 1)" if corr_mode == 1 else
                                 "fp64 MFMA SYRK (pods_corr mode 0)"),

@@ -167,6 +167,13 @@ int pods_get_corr_mode(pods_ctx* ctx, int* mode);
  * cut into several launches the events bracket all of them, residue passes included.) */
 int pods_corr_timing(pods_ctx* ctx, int enable);
 int pods_corr_kernel_ms(pods_ctx* ctx, double* total_ms, int* count);
+/* Host-only: the plan mode 1 would use for ns snapshots of row_len rows (padded to row_pad) under
+ * a residue budget of budget_bytes and force_split K splits (0 = planned).  out[8] = {scale bits
+ * b, launches, K splits, 64-row chunks per split, chunks per launch, residue bytes, partial bytes,
+ * bytes of one modulus' residues per launch (< 2^32: k_residues' offsets are 32-bit)}.
+ * PODS_ERR_UNSUPPORTED when no plan exists (K beyond ~2^43, or ns too large for 32-bit offsets). */
+int pods_corr_i8_plan_query(int ns, int64_t row_len, int64_t row_pad, int64_t budget_bytes, int force_split,
+                            int64_t* out);
 /* x[i] = x[i] / divisor for n doubles on the device. */
 int pods_divide_inplace(pods_ctx* ctx, double* x_dev, int64_t n, double divisor);
 /* The multi-device all-reduce of the partial correlations (PODFS.py:1455 summed over row slabs)

@@ -15,7 +15,9 @@ Same entry points and i_d contract as the reference's PODFS.py (Python 3):
   make_inflow_plane(i_d)                                          PODFS.py:1243-1290
 
 The arithmetic runs on the MI355X through libpodsgen (podsgen/): the correlation matrix
-on fp64 MFMA, the eigensolve with pods_syev (all eigenvalues + the nm leading vectors;
+as exact integer products on the int8 matrix cores (residues of the scaled A - mean modulo 16
+coprime moduli, one int8 SYRK each, the Chinese remainder theorem back to fp64 with one
+rounding; the fp64 MFMA SYRK with PODS_CORR=f64), the eigensolve with pods_syev (all eigenvalues + the nm leading vectors;
 torch.linalg.eigh when the full temporal-mode matrix is requested), the spatial modes and
 the shifted DFT in HIP kernels.  `A` may be the reference's host array (3P, ns) or the
 device-resident snapshots handed over by digitalfilters.main() (podsgen.DeviceSnapshots).

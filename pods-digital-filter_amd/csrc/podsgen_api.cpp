@@ -284,7 +284,17 @@ struct pods_ctx {
   DevBuf devmax;           // max |fl(a - mean)| (k_mean / k_absdev), the int8 path's scale
   bool dev_valid = false;  // devmax belongs to the current snapshots and mean
   DevBuf i8_res, i8_part, i8_items;
-  int64_t i8_key = -1;
+  // the int8 plan's inputs, compared field by field (every one of them changes the plan)
+  struct I8Key {
+    int ns = -1;
+    int64_t rowlen = -1, rowpad = -1, budget = -1;
+    int force = -1;
+    char order = 0;
+    bool operator==(const I8Key& o) const {
+      return ns == o.ns && rowlen == o.rowlen && rowpad == o.rowpad && budget == o.budget && force == o.force &&
+             order == o.order;
+    }
+  } i8_key;
   pods::CorrI8Plan i8_plan{};
   // pods_corr_timing: HIP events around each int8 SYRK launch (the roofline kernel), read back
   // by pods_corr_kernel_ms
@@ -741,9 +751,14 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
     const char* fsp = std::getenv("PODS_CORR_SPLITS");  // tests: a fixed number of K splits
     const int force = fsp ? std::max(0, std::atoi(fsp)) : 0;
     const char* ord = std::getenv("PODS_CORR_ORDER");
-    const int64_t key = ((int64_t)ns << 40) ^ (c->rowpad << 4) ^ (budget >> 20) ^ ((int64_t)force << 58) ^
-                        ((int64_t)(ord ? ord[0] : 0) << 50);
-    if (c->i8_key != key) {
+    pods_ctx::I8Key key;
+    key.ns = ns;
+    key.rowlen = c->rowlen;
+    key.rowpad = c->rowpad;
+    key.budget = budget;
+    key.force = force;
+    key.order = ord ? ord[0] : 0;
+    if (!(c->i8_key == key)) {
       if (pods::corr_i8_plan(ns, c->rowlen, c->rowpad, budget, &c->i8_plan, force) != 0)
         return fail(PODS_ERR_UNSUPPORTED, "pods_corr: K too large for the int8 correlation (PODS_CORR=f64)");
       const std::vector<int> items = pods::corr_i8_items(ns, c->i8_plan);
@@ -822,6 +837,21 @@ int pods_corr_kernel_ms(pods_ctx* c, double* total_ms, int* count) {
   *total_ms = t;
   *count = (int)c->corr_ev_used;
   c->corr_ev_used = 0;
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_corr_i8_plan_query(int ns, int64_t row_len, int64_t row_pad, int64_t budget_bytes, int force_split,
+                            int64_t* out) {
+  PODS_TRY
+  if (!out || ns <= 0 || row_len <= 0 || row_pad < row_len || budget_bytes <= 0)
+    return fail(PODS_ERR_ARG, "pods_corr_i8_plan_query: bad arguments");
+  pods::CorrI8Plan p{};
+  if (pods::corr_i8_plan(ns, row_len, row_pad, budget_bytes, &p, std::max(0, force_split)) != 0)
+    return fail(PODS_ERR_UNSUPPORTED, "pods_corr_i8_plan_query: no int8 plan for this shape");
+  const int64_t v[8] = {p.bbits, p.nlaunch, p.nsplit, p.kcs, p.chunks, p.r_bytes, p.p_bytes,
+                        p.chunks * ns * 64};
+  for (int k = 0; k < 8; ++k) out[k] = v[k];
   return PODS_OK;
   PODS_CATCH
 }

@@ -534,7 +534,10 @@ __device__ __forceinline__ double crt_value(const int (&c)[NMOD]) {
     d = (double)lo;
   } else {
     const int p = 127 - __builtin_clzll(hi);  // top bit of mag
-    const uint64_t top = (uint64_t)(mag >> (p - 63));
+    uint64_t top = (uint64_t)(mag >> (p - 63));
+    // the bits below the top 64 as a sticky bit: (double)top then rounds as the whole 128-bit
+    // value would (the rounding position is bit 10 of top), so C' is rounded to double once
+    top |= (mag << (128 - (p - 63))) != 0 ? 1u : 0u;
     d = ldexp((double)top, p - 63);
   }
   return neg ? -d : d;
@@ -626,6 +629,11 @@ int corr_i8_plan(int ns, int64_t rowlen, int64_t rowpad, int64_t budget_bytes, C
   const int64_t nkc = (rowpad + i8::KC - 1) / i8::KC;
   const int64_t per_chunk = (int64_t)i8::NMOD * ns * i8::KC;  // residue bytes per K chunk
   int64_t cmax = std::max<int64_t>(I8_KSUB * 64, budget_bytes / per_chunk);
+  // k_residues addresses one modulus' residues with a 32-bit offset (< chunks * ns * 64): keep
+  // a launch's chunks below 2^32 / (ns * 64), less the up-to-7 chunks the split rounding adds
+  const int64_t cmax32 = (int64_t)0xFFFFFFFF / ((int64_t)ns * i8::KC) - 8;
+  if (cmax32 < 1) return -1;
+  cmax = std::min(cmax, cmax32);
   p.nlaunch = (int)((nkc + cmax - 1) / cmax);
   const int64_t per_launch = (nkc + p.nlaunch - 1) / p.nlaunch;
   const int nb = (ns + i8::TB - 1) / i8::TB;
@@ -645,10 +653,13 @@ int corr_i8_plan(int ns, int64_t rowlen, int64_t rowpad, int64_t budget_bytes, C
       best = s;
     }
   }
-  p.nsplit = force_split > 0 ? (int)std::min<int64_t>(force_split, per_launch) : best;
+  // a forced split count is capped at 8 like the planner's own: k_crt sums the splits' bytes in
+  // 16-bit fields (<= 257 splits) and the item order deals splits over the 8 XCDs
+  p.nsplit = force_split > 0 ? (int)std::min<int64_t>(std::min(force_split, 8), per_launch) : best;
   best = p.nsplit;
   p.kcs = (int)(((per_launch + best - 1) / best + I8_KSUB - 1) / I8_KSUB * I8_KSUB);
   p.chunks = (int64_t)p.nsplit * p.kcs;  // chunks per launch (zero-padded past rowpad)
+  if (p.chunks * ns * i8::KC > (int64_t)0xFFFFFFFF) return -1;  // the 32-bit residue offsets
   p.nkc = nkc;
   p.nitems = tiles8 * p.nsplit;
   p.r_bytes = (int64_t)i8::NMOD * p.chunks * ns * i8::KC;

@@ -58,6 +58,7 @@ SIGNATURES = {
     "pods_get_corr_mode": (c_int, [c_void_p, c_void_p]),
     "pods_corr_timing": (c_int, [c_void_p, c_int]),
     "pods_corr_kernel_ms": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "pods_corr_i8_plan_query": (c_int, [c_int, c_i64, c_i64, c_i64, c_int, c_void_p]),
     "pods_divide_inplace": (c_int, [c_void_p, c_void_p, c_i64, c_dbl]),
     "pods_pack_lower": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "pods_unpack_lower": (c_int, [c_void_p, c_void_p, c_int, c_dbl, c_void_p]),

@@ -45,21 +45,25 @@ def _require_gpu():
                            "there is no CPU fallback")
 
 
-def shared_device():
-    """More processes than devices on this node (e.g. a gloo run of several ranks on one GPU):
-    their persistent grids must not run at the same time (pods_set_shared_device).
-    PODS_SHARED_DEVICE=0/1 overrides the detection (LOCAL_WORLD_SIZE, else the initialised
-    process group's world size, against the visible device count)."""
+def shared_device(device=0, dist=None):
+    """Does another rank of this job drive the same GPU (e.g. a gloo run of several ranks on one
+    device)?  Their persistent grids must then not run at the same time (pods_set_shared_device).
+    Decided from the devices themselves: every rank contributes (host name, PCI domain / bus /
+    device id) to one all_gather_object, so ranks pinned to one visible GPU each (per-rank
+    HIP_VISIBLE_DEVICES) or spread over nodes are not taken as sharing.  A collective: all ranks
+    call it together (run_pod does, before its first persistent launch).  Without an initialised
+    process group of more than one rank: False.  PODS_SHARED_DEVICE=0/1 overrides."""
     env = os.environ.get("PODS_SHARED_DEVICE")
     if env in ("0", "1"):
         return env == "1"
-    local = os.environ.get("LOCAL_WORLD_SIZE")
-    if local is None:
-        import torch.distributed as dist
-        if not (dist.is_available() and dist.is_initialized()):
-            return False
-        local = dist.get_world_size()
-    return int(local) > max(torch.cuda.device_count(), 1)
+    if dist is None or not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() < 2:
+        return False
+    import socket
+    p = torch.cuda.get_device_properties(device)
+    me = (socket.gethostname(), int(p.pci_domain_id), int(p.pci_bus_id), int(p.pci_device_id))
+    ids = [None] * dist.get_world_size()
+    dist.all_gather_object(ids, me)
+    return sum(1 for x in ids if tuple(x) == me) > 1
 
 
 class Context:
@@ -75,10 +79,19 @@ class Context:
         check(self.lib.pods_create(ctypes.byref(h), self.device), "pods_create")
         self.h = h
         check(self.lib.pods_set_stream(self.h, ctypes.c_void_p(self.stream.cuda_stream)), "pods_set_stream")
-        self.shared = shared_device()
-        if self.shared:
-            check(self.lib.pods_set_shared_device(self.h, 1), "pods_set_shared_device")
+        self.shared = None   # decided by detect_sharing() (the override at once)
+        if os.environ.get("PODS_SHARED_DEVICE") in ("0", "1"):
+            self.detect_sharing(None)
         self._side = None
+
+    def detect_sharing(self, dist):
+        """Once per context, before its first persistent launch in a multi-rank run (collective
+        when `dist` is an initialised group: every rank calls it, see shared_device)."""
+        if self.shared is None:
+            self.shared = shared_device(self.device, dist)
+            if self.shared:
+                check(self.lib.pods_set_shared_device(self.h, 1), "pods_set_shared_device")
+        return self.shared
 
     def corr_mode(self):
         """pods_corr's product arithmetic: 1 = exact int8 modular products + CRT, 0 = fp64 SYRK."""
@@ -426,7 +439,7 @@ class SpectrumQueue:
         cost.append(5.2 * (ns / 8192.0) ** 2)
         return cost
 
-    def __init__(self, ctx, ns, rank=0, world=1, max_slots=16):
+    def __init__(self, ctx, ns, rank=0, world=1, max_slots=None):
         self.ctx, self.ns, self.rank, self.world = ctx, ns, rank, world
         if ns > SYEV_MAX_N:
             self.cost = list(self.UNIT_MS_TWO.get(ns) or self.two_stage_costs(ns))
@@ -448,7 +461,10 @@ class SpectrumQueue:
         self.budget = self.budgets[rank]
         self._seq, self._cur = [], [0.0] * world
         self.credit = 0.0
-        self.max_slots = max_slots
+        # slots in flight: each two-stage slot (ns > 4096) owns a workspace of ~1.5 ns^2 doubles
+        # (3.2 GB at 16384) and keeps its step's C, so a rank that falls behind holds at most two
+        # of them (the oldest is finished before a third begins, _slot); a one-stage slot is small
+        self.max_slots = max_slots if max_slots is not None else (2 if ns > SYEV_MAX_N else 16)
         self.pending = []      # [step, slot, next unit, lam tensor, C]
         # step -> [lam tensor, abort words (pinned, captured on the stream when the spectrum
         # finished), event behind that copy, C until the words were read as 0]
@@ -497,11 +513,35 @@ class SpectrumQueue:
         return self._seq[step]
 
     def _slot(self):
+        """A free slot; when all max_slots are in flight, the oldest spectrum is finished first
+        (its remaining units run now, ahead of their credit) and its slot reused."""
         used = {p[1] for p in self.pending}
         for s in range(self.max_slots):
             if s not in used:
                 return s
-        raise RuntimeError("SpectrumQueue: all %d slots busy" % self.max_slots)
+        self._complete_oldest()
+        return self._slot()
+
+    def _complete_oldest(self):
+        lib = self.ctx.lib
+        rem = ctypes.c_int(0)
+        p = self.pending[0]
+        while True:
+            check(lib.pods_eigvals_advance(self.ctx.h, p[1], 1, ctypes.byref(rem)), "pods_eigvals_advance")
+            self.credit -= self.cost[min(p[2], len(self.cost) - 1)]
+            p[2] += 1
+            if rem.value == 0:
+                break
+        self._retire(p)
+
+    def _retire(self, p):
+        lib = self.ctx.lib
+        check(lib.pods_eigvals_fetch(self.ctx.h, p[1], ptr(p[3])), "pods_eigvals_fetch")
+        slot = p[1]
+        self._finish(p[0], p[3], p[4],
+                     lambda w, slot=slot: check(lib.pods_eigvals_flags_async(self.ctx.h, slot, ptr(w)),
+                                                "pods_eigvals_flags_async"))
+        self.pending.remove(p)
 
     def submit(self, C, timer=None, limit=None):
         """Registers this step's matrix (begins its spectrum when this rank owns the step), adds
@@ -540,12 +580,7 @@ class SpectrumQueue:
             self.credit -= self.cost[min(p[2], len(self.cost) - 1)]
             p[2] += 1
             if rem.value == 0:
-                check(lib.pods_eigvals_fetch(self.ctx.h, p[1], ptr(p[3])), "pods_eigvals_fetch")
-                slot = p[1]
-                self._finish(p[0], p[3], p[4],
-                             lambda w, slot=slot: check(lib.pods_eigvals_flags_async(self.ctx.h, slot, ptr(w)),
-                                                        "pods_eigvals_flags_async"))
-                self.pending.pop(0)
+                self._retire(p)
         if not self.pending:
             self.credit = min(self.credit, self.budget)  # no banking of idle time
 
@@ -750,6 +785,8 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
     ctx, lib = snap.ctx, snap.ctx.lib
     ns = snap.ns
     dist, rank, world = _dist_info(dist)
+    if world > 1:   # every rank is here: decide whether ranks share this GPU (persistent-grid lock)
+        ctx.detect_sharing(dist)
     dev = torch.device("cuda", ctx.device)
     tm = timer or (lambda name: _NullCtx())
     mean = torch.empty(snap.rowlen, dtype=torch.float64, device=dev)

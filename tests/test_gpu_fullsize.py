@@ -14,6 +14,8 @@ RNG at stream offsets up to 885 M doubles.  This module runs the production pipe
         within 1e-12 * max|C| of torch's fp64 A_c^T A_c / ns;
   (iii) eigenvalues: all 4096 within 1e-12 * lambda_0 of torch.linalg.eigh on the same C;
         T sign-aligned within 1e-10 of eigh's scaled vectors (modes with relative gap > 1e-6);
+  (iii') the same POD with the fp64 MFMA SYRK (pods_corr mode 0, which centres A in place)
+        against torch tiles, eigh and the int8 run;
   (iv)  Phi within 1e-10 (per mode, of max|Phi_j|) of torch's A_c T Lambda^-1 / ns;
   (v)   c bit-exact against the oracle DFT (the reference expression) on the same T, and
         c_count / c_ind / FC exactly the oracle's ranking (PODFS.py:1575-1593) for every mode.
@@ -53,13 +55,19 @@ def c3():
 
     A_raw = device_copy()
     pod = E.run_pod(snap, s.nm, keep_C=True)
-    # the default (int8) correlation subtracts the mean while forming its residues and leaves A as
-    # generated; centre it in place now (pods_center, main() :1493-1495) for the checks below
-    podsgen.check(gen.ctx.lib.pods_center(gen.ctx.h), "pods_center")
+    assert torch.equal(device_copy(), A_raw)   # the int8 correlation leaves A as generated
+    # the same POD with the fp64 MFMA SYRK (pods_corr mode 0, PODS_CORR=f64): it centres A in
+    # place first (k_center, main() :1493-1495), as the reference does, so A_c comes from there
+    mode = gen.ctx.corr_mode()
+    gen.ctx.set_corr_mode(0)
+    try:
+        pod64 = E.run_pod(snap, s.nm, keep_C=True)
+    finally:
+        gen.ctx.set_corr_mode(mode)
     A_c = device_copy()
     fo = E.run_fourier(gen.ctx, pod.T, pod.nm, s.ns, s.dt_eff, s.et)
     torch.cuda.synchronize()
-    yield dict(s=s, gen=gen, A_raw=A_raw, A_c=A_c, pod=pod, fo=fo)
+    yield dict(s=s, gen=gen, A_raw=A_raw, A_c=A_c, pod=pod, pod64=pod64, fo=fo)
     gen.ctx.close()
 
 
@@ -100,6 +108,40 @@ def test_c3_correlation_tiles(c3):
         got = C[bi * b:(bi + 1) * b, bj * b:(bj + 1) * b]
         err = float((got - ref).abs().max())
         assert err <= 1e-12 * cmax, (bi, bj, err / cmax)
+
+
+@pytest.mark.timeout(600)
+def test_c3_fp64_syrk_path(c3):
+    """the fp64 MFMA contraction north_star names (pods_corr mode 0,
+    k_syrk_g128 on the in-place-centred A) stays pinned at full size: C exactly symmetric, the
+    sampled tiles within 1e-12 max|C| of torch's fp64 A_c^T A_c / ns and of the int8 path's C, all
+    4096 eigenvalues within 1e-12 lambda_0 of eigh on its own C and of the int8 run's, nm /
+    num_valid the same, T within 1e-10 of the int8 run's (sign-aligned, gap rule)."""
+    pod, p64 = c3["pod"], c3["pod64"]
+    C64, C8 = p64.C, pod.C
+    assert torch.equal(C64, C64.T)
+    assert torch.equal(p64.mean, pod.mean)
+    Ac = c3["A_c"]
+    cmax = float(C64.abs().max())
+    b = 256
+    for bi, bj in [(0, 0), (3, 1), (9, 9), (15, 2), (15, 15)]:
+        X = Ac[:, bi * b:(bi + 1) * b]
+        Y = Ac[:, bj * b:(bj + 1) * b]
+        ref = (X.T @ Y) / NS
+        got = C64[bi * b:(bi + 1) * b, bj * b:(bj + 1) * b]
+        assert float((got - ref).abs().max()) <= 1e-12 * cmax, (bi, bj)
+    assert float((C64 - C8).abs().max()) <= 1e-12 * cmax
+    lam = torch.flip(torch.linalg.eigvalsh(C64), (0,)).cpu().numpy()
+    assert np.max(np.abs(p64.energy - lam)) <= 1e-12 * lam[0]
+    assert np.max(np.abs(p64.energy - pod.energy)) <= 1e-12 * lam[0]
+    assert (p64.nm, p64.num_valid) == (pod.nm, pod.num_valid)
+    T64, T8 = p64.T.cpu().numpy(), pod.T.cpu().numpy()
+    for j in range(pod.nm):
+        gap = min(abs(lam[j] - lam[j - 1]) if j else np.inf, abs(lam[j] - lam[j + 1]))
+        if gap <= 1e-6 * lam[0]:
+            continue
+        sg = np.sign(np.dot(T64[:, j], T8[:, j]))
+        assert np.max(np.abs(sg * T64[:, j] - T8[:, j])) <= 1e-10 * np.max(np.abs(T8[:, j])), j
 
 
 @pytest.mark.timeout(600)

@@ -40,6 +40,41 @@ def test_persistent_grid_rule():
     assert lib.pods_host_persistent_grid_fits(-1, 256, 1) == -1
 
 
+def _i8_plan(ns, rowlen, budget, force=0):
+    from podsgen import _lib
+    lib = _lib.load()
+    out = np.zeros(8, dtype=np.int64)
+    rowpad = (rowlen + 15) // 16 * 16
+    rc = lib.pods_corr_i8_plan_query(ns, rowlen, rowpad, int(budget), force, out.ctypes.data)
+    return rc, dict(zip(("bbits", "nlaunch", "nsplit", "kcs", "chunks", "r_bytes", "p_bytes", "mod_bytes"),
+                        (int(v) for v in out)))
+
+
+@pytest.mark.parametrize("ns,rowlen", [(4096, 196608), (8192, 786432), (2048, 3145728), (16384, 393216),
+                                       (72, 140000), (4096, 24576)])
+@pytest.mark.parametrize("budget_gib", [0.0001, 16, 64, 200])
+def test_corr_i8_plan_offsets_fit_32_bits(ns, rowlen, budget_gib):
+    """k_residues addresses one modulus' residues with 32-bit offsets, so no
+    launch may hold 2^32 bytes per modulus, whatever PODS_CORR_BUDGET_GB says (a 64 GiB budget
+    used to wrap them); the launches cover every K chunk and the plan keeps b = 52 up to C4's K."""
+    rc, p = _i8_plan(ns, rowlen, budget_gib * 2 ** 30)
+    assert rc == 0, p
+    assert p["mod_bytes"] == p["chunks"] * ns * 64 < 2 ** 32
+    assert p["nlaunch"] * p["chunks"] >= -(-rowlen // 64)
+    assert p["r_bytes"] == 16 * p["mod_bytes"]
+    assert 1 <= p["nsplit"] <= 8 and p["nsplit"] * p["kcs"] == p["chunks"]
+    if rowlen <= 786432:
+        assert p["bbits"] == 52
+
+
+@pytest.mark.parametrize("force", [1, 3, 8, 9, 300, 100000])
+def test_corr_i8_plan_forced_splits_capped(force):
+    """a forced split count is capped at 8 (k_crt sums the splits' bytes in
+    16-bit fields; 258 or more used to overflow them)."""
+    rc, p = _i8_plan(4096, 196608, 16 * 2 ** 30, force)
+    assert rc == 0 and p["nsplit"] == min(force, 8)
+
+
 @pytest.mark.parametrize("ns,dt", [(4096, 0.1), (520, 0.037), (17, 0.05), (64, 0.1), (5, 0.1), (2, 0.3),
                                    (8192, 0.0731)])
 def test_dft_twiddles_are_the_reference_expression(ns, dt):
