@@ -291,7 +291,7 @@ def main():
     # as setup_ms, and paid once by a single digitalfilters.py run
     torch.cuda.synchronize()
     t_setup = time.perf_counter()
-    gen = E.Generator(setup, device=device, rank=rank, world=world)
+    gen = E.Generator(setup, device=device, rank=rank, world=world, dist=dist if world > 1 else None)
     torch.cuda.synchronize()
     setup_ms = {"configure": (time.perf_counter() - t_setup) * 1e3}
     t_setup = time.perf_counter()
@@ -306,7 +306,16 @@ def main():
     split = (world > 1 or os.environ.get("PODS_EIGEN") == "split") and ns >= E.SPLIT_MIN_N
     spectrum = E.SpectrumQueue(gen.ctx, ns, rank, world) if split else None
 
+    # several ranks: step k-1's POD tail (rank 0's leading-pair solve, broadcasts, spatial modes)
+    # runs while the device has step k's generation and correlation (engine.ShardedSteps, two
+    # snapshot banks; PODS_PIPELINE=0 runs each tail right after its own all-reduce)
+    runner = E.ShardedSteps(setup, gen, d, spectrum) if world > 1 else None
+
     def step(timer=None, backlog=None, ahead=False):
+        if runner is not None:
+            runner.backlog = backlog
+            runner.step(timer=timer, prefetch_next=ahead)
+            return None, None, None
         return E.pipeline(setup, device=device, dist=d, gen=gen, timer=timer, spectrum=spectrum, backlog=backlog,
                           prefetch_next=ahead)
 
@@ -315,6 +324,8 @@ def main():
     # not prefetch, so the timed region holds exactly `steps` whole generations.
     for w in range(args.warmup):
         step(ahead=w < args.warmup - 1)
+    if runner is not None:
+        runner.flush()
     if spectrum is not None:
         spectrum.drain()
         spectrum.results()
@@ -334,6 +345,9 @@ def main():
     t0 = time.perf_counter()
     for s in range(args.steps):
         _, pod, _ = step(timer=tm_run, backlog=backlog, ahead=s < args.steps - 1)
+    if runner is not None:
+        runner.flush(tm_run)
+        pod = runner.results[-1]
     backlog.flush()
     fo = backlog.results[-1]
     if spectrum is not None:
@@ -440,6 +454,8 @@ def main():
                      "synthetic (seeded MT19937 random field, built tanh/top-hat profile)"),
             "config": {"workload": desc, "jma": J, "kma": K, "ns": ns, "nm": setup.nm,
                        "nf": [setup.nfx, setup.nfy, setup.nfz], "parallelism": "row-slab dp%d" % world,
+                       "pipelined_tail": bool(runner is not None and runner.pipelined),
+                       "mt_state_exchange": bool(gen._xch is not None),
                        "backend": args.backend if world > 1 else None, "dist_world_size": observed_world},
             "roofline": roofline,
             "combined_roofline": combined_roofline(J, K, ns, ms, world, corr_mode),

@@ -107,7 +107,35 @@ int pods_df_generate(pods_ctx* ctx);
 /* with PODS_GEN_PLANES: the planes' workgroups are limited to 2 per CU (padded LDS), so they
  * can run beside the late tridiagonalisation ranges of a pods_syev (see pods_syev_marker) */
 #define PODS_GEN_BESIDE_SOLVER 16
+/* with pods_df_set_exchange: record the segment-start states this rank owns (see below) */
+#define PODS_GEN_RECORD 32
 int pods_df_generate_parts(pods_ctx* ctx, int parts);
+/* Multi-GPU generation without every rank twisting the whole MT19937 stream (the reference
+ * draws it sequentially, digitalfilters.py:1361-1367, :1454-1467): the stream is cut into world x
+ * ~2048 substreams, rank r owning a contiguous 1/world of them.  PODS_GEN_JUMP then jumps only
+ * the owned substreams; PODS_GEN_RECORD twists them once and records, for every rank q and
+ * plane, the state at the block where q's row segment (its slab rows plus the 2nfy halo) starts
+ * -- when that block is owned here; the caller moves the records with ONE all_to_all between
+ * two device buffers it owns (pods_df_exchange_bind; per-peer byte counts from
+ * pods_df_exchange_sizes: rank r's send chunk for q, in plane order, lands in q's receive
+ * buffer after the chunks of ranks < r); and
+ * PODS_GEN_PLANES regenerates this rank's segments from the received states.  The planes are
+ * bit-identical to the single-stream generation.  j0s / j1s: every rank's slab [j0, j1) (this
+ * rank's must equal the configured one).  world <= 1 turns the exchange off; pods_df_configure
+ * does too. */
+int pods_df_set_exchange(pods_ctx* ctx, int world, int rank, const int* j0s, const int* j1s);
+int pods_df_exchange_sizes(pods_ctx* ctx, int64_t* send_bytes, int64_t* recv_bytes);
+int pods_df_exchange_bind(pods_ctx* ctx, void* send_dev, void* recv_dev);
+/* Two snapshot banks (0 = the default): bank selects which snapshot matrix -- with its mean,
+ * scale and centring state -- every snapshot call (generation, pods_mean, pods_corr,
+ * pods_center, pods_spatial_modes*, pods_df_snapshots) uses from now on.  A multi-GPU run
+ * generates and correlates step k in one bank while step k-1's spatial modes (PODFS.py:1330-1333)
+ * still read the other.  Bank 1 is allocated (zeroed) on first use; pods_df_configure returns to
+ * bank 0.  Replaces nothing in the reference (one step at a time). */
+int pods_select_snapshots(pods_ctx* ctx, int bank);
+/* A new seed for the next generation (np.random.seed, digitalfilters.py:1344) without
+ * reconfiguring: the next PODS_GEN_JUMP starts from it (multi-step runs of different inputs). */
+int pods_df_set_seed(pods_ctx* ctx, uint32_t seed);
 /* Device pointer and row length (= 3*P_local) of the snapshot matrix.  Device layout is
  * K-tiled: element (snapshot i, row r of the reference A) is at
  * a_dev[((r/16)*ns + i)*16 + r%16], rows padded with zeros to a multiple of 16. */

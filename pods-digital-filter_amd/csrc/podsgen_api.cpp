@@ -182,6 +182,34 @@ struct RngBuffers {
   }
 };
 
+// Multi-GPU state exchange (pods_df_set_exchange): the stream cut into world * (about 2048)
+// substreams of Bs blocks, owner r twisting substreams [g_lo, g_hi) once; the start state of
+// every rank's row segment in every plane is recorded by that segment's owner and sent to the
+// rank in one all_to_all (the caller's collective, pods_df_exchange_buffers); each rank then
+// regenerates only its own segments from those states (k_mt_chains).
+struct Exchange {
+  bool on = false;
+  int world = 1, rank = 0;
+  int64_t Bs = 0, blocks = 0;
+  int G = 0, g_lo = 0, g_hi = 0;
+  int nrec_out = 0, nseg = 0;                        // records this rank sends, segments it makes
+  std::vector<int64_t> send_counts, recv_counts;     // records per peer
+  DevBuf poly2, jobs, states, bases;                 // the owner's jump-ahead
+  DevBuf ch_b0, ch_nb, rec_block, rec_slot, rec_first;  // phase A (record)
+  DevBuf seg_b0, seg_nb;                             // phase C (segments)
+  uint32_t* send = nullptr;                          // caller-owned (pods_df_exchange_bind)
+  uint32_t* recv = nullptr;
+  std::vector<uint32_t> seed_host;
+  uint32_t seed = 0;
+  void free_all() {
+    for (DevBuf* b : {&poly2, &jobs, &states, &bases, &ch_b0, &ch_nb, &rec_block, &rec_slot, &rec_first, &seg_b0,
+                      &seg_nb})
+      release(*b);
+    send = recv = nullptr;
+    on = false;
+  }
+};
+
 // SYRK work items {bi, bj, split, 0}: split-major, then 8x8 super-blocks of 128x128 tiles
 // in the lower triangle, tiles row-major inside a super-block.  Consecutive items go to one
 // XCD, so the 64 workgroups an XCD holds at once (two per CU) cover one super-block: 16
@@ -234,6 +262,14 @@ struct pods_ctx {
   int64_t S = 0, Sl = 0, Pl = 0, rowlen = 0, rowpad = 0;  // rowpad: rowlen rounded up to 16
   RngLayout layout;
   RngBuffers rng;
+  Exchange xch;
+  // the other snapshot bank (pods_select_snapshots): a second A with its mean / scale / state, so
+  // a multi-GPU run can generate step k while step k-1's spatial modes still read its snapshots
+  struct SnapBank {
+    DevBuf A, mean, devmax;
+    bool have_snapshots = false, mean_valid = false, centered = false, dev_valid = false;
+  } alt;
+  int bank = 0;
   DevBuf R, T1, A, mean, lund, taps, rot, prog_mean, prog_dft, mag, lam, cwork, items, spwork, prog_rank;
   DevBuf e_wm, e_x, e_flags, e_det, e_v, e_t, e_part, e_w2, e_inv, e_cnt;  // pods_syev workspace
   int e_G = 0;
@@ -468,6 +504,8 @@ int pods_destroy(pods_ctx* c) {
                     &c->e2_ipiv, &c->dft_w})
     release(*b);
   c->rng.free_all();
+  c->xch.free_all();
+  for (DevBuf* b : {&c->alt.A, &c->alt.mean, &c->alt.devmax}) release(*b);
   release(c->sub_part);
   release(c->sub_R);
   release(c->sub_cheb);
@@ -551,6 +589,14 @@ int pods_df_configure(pods_ctx* c, const pods_df_params* prm, const double* bx, 
   if (p.lund_mode != PODS_LUND_NONE && !lund_host) return fail(PODS_ERR_ARG, "lund_host is null");
   if (p.rotate && !rot_host) return fail(PODS_ERR_ARG, "rot_host is null");
   PODS_HIP(hipSetDevice(c->device));
+  if (c->bank == 1) {  // back to bank 0; the other bank is rebuilt on demand for the new shape
+    std::swap(c->A, c->alt.A);
+    std::swap(c->mean, c->alt.mean);
+    std::swap(c->devmax, c->alt.devmax);
+    c->bank = 0;
+  }
+  for (DevBuf* b : {&c->alt.A, &c->alt.mean, &c->alt.devmax}) release(*b);
+  c->alt = pods_ctx::SnapBank{};
   c->p = p;
   c->NX = 2 * p.nfx + 1;
   c->NY = 2 * p.nfy + 1;
@@ -610,6 +656,7 @@ int pods_df_configure(pods_ctx* c, const pods_df_params* prm, const double* bx, 
   PODS_HIP(hipMemcpy(c->rot.p, r9, sizeof(r9), hipMemcpyHostToDevice));
   if (int e = upload_mean_program(c, p.ns)) return e;
   if (int e = upload_rng(c, c->layout, p.seed, c->rng)) return e;
+  c->xch.free_all();  // a new configuration: pods_df_set_exchange again for a multi-GPU run
   c->configured = true;
   c->have_snapshots = false;
   c->mean_valid = false;
@@ -619,18 +666,191 @@ int pods_df_configure(pods_ctx* c, const pods_df_params* prm, const double* bx, 
   PODS_CATCH
 }
 
+int pods_df_set_exchange(pods_ctx* c, int world, int rank, const int* j0s, const int* j1s) {
+  PODS_TRY
+  using namespace pods::mt;
+  if (int e = check_ctx(c)) return e;
+  if (!c->configured) return fail(PODS_ERR_STATE, "pods_df_set_exchange before pods_df_configure");
+  Exchange& X = c->xch;
+  X.free_all();
+  if (world <= 1) return PODS_OK;
+  const pods_df_params& p = c->p;
+  if (rank < 0 || rank >= world || !j0s || !j1s) return fail(PODS_ERR_ARG, "pods_df_set_exchange: bad rank/slabs");
+  if (j0s[rank] != p.j0 || j1s[rank] != p.j1)
+    return fail(PODS_ERR_ARG, "pods_df_set_exchange: this rank's slab differs from the configured one");
+  for (int q = 0; q < world; ++q)
+    if (j0s[q] < 0 || j1s[q] > p.jma || j0s[q] >= j1s[q]) return fail(PODS_ERR_ARG, "pods_df_set_exchange: bad slab");
+  if (c->S < 312) return fail(PODS_ERR_UNSUPPORTED, "pods_df_set_exchange: planes shorter than one block");
+  PODS_HIP(hipSetDevice(c->device));
+  const int64_t nplanes = 3 * (int64_t)(c->NX + p.ns - 1);
+  const int64_t ntot = nplanes * c->S;
+  X.world = world;
+  X.rank = rank;
+  X.blocks = (ntot + 311) / 312;
+  // the owners' substreams are 1/world of the one-GPU length, so a chain is as long as ... / world
+  X.Bs = std::max<int64_t>(64, (c->layout.Bs + world - 1) / world);
+  X.G = (int)((X.blocks + X.Bs - 1) / X.Bs);
+  if (X.G < world) return fail(PODS_ERR_UNSUPPORTED, "pods_df_set_exchange: stream too short for the ranks");
+  std::vector<int> glo(world + 1);
+  for (int r = 0; r <= world; ++r) glo[r] = (int)((int64_t)X.G * r / world);
+  X.g_lo = glo[rank];
+  X.g_hi = glo[rank + 1];
+  auto owner = [&](int64_t block) {
+    const int g = (int)(block / X.Bs);
+    return (int)(std::upper_bound(glo.begin(), glo.end(), g) - glo.begin()) - 1;
+  };
+  // jump jobs of this owner's substreams g >= 1: mt^(1) jumped by t^(624 (g Bs - 1)) mod phi
+  const int pfirst = std::max(1, X.g_lo);
+  const int npoly = X.g_hi - pfirst;
+  if (npoly > 0) {
+    const JumpTables& jt = jump_tables(X.Bs, std::max(1, X.G - 1), 1);
+    PODS_HIP(ensure(X.poly2, (size_t)npoly * N * 4));
+    PODS_HIP(hipMemcpy(X.poly2.p, &jt.level2[(size_t)pfirst * N], (size_t)npoly * N * 4, hipMemcpyHostToDevice));
+    std::vector<int> jobs(3 * (size_t)npoly);
+    for (int k = 0; k < npoly; ++k) {
+      jobs[k] = 0;                              // source: mt^(1)
+      jobs[npoly + k] = k;                      // polynomial of substream pfirst + k
+      jobs[2 * npoly + k] = pfirst + k - X.g_lo;  // local state index
+    }
+    PODS_HIP(ensure(X.jobs, jobs.size() * sizeof(int)));
+    PODS_HIP(hipMemcpy(X.jobs.p, jobs.data(), jobs.size() * sizeof(int), hipMemcpyHostToDevice));
+  }
+  const int nch = X.g_hi - X.g_lo;
+  PODS_HIP(ensure(X.states, (size_t)nch * N * 4));
+  PODS_HIP(ensure(X.bases, (size_t)N * 4));
+  X.seed_host.assign(2 * N, 0);
+  seed_state(p.seed, X.seed_host.data());
+  std::memcpy(X.seed_host.data() + N, X.seed_host.data(), N * 4);
+  twist(X.seed_host.data() + N);
+  // phase A chains and the records: every rank's segment start in every plane whose block this
+  // rank owns, grouped by target rank (plane order within), sorted by block for the chains
+  std::vector<int64_t> cb0(nch);
+  std::vector<int> cnb(nch);
+  for (int k = 0; k < nch; ++k) {
+    const int64_t g = X.g_lo + k;
+    cb0[k] = g * X.Bs;
+    cnb[k] = (int)std::min<int64_t>(X.Bs, X.blocks - g * X.Bs);
+  }
+  X.send_counts.assign(world, 0);
+  X.recv_counts.assign(world, 0);
+  std::vector<std::pair<int64_t, int>> recs;  // (block, slot)
+  std::vector<int64_t> send_off(world + 1, 0);
+  for (int q = 0; q < world; ++q) {
+    for (int64_t pl = 0; pl < nplanes; ++pl) {
+      const int64_t b = (pl * c->S + (int64_t)j0s[q] * c->Kp) / 312;
+      const int r = owner(b);
+      if (r == rank) recs.push_back({b, (int)(send_off[q] + X.send_counts[q]++)});
+      if (q == rank) ++X.recv_counts[r];
+    }
+    send_off[q + 1] = send_off[q] + X.send_counts[q];
+  }
+  std::stable_sort(recs.begin(), recs.end(),
+                   [](const std::pair<int64_t, int>& a, const std::pair<int64_t, int>& b) { return a.first < b.first; });
+  X.nrec_out = (int)recs.size();
+  std::vector<int64_t> rb(recs.size());
+  std::vector<int> rs(recs.size()), rf(nch + 1, 0);
+  for (size_t k = 0; k < recs.size(); ++k) {
+    rb[k] = recs[k].first;
+    rs[k] = recs[k].second;
+    ++rf[(int)(recs[k].first / X.Bs) - X.g_lo + 1];
+  }
+  for (int k = 0; k < nch; ++k) rf[k + 1] += rf[k];
+  // phase C: this rank's segment of every plane (the 2nfy halo rows included)
+  X.nseg = (int)nplanes;
+  std::vector<int64_t> sb0(nplanes);
+  std::vector<int> snb(nplanes);
+  for (int64_t pl = 0; pl < nplanes; ++pl) {
+    const int64_t s0 = pl * c->S + (int64_t)p.j0 * c->Kp;
+    const int64_t s1 = std::min(ntot, pl * c->S + (int64_t)(p.j1 + 2 * p.nfy) * c->Kp);
+    sb0[pl] = s0 / 312;
+    snb[pl] = (int)((s1 + 311) / 312 - sb0[pl]);
+  }
+  auto up = [&](DevBuf& d, const void* src, size_t bytes) -> hipError_t {
+    hipError_t e = ensure(d, bytes);
+    if (e == hipSuccess && bytes) e = hipMemcpy(d.p, src, bytes, hipMemcpyHostToDevice);
+    return e;
+  };
+  PODS_HIP(up(X.ch_b0, cb0.data(), cb0.size() * 8));
+  PODS_HIP(up(X.ch_nb, cnb.data(), cnb.size() * 4));
+  PODS_HIP(up(X.rec_block, rb.data(), rb.size() * 8));
+  PODS_HIP(up(X.rec_slot, rs.data(), rs.size() * 4));
+  PODS_HIP(up(X.rec_first, rf.data(), rf.size() * 4));
+  PODS_HIP(up(X.seg_b0, sb0.data(), sb0.size() * 8));
+  PODS_HIP(up(X.seg_nb, snb.data(), snb.size() * 4));
+  X.on = true;
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_df_exchange_sizes(pods_ctx* c, int64_t* send_bytes, int64_t* recv_bytes) {
+  if (int e = check_ctx(c)) return e;
+  const Exchange& X = c->xch;
+  if (!X.on) return fail(PODS_ERR_STATE, "pods_df_exchange_sizes: no exchange configured");
+  for (int r = 0; r < X.world; ++r) {
+    if (send_bytes) send_bytes[r] = X.send_counts[r] * pods::mt::N * 4;
+    if (recv_bytes) recv_bytes[r] = X.recv_counts[r] * pods::mt::N * 4;
+  }
+  return PODS_OK;
+}
+
+int pods_df_exchange_bind(pods_ctx* c, void* send_dev, void* recv_dev) {
+  if (int e = check_ctx(c)) return e;
+  Exchange& X = c->xch;
+  if (!X.on) return fail(PODS_ERR_STATE, "pods_df_exchange_bind: no exchange configured");
+  if (!send_dev || !recv_dev) return fail(PODS_ERR_ARG, "pods_df_exchange_bind: null buffer");
+  X.send = static_cast<uint32_t*>(send_dev);
+  X.recv = static_cast<uint32_t*>(recv_dev);
+  return PODS_OK;
+}
+
 int pods_df_generate_parts(pods_ctx* c, int parts) {
   PODS_TRY
   if (int e = check_ctx(c)) return e;
   if (!c->configured) return fail(PODS_ERR_STATE, "pods_df_generate before pods_df_configure");
-  if (parts & ~(PODS_GEN_ALL | PODS_GEN_BESIDE_SOLVER)) return fail(PODS_ERR_ARG, "bad generation parts");
+  if (parts & ~(PODS_GEN_ALL | PODS_GEN_BESIDE_SOLVER | PODS_GEN_RECORD))
+    return fail(PODS_ERR_ARG, "bad generation parts");
   PODS_HIP(hipSetDevice(c->device));
   const pods_df_params& p = c->p;
   const RngLayout& L = c->layout;
-  if (parts & PODS_GEN_JUMP) {
+  Exchange& X = c->xch;
+  if (X.on) {
+    // the multi-GPU state exchange: JUMP = this owner's substreams, RECORD = its segment-start
+    // records (the caller then runs the all_to_all), PLANES = this rank's segments
+    using pods::mt::N;
+    if ((parts & (PODS_GEN_RECORD | PODS_GEN_PLANES)) && (!X.send || !X.recv))
+      return fail(PODS_ERR_STATE, "exchange buffers not bound (pods_df_exchange_bind)");
+    if (parts & PODS_GEN_JUMP) {
+      if (X.g_lo == 0)
+        PODS_HIP(hipMemcpyAsync(X.states.p, X.seed_host.data(), N * 4, hipMemcpyHostToDevice, c->stream));
+      PODS_HIP(hipMemcpyAsync(X.bases.p, X.seed_host.data() + N, N * 4, hipMemcpyHostToDevice, c->stream));
+      const int pfirst = std::max(1, X.g_lo), npoly = X.g_hi - pfirst;
+      if (npoly > 0) {
+        const int* jb = X.jobs.as<int>();
+        PODS_HIP(pods::launch_mt_jump(X.bases.as<uint32_t>(), jb, X.poly2.as<uint32_t>(), jb + npoly,
+                                      X.states.as<uint32_t>(), jb + 2 * npoly, npoly, c->stream));
+      }
+    }
+    if (parts & PODS_GEN_RECORD) {
+      const int64_t ntot = 3 * (int64_t)(c->NX + p.ns - 1) * c->S;
+      PODS_HIP(pods::launch_mt_chains(0, X.states.as<uint32_t>(), X.ch_b0.as<int64_t>(), X.ch_nb.as<int>(),
+                                      X.g_hi - X.g_lo, X.rec_block.as<int64_t>(), X.rec_slot.as<int>(),
+                                      X.rec_first.as<int>(), X.send, ntot, c->S, c->Kp, 0, 0, c->Sl,
+                                      p.rng_low, p.rng_range, nullptr, c->stream));
+    }
+    if (parts & PODS_GEN_PLANES) {
+      const int64_t ntot = 3 * (int64_t)(c->NX + p.ns - 1) * c->S;
+      PODS_HIP(pods::launch_mt_chains(1, X.recv, X.seg_b0.as<int64_t>(), X.seg_nb.as<int>(), X.nseg,
+                                      nullptr, nullptr, nullptr, nullptr, ntot, c->S, c->Kp, p.j0,
+                                      p.j1 + 2 * p.nfy, c->Sl, p.rng_low, p.rng_range, c->R.as<double>(),
+                                      c->stream));
+    }
+  } else if (parts & PODS_GEN_RECORD) {
+    return fail(PODS_ERR_STATE, "PODS_GEN_RECORD without pods_df_set_exchange");
+  }
+  if (!X.on && (parts & PODS_GEN_JUMP)) {
     if (int e = run_jumps(c, L, c->rng)) return e;
   }
-  if (parts & PODS_GEN_PLANES) {
+  if (!X.on && (parts & PODS_GEN_PLANES)) {
     PODS_HIP(pods::launch_mt_generate(c->rng.states.as<uint32_t>(), L.G, L.Bs, L.ntot, c->S, c->Kp, p.j0,
                                       p.j1 + 2 * p.nfy, c->Sl, p.rng_low, p.rng_range, c->R.as<double>(),
                                       c->stream, (parts & PODS_GEN_BESIDE_SOLVER) ? 2 : 0));
@@ -660,6 +880,53 @@ int pods_df_generate_parts(pods_ctx* c, int parts) {
 }
 
 int pods_df_generate(pods_ctx* c) { return pods_df_generate_parts(c, PODS_GEN_ALL); }
+
+int pods_df_set_seed(pods_ctx* c, uint32_t seed) {
+  PODS_TRY
+  using namespace pods::mt;
+  if (int e = check_ctx(c)) return e;
+  if (!c->configured) return fail(PODS_ERR_STATE, "pods_df_set_seed before pods_df_configure");
+  c->p.seed = seed;
+  // the host seed states (mt^(0), mt^(1)) the next PODS_GEN_JUMP uploads; the jump polynomials
+  // do not depend on the seed
+  for (std::vector<uint32_t>* h : {&c->rng.seed_host, &c->xch.seed_host}) {
+    if (h->size() != 2 * (size_t)N) continue;
+    seed_state(seed, h->data());
+    std::memcpy(h->data() + N, h->data(), N * 4);
+    twist(h->data() + N);
+  }
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_select_snapshots(pods_ctx* c, int bank) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (bank != 0 && bank != 1) return fail(PODS_ERR_ARG, "pods_select_snapshots: bank must be 0 or 1");
+  if (bank == c->bank) return PODS_OK;
+  if (!c->configured) return fail(PODS_ERR_STATE, "pods_select_snapshots before pods_df_configure");
+  PODS_HIP(hipSetDevice(c->device));
+  pods_ctx::SnapBank& o = c->alt;
+  const size_t abytes = (size_t)c->p.ns * c->rowpad * sizeof(double), mbytes = (size_t)c->rowpad * sizeof(double);
+  if (o.A.bytes < abytes || o.mean.bytes < mbytes) {
+    // padded K rows of the K-tiled matrix (and of the mean) must read as zero, as in bank 0
+    PODS_HIP(ensure(o.A, abytes));
+    PODS_HIP(ensure(o.mean, mbytes));
+    PODS_HIP(hipMemsetAsync(o.A.p, 0, abytes, c->stream));
+    PODS_HIP(hipMemsetAsync(o.mean.p, 0, mbytes, c->stream));
+  }
+  PODS_HIP(ensure(o.devmax, sizeof(double)));
+  std::swap(c->A, o.A);
+  std::swap(c->mean, o.mean);
+  std::swap(c->devmax, o.devmax);
+  std::swap(c->have_snapshots, o.have_snapshots);
+  std::swap(c->mean_valid, o.mean_valid);
+  std::swap(c->centered, o.centered);
+  std::swap(c->dev_valid, o.dev_valid);
+  c->bank = bank;
+  return PODS_OK;
+  PODS_CATCH
+}
 
 int pods_df_snapshots(pods_ctx* c, double** a_dev, int64_t* row_len) {
   if (int e = check_ctx(c)) return e;

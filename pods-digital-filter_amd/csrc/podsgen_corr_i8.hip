@@ -144,7 +144,7 @@ template <int V>
 __device__ __forceinline__ void residues_body(const double* __restrict__ AT, int ns, int64_t rowlen,
                                               int64_t rowpad, const double* __restrict__ mean,
                                               const double* __restrict__ devmax, int bbits, int64_t kc0,
-                                              int64_t nkc, int8_t* __restrict__ R, int64_t lstride) {
+                                              int64_t nkc, int8_t* __restrict__ R, int64_t ms, int64_t cs) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int q = (int)(t & 3);
   const int64_t rest = t >> 2;
@@ -168,7 +168,10 @@ __device__ __forceinline__ void residues_body(const double* __restrict__ AT, int
     for (int e = 0; e < 16; ++e) a[e] = 0.0;
   }
   const int sg = scale_exp(*devmax, bbits);
-  const uint32_t doff = (uint32_t)((kcl * ns + i) * 64 + q * 16);  // < lstride < 4 GB
+  // modulus l's bytes of this thread: R + l * ms + kcl * cs + i * 64 + q * 16 (ms, cs: the
+  // modulus and K-chunk strides of the residue layout, see launch_corr_i8)
+  int8_t* const rb = R + kcl * cs;
+  const uint32_t doff = (uint32_t)(i * 64 + q * 16);
   // the byte of r + 1.5 * 2^23 (|r| <= 127) is r's two's-complement byte: pack 16 of them
   auto store16 = [&](const f32x2 (&sv)[8], int l) {
     uint32_t w[4];
@@ -179,7 +182,7 @@ __device__ __forceinline__ void residues_body(const double* __restrict__ AT, int
       const uint32_t h1 = __builtin_amdgcn_perm(__float_as_uint(v.y), __float_as_uint(v.x), 0x0C0C0400u);
       w[pq] = h0 | (h1 << 16);
     }
-    int8_t* base = R + (int64_t)l * lstride;  // uniform: a scalar base + 32-bit offset store
+    int8_t* base = rb + (int64_t)l * ms;
     *reinterpret_cast<uint4*>(base + doff) = make_uint4(w[0], w[1], w[2], w[3]);
   };
   constexpr float MAG = 12582912.0f;  // 1.5 * 2^23
@@ -288,8 +291,8 @@ __device__ __forceinline__ void residues_body(const double* __restrict__ AT, int
 
 #define PODS_RES_ARGS const double* __restrict__ AT, int ns, int64_t rowlen, int64_t rowpad, \
     const double* __restrict__ mean, const double* __restrict__ devmax, int bbits, int64_t kc0, int64_t nkc, \
-    int8_t* __restrict__ R, int64_t lstride
-#define PODS_RES_PASS AT, ns, rowlen, rowpad, mean, devmax, bbits, kc0, nkc, R, lstride
+    int8_t* __restrict__ R, int64_t ms, int64_t cs
+#define PODS_RES_PASS AT, ns, rowlen, rowpad, mean, devmax, bbits, kc0, nkc, R, ms, cs
 template <int V>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) void k_residues(PODS_RES_ARGS) {
   residues_body<V>(PODS_RES_PASS);
@@ -324,8 +327,9 @@ __device__ __forceinline__ int swz(int quartet) { return (0x78 >> (2 * quartet))
 // reads it as both operands.  items: {bi, bj, split, -} (bi < 0: an empty slot that keeps the
 // item count a multiple of 8).  DIAG (measurement only): 1 = no MFMAs, 2 = no operand traffic.
 template <int NST, int DIAG, bool SAME, int ILV>
-__device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int ns, int nt, int i0, int j0, int m,
-                                          char* smem, uint8_t* __restrict__ dst, int ldp, int accumulate) {
+__device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int64_t cstride, int ns, int nt, int i0,
+                                          int j0, int m, char* smem, uint8_t* __restrict__ dst, int ldp,
+                                          int accumulate) {
   constexpr int STG = 2 * PANEL;
   constexpr int Q = SAME ? 2 : 4;  // DMA instructions per wave per stage
   constexpr int D = NST - 2;       // DMA lead in K steps beyond the one being read
@@ -344,7 +348,6 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int n
     yo[q] = (int64_t)min(j0 + rw, ns - 1) * KC + ls * 16;
   }
   const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
-  const int64_t cstride = (int64_t)ns * KC;
   // piece q of step t's DMA (q < 2: the row panel, 2-3: the column panel)
   auto piece = [&](int t, int q) {
     if constexpr (DIAG == 2) return;
@@ -474,7 +477,8 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int n
 }
 
 template <int NST, int DIAG = 0, int ILV = 0>
-__global__ __launch_bounds__(512, 1) void k_syrk_i8(const int8_t* __restrict__ R, int ns, int64_t lstride, int kcs,
+__global__ __launch_bounds__(512, 1) void k_syrk_i8(const int8_t* __restrict__ R, int ns, int64_t ms, int64_t cs,
+                                                    int kcs,
                                                     const int4* __restrict__ items, int nitems, int nsplit,
                                                     uint8_t* __restrict__ P, int64_t pslab, int ldp, int accumulate,
                                                     int xcd_ranges) {
@@ -488,13 +492,13 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8(const int8_t* __restrict__ R
   const int4 it = items[b - l * nitems];
   if (it.x < 0) return;
   const int bi = it.x, bj = it.y, sp = it.z;
-  const int8_t* base = R + (int64_t)l * lstride + (int64_t)sp * kcs * ns * KC;
+  const int8_t* base = R + (int64_t)l * ms + (int64_t)sp * kcs * cs;
   uint8_t* dst = P + (int64_t)(l * nsplit + sp) * pslab;
   const int m = modulus(l);
   if (bi == bj)
-    syrk_tile<NST, DIAG, true, ILV>(base, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
+    syrk_tile<NST, DIAG, true, ILV>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
   else
-    syrk_tile<NST, DIAG, false, ILV>(base, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
+    syrk_tile<NST, DIAG, false, ILV>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
 }
 
 // ---- CRT reconstruction ----------------------------------------------------------------------
@@ -799,7 +803,14 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
   const size_t lds = (size_t)(variant == 5 || (variant >= 45 && variant <= 47) ? 5 : 4) * 2 * PANEL;
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  const int64_t lstride = p.chunks * ns * KC;
+  // residue layout: modulus l's K chunk kc at R + l * ms + kc * cs.  Default: one matrix per
+  // modulus ([NMOD][chunks][ns][64]).  PODS_RES_LAYOUT=1 (A/B): the moduli interleaved per K
+  // chunk ([chunks][NMOD][ns][64]), so a residue wave's 16 stores land in one 16 * ns * 64-byte
+  // window instead of 16 matrices apart
+  const char* lay = std::getenv("PODS_RES_LAYOUT");
+  const bool ilv = lay && lay[0] == '1';
+  const int64_t ms = ilv ? (int64_t)ns * KC : p.chunks * ns * KC;
+  const int64_t cs = ilv ? (int64_t)NMOD * ns * KC : (int64_t)ns * KC;
   const int ldp = (ns + 63) / 64 * 64;
   const int64_t pslab = (int64_t)ns * ldp;
   if (syrk_begin && p.nlaunch > 1) e = hipEventRecord(syrk_begin, st);
@@ -816,10 +827,10 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
       const double* mean_ = mean;
       const double* dm_ = devmax;
       int bb_ = p.bbits;
-      int64_t kc_ = kc0, nk_ = p.chunks, ls_ = lstride, rl_ = rowlen, rp_ = rowpad;
+      int64_t kc_ = kc0, nk_ = p.chunks, ms_ = ms, cs_ = cs, rl_ = rowlen, rp_ = rowpad;
       int ns_ = ns;
       int8_t* R_ = R;
-      void* rargs[] = {&AT_, &ns_, &rl_, &rp_, &mean_, &dm_, &bb_, &kc_, &nk_, &R_, &ls_};
+      void* rargs[] = {&AT_, &ns_, &rl_, &rp_, &mean_, &dm_, &bb_, &kc_, &nk_, &R_, &ms_, &cs_};
       e = hipLaunchKernel(rk, dim3((unsigned)((thr + 255) / 256)), dim3(256), rargs, 0, st);
       if (e != hipSuccess) return e;
     }
@@ -834,7 +845,8 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
       const char* ord = std::getenv("PODS_CORR_ORDER");
       int xr_ = ord && ord[0] == 'x' ? 1 : 0;
       const int4* it_ = reinterpret_cast<const int4*>(items);
-      void* args[] = {&R, const_cast<int*>(&ns), const_cast<int64_t*>(&lstride), const_cast<int*>(&p.kcs),
+      int64_t ms_ = ms, cs_ = cs;
+      void* args[] = {&R, const_cast<int*>(&ns), &ms_, &cs_, const_cast<int*>(&p.kcs),
                       &it_, const_cast<int*>(&p.nitems), const_cast<int*>(&p.nsplit), &P,
                       const_cast<int64_t*>(&pslab), const_cast<int*>(&ldp_), const_cast<int*>(&acc_), &xr_};
       e = hipLaunchKernel(fn, dim3((unsigned)(NMOD * p.nitems)), dim3(512), args, lds, st);

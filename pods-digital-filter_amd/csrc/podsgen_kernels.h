@@ -22,6 +22,11 @@ hipError_t launch_mt_jump(const uint32_t* src, const int* src_idx, const uint32_
 hipError_t launch_mt_generate(const uint32_t* states, int G, int64_t Bs, int64_t ntot, int64_t S,
                               int Kp, int rlo, int rhi, int64_t Sl, double low, double range,
                               double* out, hipStream_t st, int per_cu = 0);
+// the multi-GPU state exchange's chains (mode 0: record segment start states, 1: store segments)
+hipError_t launch_mt_chains(int mode, const uint32_t* st0, const int64_t* b0, const int* nb, int nchains,
+                            const int64_t* rec_block, const int* rec_slot, const int* rec_first, uint32_t* rec_out,
+                            int64_t ntot, int64_t S, int Kp, int rlo, int rhi, int64_t Sl, double low, double range,
+                            double* out, hipStream_t st);
 hipError_t launch_filter_x(int NX, const double* R, const double* bx, int ns, int64_t Sl, int ncomp,
                            int chunk, double* T1, hipStream_t st);
 // lund_sj: 0 = one row of 9 x K parameters for every j (plain layout lund[e * Pl + k]);

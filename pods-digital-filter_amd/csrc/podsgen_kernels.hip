@@ -373,6 +373,99 @@ __global__ __launch_bounds__(256) void k_mt_generate_slab(const uint32_t* __rest
   }
 }
 
+// Chains of the stream for the multi-GPU state exchange (r5; pods_df_set_exchange).  Chain c
+// starts from the 624-word state st0 + c * 624 (the state before the twist that makes its first
+// block b0[c]) and runs nb[c] blocks, with the double-buffered LDS twist of k_mt_generate_slab.
+//   RECORD (an owner rank's own substreams): before the twist of block b, the state is copied
+//     to rec_out + 624 * slot for every record (b, slot) of the chain (rec_first[c] ..
+//     rec_first[c+1], sorted by block) -- the start state of another rank's row segment;
+//   STORE (a rank's own row segments, one chain per plane): the doubles of the chain's blocks
+//     whose padded row lies in [rlo, rhi) of their plane go to out[q Sl + o - rlo Kp], exactly
+//     as in k_mt_generate_slab (bit for bit the same doubles).
+// So no rank twists the whole stream: each twists its 1/N share once and the ~12 K segment
+// starts of every rank (2.5 KB each) travel in one all_to_all.
+template <bool RECORD, bool STORE>
+__global__ __launch_bounds__(256) void k_mt_chains(const uint32_t* __restrict__ st0, const int64_t* __restrict__ b0,
+                                                   const int* __restrict__ nbk, int nchains,
+                                                   const int64_t* __restrict__ rec_block,
+                                                   const int* __restrict__ rec_slot, const int* __restrict__ rec_first,
+                                                   uint32_t* __restrict__ rec_out, int64_t ntot, int64_t S, int Kp,
+                                                   int rlo, int rhi, int64_t Sl, double low, double range,
+                                                   double* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint32_t buf[2][MTN];
+  const int t = threadIdx.x;
+  for (int c = blockIdx.x; c < nchains; c += gridDim.x) {
+    __syncthreads();  // the previous chain's last tempering / record read buf
+    for (int i = t; i < MTN; i += 256) buf[0][i] = st0[(size_t)c * MTN + i];
+    __syncthreads();
+    const int64_t bb = b0[c];
+    const int64_t nb = nbk[c];
+    const int64_t D0 = bb * 312;
+    const int64_t olo = (int64_t)rlo * Kp, ohi = (int64_t)rhi * Kp;
+    int64_t q0 = STORE ? D0 / S : 0, o0 = STORE ? D0 - (D0 / S) * S : 0;
+    int ri = RECORD ? rec_first[c] : 0;
+    const int re = RECORD ? rec_first[c + 1] : 0;
+    for (int64_t b = 0; b <= nb; ++b) {
+      const uint32_t* cur = buf[b & 1];
+      uint32_t* nxt = buf[(b + 1) & 1];
+      const bool tw = b < nb;
+      if constexpr (RECORD) {
+        // cur is the state before block bb + b's twist
+        while (ri < re && rec_block[ri] == bb + b) {
+          uint32_t* dst = rec_out + (size_t)rec_slot[ri] * MTN;
+          for (int i = t; i < MTN; i += 256) dst[i] = cur[i];
+          ++ri;
+        }
+      }
+      if (tw) twist_chain(cur, nxt, t);
+      if constexpr (STORE) {
+        if (b >= 1) {
+          const int64_t e0 = o0 + 311;
+          const bool any = (o0 < ohi && e0 >= olo) || (e0 >= S && e0 - S >= olo);
+          if (any && t < 156) {
+            const uint4 w = reinterpret_cast<const uint4*>(cur)[t];
+            const uint32_t a0 = mt_temper(w.x) >> 5, c0 = mt_temper(w.y) >> 6;
+            const uint32_t a1 = mt_temper(w.z) >> 5, c1 = mt_temper(w.w) >> 6;
+            const double u0 = ((double)a0 * 67108864.0 + (double)c0) / 9007199254740992.0;
+            const double u1 = ((double)a1 * 67108864.0 + (double)c1) / 9007199254740992.0;
+            const int64_t Db = D0 + (b - 1) * 312 + 2 * t;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              int64_t q = q0, o = o0 + 2 * t + h;
+              if (o >= S) {
+                o -= S;
+                ++q;
+              }
+              if (Db + h < ntot && o >= olo && o < ohi) out[q * Sl + o - olo] = low + range * (h ? u1 : u0);
+            }
+          }
+          o0 += 312;
+          if (o0 >= S) {
+            o0 -= S;
+            ++q0;
+          }
+        }
+      }
+      if (!tw) break;
+      __syncthreads();  // nxt complete; cur (tempered / recorded above) becomes the next nxt
+    }
+  }
+}
+
+hipError_t launch_mt_chains(int mode, const uint32_t* st0, const int64_t* b0, const int* nb, int nchains,
+                            const int64_t* rec_block, const int* rec_slot, const int* rec_first, uint32_t* rec_out,
+                            int64_t ntot, int64_t S, int Kp, int rlo, int rhi, int64_t Sl, double low, double range,
+                            double* out, hipStream_t st) {
+  if (nchains <= 0) return hipSuccess;
+  if (mode == 0)
+    hipLaunchKernelGGL((k_mt_chains<true, false>), dim3(nchains), dim3(256), 0, st, st0, b0, nb, nchains, rec_block,
+                       rec_slot, rec_first, rec_out, ntot, S, Kp, rlo, rhi, Sl, low, range, out);
+  else
+    hipLaunchKernelGGL((k_mt_chains<false, true>), dim3(nchains), dim3(256), 0, st, st0, b0, nb, nchains, rec_block,
+                       rec_slot, rec_first, rec_out, ntot, S, Kp, rlo, rhi, Sl, low, range, out);
+  return hipGetLastError();
+}
+
 // -----------------------------------------------------------------------------------------
 // separable filter
 // -----------------------------------------------------------------------------------------

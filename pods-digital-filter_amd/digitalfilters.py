@@ -344,7 +344,7 @@ def main(argv=None):
     i_d.hdf5 = options.hdf5
     i_d.verbose = options.verbose
     i_d.seed = s.seed
-    gen = _E.Generator(s, device=local, rank=rank, world=world)
+    gen = _E.Generator(s, device=local, rank=rank, world=world, dist=dist if world > 1 else None)
     i_d._pods_ctx = gen.ctx
     snap = gen.generate()  # main() step loop :1403-1477 as one device pass
     if options.verbose:  # per-step snapshot planes (:1479-1481), written by rank 0

@@ -15,6 +15,7 @@ PODS_LUND_PRF = 1
 PODS_LUND_NONE = -1
 PODS_GEN_JUMP, PODS_GEN_PLANES, PODS_GEN_XPASS, PODS_GEN_YZPASS, PODS_GEN_ALL = 1, 2, 4, 8, 15  # podsgen.h
 PODS_GEN_BESIDE_SOLVER = 16
+PODS_GEN_RECORD = 32
 
 c_int = ctypes.c_int
 c_i64 = ctypes.c_int64
@@ -46,6 +47,11 @@ SIGNATURES = {
     "pods_df_generate": (c_int, [c_void_p]),
     "pods_df_generate_parts": (c_int, [c_void_p, c_int]),
     "pods_df_snapshots": (c_int, [c_void_p, ctypes.POINTER(c_void_p), ctypes.POINTER(c_i64)]),
+    "pods_df_set_exchange": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "pods_df_exchange_sizes": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "pods_select_snapshots": (c_int, [c_void_p, c_int]),
+    "pods_df_set_seed": (c_int, [c_void_p, c_u32]),
+    "pods_df_exchange_bind": (c_int, [c_void_p, c_void_p, c_void_p]),
     "pods_set_snapshots": (c_int, [c_void_p, c_void_p, c_int, c_i64]),
     "pods_copy_snapshots": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     "pods_copy": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_size_t, c_int]),

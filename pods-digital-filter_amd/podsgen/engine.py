@@ -180,10 +180,12 @@ class DeviceSnapshots:
 class Generator:
     """digitalfilters.py main() step loop (:1403-1477) on one GPU / row slab."""
 
-    def __init__(self, setup: DFSetup, device=0, rank=0, world=1, ctx: Optional[Context] = None):
+    def __init__(self, setup: DFSetup, device=0, rank=0, world=1, ctx: Optional[Context] = None, dist=None,
+                 exchange=None):
         self.setup = setup
         self.ctx = ctx or Context(device)
         self.rank, self.world = rank, world
+        self.dist = dist
         self.j0, self.j1 = row_slab(setup.jma, rank, world)
         bx, by, bz = setup.taps()
         rot = setup.rotation()
@@ -199,6 +201,46 @@ class Generator:
         check(self.ctx.lib.pods_df_configure(self.ctx.h, ctypes.byref(p), ptr(k[0]), ptr(k[1]), ptr(k[2]),
                                              ptr(k[3]), ptr(k[4])), "pods_df_configure")
         self.rowlen = 3 * (self.j1 - self.j0) * setup.kma
+        # several ranks: no rank twists the whole MT19937 stream -- each owns 1/world of it and
+        # the segment-start states travel in one all_to_all per generation (exchange_states);
+        # PODS_MT_EXCHANGE=0 makes every rank twist the whole stream instead (A/B)
+        if exchange is None:
+            exchange = world > 1 and dist is not None and os.environ.get("PODS_MT_EXCHANGE", "1") != "0"
+        self._xch = None
+        if exchange:
+            self.enable_exchange()
+
+    def enable_exchange(self):
+        """pods_df_set_exchange with every rank's slab; the send / receive buffers are torch
+        tensors on this device (pods_df_exchange_bind)."""
+        lib, h = self.ctx.lib, self.ctx.h
+        slabs = [row_slab(self.setup.jma, q, self.world) for q in range(self.world)]
+        j0s = np.array([a for a, _ in slabs], dtype=np.int32)
+        j1s = np.array([b for _, b in slabs], dtype=np.int32)
+        check(lib.pods_df_set_exchange(h, self.world, self.rank, ptr(j0s), ptr(j1s)), "pods_df_set_exchange")
+        sb = np.zeros(self.world, dtype=np.int64)
+        rb = np.zeros(self.world, dtype=np.int64)
+        check(lib.pods_df_exchange_sizes(h, ptr(sb), ptr(rb)), "pods_df_exchange_sizes")
+        dev = torch.device("cuda", self.ctx.device)
+        self._send = torch.empty(max(int(sb.sum()), 16), dtype=torch.uint8, device=dev)
+        self._recv = torch.empty(max(int(rb.sum()), 16), dtype=torch.uint8, device=dev)
+        check(lib.pods_df_exchange_bind(h, ptr(self._send), ptr(self._recv)), "pods_df_exchange_bind")
+        self._xch = ([int(x) for x in sb], [int(x) for x in rb])
+
+    def exchange_states(self):
+        """The all_to_all of the segment-start states (2.5 KB per rank and plane; every rank calls
+        generate() together).  RCCL moves device buffers; gloo (CPU transport, e.g. several ranks on
+        one GPU) goes through host copies."""
+        sb, rb = self._xch
+        d = self.dist
+        n_s, n_r = sum(sb), sum(rb)
+        if d.get_backend() == "nccl":
+            d.all_to_all_single(self._recv[:n_r], self._send[:n_s], output_split_sizes=rb, input_split_sizes=sb)
+        else:
+            send = self._send[:n_s].cpu()
+            recv = torch.empty(n_r, dtype=torch.uint8)
+            d.all_to_all_single(recv, send, output_split_sizes=rb, input_split_sizes=sb)
+            self._recv[:n_r].copy_(recv)
 
     _ahead = None      # event behind the next run's prefetched parts (prefetch_*)
     _ahead_parts = 0   # which parts: PODS_GEN_JUMP, + PODS_GEN_PLANES
@@ -207,7 +249,19 @@ class Generator:
         """The whole generation on the current stream -- or, after prefetch_jump() (and
         prefetch_planes_beside_solver()), the parts not yet done, behind the event of those
         already enqueued on the gen stream."""
-        if self._ahead is not None:
+        if self._xch is not None:   # the state exchange: own substreams, all_to_all, own segments
+            done = 0
+            if self._ahead is not None:
+                torch.cuda.current_stream(self.ctx.device).wait_event(self._ahead)
+                done = self._ahead_parts
+                self._ahead, self._ahead_parts = None, 0
+            pre = (_lib.PODS_GEN_JUMP | _lib.PODS_GEN_RECORD) & ~done
+            if pre:
+                check(self.ctx.lib.pods_df_generate_parts(self.ctx.h, pre), "pods_df_generate_parts")
+            self.exchange_states()
+            rest = _lib.PODS_GEN_PLANES | _lib.PODS_GEN_XPASS | _lib.PODS_GEN_YZPASS
+            check(self.ctx.lib.pods_df_generate_parts(self.ctx.h, rest), "pods_df_generate_parts")
+        elif self._ahead is not None:
             torch.cuda.current_stream(self.ctx.device).wait_event(self._ahead)
             rest = _lib.PODS_GEN_ALL & ~self._ahead_parts
             self._ahead, self._ahead_parts = None, 0
@@ -227,7 +281,7 @@ class Generator:
             ev = torch.cuda.Event()
             ev.record(gs)
         self._ahead = ev
-        self._ahead_parts |= parts & _lib.PODS_GEN_ALL
+        self._ahead_parts |= parts & (_lib.PODS_GEN_ALL | _lib.PODS_GEN_RECORD)
 
     def prefetch_jump(self, timer=None):
         """Enqueue the NEXT run's MT19937 jump-ahead on the gen stream, after everything the main
@@ -239,7 +293,9 @@ class Generator:
         its time -- both stream 7-13 GB through HBM -- and beside the SYRK they took 10.9 ms
         instead of 2.4 and cost the SYRK 2.7 ms, no net gain; spread over 64-256 workgroups they
         took 46-77 ms, each substream being a latency-bound twist chain.)"""
-        self._on_gen_stream(_lib.PODS_GEN_JUMP, timer, "gen_jump_ahead")
+        # with the state exchange the owned substreams' records too (they need only the seed)
+        parts = _lib.PODS_GEN_JUMP | (_lib.PODS_GEN_RECORD if self._xch is not None else 0)
+        self._on_gen_stream(parts, timer, "gen_jump_ahead")
 
     def prefetch_planes_beside_solver(self, timer=None):
         """Enqueue the NEXT run's random planes on the gen stream behind the marker the current
@@ -251,7 +307,7 @@ class Generator:
         / 4 with up to 3 or 6 generator workgroups per CU: the solver grows least this way
         (36.5 -> 36.9 ms against 37.1-37.2).  Called right after pods_syev is enqueued (after
         prefetch_jump); does nothing when no marker was recorded (ns <= 1536)."""
-        if self._ahead_parts != _lib.PODS_GEN_JUMP:
+        if self._ahead_parts != _lib.PODS_GEN_JUMP or self._xch is not None:
             return
         gs = self.ctx.gen_stream()
         if self.ctx.lib.pods_stream_wait_marker(self.ctx.h, ctypes.c_void_p(gs.cuda_stream)) != _lib.PODS_OK:
@@ -760,6 +816,24 @@ def eigen_solve_speculative(ctx: Context, C, ns, nm, tol_CN, tm, beside=None):
     return T, lam_t, Y, verify
 
 
+def pod_head(snap: DeviceSnapshots, world=1, timer=None):
+    """The mean and the (partial, when world > 1) correlation of run_pod (PODFS.py:1451-1455 after
+    main() :1492-1495), enqueued on the current stream: returns (C, mean)."""
+    ctx, lib = snap.ctx, snap.ctx.lib
+    dev = torch.device("cuda", ctx.device)
+    tm = timer or (lambda name: _NullCtx())
+    mean = torch.empty(snap.rowlen, dtype=torch.float64, device=dev)
+    with tm("mean"):
+        check(lib.pods_mean(ctx.h, ptr(mean), 1), "pods_mean")
+    if ctx.corr_mode() == 0:   # the fp64 SYRK reads A centred in place (main() :1493-1495); the
+        with tm("center"):     # int8 correlation subtracts the mean while forming its residues
+            check(lib.pods_center(ctx.h), "pods_center")
+    C = torch.empty((snap.ns, snap.ns), dtype=torch.float64, device=dev)
+    with tm("corr"):
+        check(lib.pods_corr(ctx.h, ptr(C), 1 if world == 1 else 0), "pods_corr")
+    return C, mean
+
+
 def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=False,
             keep_C=False, timer=None, on_temporal=None, spectrum=None, before_eigen=None, beside_solve=None):
     """PODFS.POD (PODFS.py:1294-1393) with correct_for_cell_volumes='false'.
@@ -789,15 +863,7 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
         ctx.detect_sharing(dist)
     dev = torch.device("cuda", ctx.device)
     tm = timer or (lambda name: _NullCtx())
-    mean = torch.empty(snap.rowlen, dtype=torch.float64, device=dev)
-    with tm("mean"):
-        check(lib.pods_mean(ctx.h, ptr(mean), 1), "pods_mean")
-    if ctx.corr_mode() == 0:   # the fp64 SYRK reads A centred in place (main() :1493-1495); the
-        with tm("center"):     # int8 correlation subtracts the mean while forming its residues
-            check(lib.pods_center(ctx.h), "pods_center")
-    C = torch.empty((ns, ns), dtype=torch.float64, device=dev)
-    with tm("corr"):
-        check(lib.pods_corr(ctx.h, ptr(C), 1 if world == 1 else 0), "pods_corr")
+    C, mean = pod_head(snap, world, timer)
     if world > 1:
         with tm("allreduce"):
             allreduce_correlation(dist, C, ns, *device_triangle_ops(ctx))
@@ -846,6 +912,22 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
                 on_temporal(T, nmt, t_ready)
         return PODResult(energy=lam_desc, num_valid=nvalid, nm=nmt, mean=mean, T=T, phi=phi[:, :nmt],
                          C=C if keep_C else None)
+    return pod_tail(ctx, snap, C, mean, nm, tol_CN, dist, full_temporal, keep_C, timer, on_temporal, spectrum)
+
+
+def pod_tail(ctx, snap, C, mean, nm, tol_CN, dist, full_temporal=False, keep_C=False, timer=None, on_temporal=None,
+             spectrum=None, solve_stream=None, c_ready=None):
+    """The part of run_pod after the correlation (PODFS.py:1309-1333) on the multi-rank / split
+    path: rank 0's eigensolve (the nm leading pairs when a SpectrumQueue takes the rest), the
+    broadcasts of lambda and T[:, :nm], every rank's spatial modes of its row slab, and the
+    spectrum units.  solve_stream (rank 0): the eigensolve runs there, after the event c_ready
+    (C complete), so a caller can have the next step's generation and correlation already on the
+    main stream (ShardedSteps); the main stream waits for the solve only before the broadcasts."""
+    dist, rank, world = _dist_info(dist)
+    lib = ctx.lib
+    ns = snap.ns
+    dev = torch.device("cuda", ctx.device)
+    tm = timer or (lambda name: _NullCtx())
     meta = torch.zeros(4, dtype=torch.int64, device=dev)
     T = lam_desc = nvalid = None
     defer = spectrum is not None
@@ -853,10 +935,21 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
         spectrum.submit(C, timer, limit=spectrum.lead)   # as that takes: rank 0 waits for them at
                                                          # the broadcast), the rest after Phi
     if rank == 0:
-        lam_desc, nvalid, nmt, T, lam_modes = eigen_solve(ctx, C, ns, nm, tol_CN, full_temporal, tm, world,
-                                                          defer_full=defer)
-        t_ready = torch.cuda.Event()
-        t_ready.record()
+        if solve_stream is not None:
+            if c_ready is not None:
+                solve_stream.wait_event(c_ready)
+            with ctx.on_stream(solve_stream):
+                lam_desc, nvalid, nmt, T, lam_modes = eigen_solve(ctx, C, ns, nm, tol_CN, full_temporal, tm, world,
+                                                                  defer_full=defer)
+                t_ready = torch.cuda.Event()
+                t_ready.record()
+            torch.cuda.current_stream(dev).wait_event(t_ready)
+            T.record_stream(torch.cuda.current_stream(dev))
+        else:
+            lam_desc, nvalid, nmt, T, lam_modes = eigen_solve(ctx, C, ns, nm, tol_CN, full_temporal, tm, world,
+                                                              defer_full=defer)
+            t_ready = torch.cuda.Event()
+            t_ready.record()
         if world > 1 and on_temporal is not None:   # beside the broadcasts and the spatial pass
             on_temporal(T, nmt, t_ready)
         meta[0] = -1 if nvalid is None else nvalid
@@ -1093,7 +1186,7 @@ def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=Non
     (Generator.prefetch_jump)."""
     dist_, rank, world = _dist_info(dist)
     tm = timer or (lambda name: _NullCtx())
-    gen = gen or Generator(setup, device=device, rank=rank, world=world)
+    gen = gen or Generator(setup, device=device, rank=rank, world=world, dist=dist_)
     with tm("generate"):
         snap = gen.generate()
     if prefetch_next:
@@ -1117,6 +1210,92 @@ def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=Non
         return gen, pod, None
     fo = pending[-1]() if pending else None
     return gen, pod, fo
+
+
+class ShardedSteps:
+    """Several ranks, several steps (bench.py --gpus N > 1): the POD tail of step k-1 runs while
+    the device already has step k's generation and correlation.
+
+    step() enqueues step k's generation (into snapshot bank k % 2, pods_select_snapshots) and its
+    mean + partial correlation, THEN runs step k-1's tail (pod_tail: rank 0 solves for the nm
+    leading pairs on its own stream behind the event of step k-1's all-reduce, so the device runs
+    that latency-bound solve beside step k's HBM / MFMA-bound kernels; the other ranks run their
+    spectrum units; broadcasts of lambda and T; every rank's spatial modes of step k-1 from bank
+    (k-1) % 2; the Fourier stage on rank 0), and only then step k's all-reduce.  Every result is
+    that of the unpipelined order bit for bit (same kernels on the same inputs); pipelined=False
+    (PODS_PIPELINE=0) runs each step's tail right after its own all-reduce.  results[k] is step
+    k's PODResult once its tail has run; flush() runs the last tail."""
+
+    def __init__(self, setup: DFSetup, gen, dist, spectrum=None, backlog=None, pipelined=None):
+        self.setup, self.gen, self.dist = setup, gen, dist
+        self.spectrum, self.backlog = spectrum, backlog
+        if pipelined is None:
+            pipelined = os.environ.get("PODS_PIPELINE", "1") != "0"
+        self.pipelined = pipelined
+        self.k = 0
+        self.pending = None
+        self.results = []
+        _, self.rank, self.world = _dist_info(dist)
+        self._solve = None
+
+    def _solve_stream(self):
+        if self._solve is None:
+            self._solve = torch.cuda.Stream(device=self.gen.ctx.device)
+        return self._solve
+
+    def step(self, timer=None, prefetch_next=False, seed=None):
+        """One step; seed: a new np.random.seed for this step's field (pods_df_set_seed; must not
+        be combined with a jump-ahead prefetched under the previous seed)."""
+        ctx = self.gen.ctx
+        tm = timer or (lambda name: _NullCtx())
+        if seed is not None:
+            check(ctx.lib.pods_df_set_seed(ctx.h, int(seed) & 0xffffffff), "pods_df_set_seed")
+        bank = self.k % 2 if self.pipelined else 0
+        check(ctx.lib.pods_select_snapshots(ctx.h, bank), "pods_select_snapshots")
+        with tm("generate"):
+            snap = self.gen.generate()
+        if prefetch_next:
+            self.gen.prefetch_jump(timer)
+        C, mean = pod_head(snap, self.world, timer)
+        if self.pending is not None:
+            self._tail(timer)
+        check(ctx.lib.pods_select_snapshots(ctx.h, bank), "pods_select_snapshots")
+        if self.world > 1:
+            ctx.detect_sharing(self.dist)
+            with tm("allreduce"):
+                allreduce_correlation(self.dist, C, snap.ns, *device_triangle_ops(ctx))
+        ready = torch.cuda.Event()
+        ready.record()
+        self.pending = (bank, snap, C, mean, ready)
+        self.k += 1
+        if not self.pipelined:
+            self._tail(timer)
+
+    def _tail(self, timer):
+        bank, snap, C, mean, ready = self.pending
+        self.pending = None
+        ctx = self.gen.ctx
+        s = self.setup
+        self.gen.join_ahead()   # the persistent spectrum kernels must not find generator workgroups
+        check(ctx.lib.pods_select_snapshots(ctx.h, bank), "pods_select_snapshots")
+        fo = []
+
+        def start_fourier(T, nmt, t_ready):
+            fo.append(launch_fourier(ctx, T, nmt, s.ns, s.dt_eff, s.et, timer=timer, side=True, ready=t_ready))
+        if self.backlog is not None:
+            self.backlog.finish_pending()
+        pod = pod_tail(ctx, snap, C, mean, s.nm, 1.0e-15, self.dist, timer=timer, on_temporal=start_fourier,
+                       spectrum=self.spectrum, solve_stream=self._solve_stream() if self.rank == 0 else None,
+                       c_ready=ready)
+        self.results.append(pod)
+        if self.backlog is not None:
+            self.backlog.pending.append(fo[-1] if fo else None)
+
+    def flush(self, timer=None):
+        if self.pending is not None:
+            self._tail(timer)
+        if self.backlog is not None:
+            self.backlog.finish_pending()
 
 
 def wall():

@@ -138,6 +138,79 @@ def _rank_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
+PIPE_SEEDS = (11, 12, 13)
+
+
+def _steps_worker(rank, world, port, out):
+    """Three steps of different seeds through engine.ShardedSteps, pipelined (step k-1's tail
+    after step k's generation and correlation, two snapshot banks, rank 0's solve on its own
+    stream) and not; every per-step output kept."""
+    import torch
+    import torch.distributed as dist
+    import podsgen
+    from podsgen import engine as E
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    s = podsgen.DFSetup(jma=48, kma=40, ns=1024, seed=PIPE_SEEDS[0])
+    res = {}
+    for pipelined in (True, False):
+        gen = E.Generator(s, device=0, rank=rank, world=world, dist=dist)
+        spectrum = E.SpectrumQueue(gen.ctx, s.ns, rank, world)
+        backlog = E.FourierBacklog()
+        run = E.ShardedSteps(s, gen, dist, spectrum, backlog, pipelined=pipelined)
+        for seed in PIPE_SEEDS:
+            run.step(seed=seed)
+        run.flush()
+        spectrum.drain()
+        torch.cuda.synchronize()
+        res[pipelined] = dict(
+            T=[p.T.cpu().numpy() for p in run.results], phi=[p.phi.cpu().numpy() for p in run.results],
+            mean=[p.mean.cpu().numpy() for p in run.results], nm=[p.nm for p in run.results],
+            spectra=spectrum.results(),
+            fc=[None if f is None else (f.c, f.c_count, f.FC) for f in backlog.results])
+        gen.ctx.close()
+    out[rank] = res
+    dist.destroy_process_group()
+
+
+def test_pipelined_steps_bit_equal_two_ranks_one_device():
+    """with several ranks, step k-1's POD tail (rank 0's leading-pair solve on
+    its own stream, the broadcasts, the spatial modes from the other snapshot bank, the Fourier
+    stage) runs after step k's generation and correlation are enqueued.  On 2 ranks (gloo, one
+    GPU), three steps of different seeds: lambda (the spread spectra), T, Phi, the mean, nm and
+    the Fourier coefficients / counts / FC rows equal the unpipelined run's bit for bit, and the
+    steps differ from each other (so a bank mix-up would show)."""
+    import multiprocessing as mp
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = 29700 + os.getpid() % 1000
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_steps_worker, args=(r, 2, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(600)
+        assert p.exitcode == 0
+    for r in range(2):
+        a, b = out[r][True], out[r][False]
+        assert a["nm"] == b["nm"]
+        for key in ("T", "phi", "mean"):
+            for k in range(len(PIPE_SEEDS)):
+                assert np.array_equal(a[key][k], b[key][k]), (r, key, k)
+            assert not np.array_equal(a[key][0], a[key][1]), (r, key)
+        assert sorted(a["spectra"]) == sorted(b["spectra"])
+        for k in a["spectra"]:
+            assert np.array_equal(a["spectra"][k], b["spectra"][k]), (r, k)
+        assert len(a["fc"]) == len(b["fc"])
+        for fa, fb in zip(a["fc"], b["fc"]):
+            assert (fa is None) == (fb is None)
+            if fa is not None:
+                for x, y in zip(fa, fb):
+                    assert np.array_equal(x, y)
+    assert sum(len(out[r][True]["spectra"]) for r in range(2)) == len(PIPE_SEEDS)
+    assert out[0][True]["fc"][0] is not None
+
+
 def test_sharded_pipeline_two_ranks_one_device():
     """Row slabs on 2 ranks (gloo transport, one GPU) == the single-rank pipeline."""
     import multiprocessing as mp

@@ -341,6 +341,38 @@ def test_row_slabs_large(ctx, J, K, ns, world):
         assert np.array_equal(rows, full[comp * P:(comp + 1) * P]), comp
 
 
+@pytest.mark.parametrize("J,K,ns,world", [(256, 256, 40, 8), (96, 70, 33, 5), (64, 40, 61, 2), (64, 40, 5, 3)])
+def test_mt_state_exchange_bit_exact(J, K, ns, world):
+    """The multi-GPU state exchange (pods_df_set_exchange): every rank twists only its 1/world of
+    the MT19937 stream, records the segment-start states of every rank, the records move by an
+    all_to_all (emulated here on one device: rank r's send chunk for q, concatenated over r),
+    and each rank regenerates only its own row segments -- the snapshot rows bit for bit those of
+    the slab generator that twists the whole stream (digitalfilters.py:1361-1367, :1454-1467)."""
+    s = podsgen.DFSetup(jma=J, kma=K, ns=ns, seed=977)
+    gens = [E.Generator(s, rank=r, world=world, ctx=E.Context(0), exchange=False) for r in range(world)]
+    for g in gens:
+        g.enable_exchange()
+        podsgen.check(g.ctx.lib.pods_df_generate_parts(g.ctx.h, _lib.PODS_GEN_JUMP | _lib.PODS_GEN_RECORD), "record")
+    torch.cuda.synchronize()
+    for q, gq in enumerate(gens):
+        chunks = []
+        for gr in gens:
+            sb = gr._xch[0]
+            off = sum(sb[:q])
+            chunks.append(gr._send[off:off + sb[q]])
+        recv = torch.cat(chunks)
+        assert recv.numel() == sum(gq._xch[1])
+        gq._recv[:recv.numel()].copy_(recv)
+        podsgen.check(gq.ctx.lib.pods_df_generate_parts(
+            gq.ctx.h, _lib.PODS_GEN_PLANES | _lib.PODS_GEN_XPASS | _lib.PODS_GEN_YZPASS), "segments")
+    for q, gq in enumerate(gens):
+        got = gq.snapshots().to_host()
+        ref = E.Generator(s, rank=q, world=world, ctx=gq.ctx, exchange=False).generate().to_host()
+        assert np.array_equal(got, ref), q
+    for g in gens:
+        g.ctx.close()
+
+
 def test_center_in_place(ctx):
     """pods_center: A - mean (main() :1493-1495) in place, bit for bit the numpy subtraction;
     the correlation from the centred A equals the one that subtracts inside the SYRK."""

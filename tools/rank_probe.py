@@ -2,7 +2,7 @@
 the all-reduce): generate + mean (+ centre with the fp64 SYRK) + partial correlation for rank 0's row slab at world = 1, 2,
 4, 8, in steady state, without and with the next step's MT19937 jump-ahead on the gen stream
 (Generator.prefetch_jump, as bench.py runs it).
-   python tools/rank_probe.py [J K NS]"""
+   python tools/rank_probe.py [J K NS [WORLDS]]   (WORLDS: comma-separated, default 1,2,4,8)"""
 import os
 import sys
 import time
@@ -14,9 +14,10 @@ import podsgen  # noqa: E402
 from podsgen import engine as E  # noqa: E402
 
 J, K, NS = (int(a) for a in sys.argv[1:4]) if len(sys.argv) > 3 else (256, 256, 4096)
+WORLDS = [int(w) for w in sys.argv[4].split(",")] if len(sys.argv) > 4 else [1, 2, 4, 8]
 s = podsgen.DFSetup(jma=J, kma=K, ns=NS, seed=12345)
 ctx = E.Context(0)
-for world in (1, 2, 4, 8):
+for world in WORLDS:
     gen = E.Generator(s, rank=0, world=world, ctx=ctx)
     C = torch.empty((NS, NS), dtype=torch.float64, device="cuda")
     mean = torch.empty(gen.rowlen, dtype=torch.float64, device="cuda")
