@@ -326,10 +326,36 @@ __device__ __forceinline__ int swz(int quartet) { return (0x78 >> (2 * quartet))
 // are read between the two halves of step t's MFMAs.  A diagonal tile (SAME) loads one panel and
 // reads it as both operands.  items: {bi, bj, split, -} (bi < 0: an empty slot that keeps the
 // item count a multiple of 8).  DIAG (measurement only): 1 = no MFMAs, 2 = no operand traffic.
+// Soft XCD pacing (the persistent SYRK): one lane of the workgroup counts it in and waits until
+// all nslot workgroups of its XCD have arrived `epoch` times, or a bounded spin has passed.  It
+// only paces the workgroups that share an L2 (so they read the same K window of the same panels);
+// no data moves through it, so a timeout (a workgroup not resident yet) costs time, never
+// correctness.  Raw s_barrier (no memory drain) around it; vector atomics only.
+__device__ __forceinline__ void pace_xcd(unsigned* ctr, unsigned& epoch, unsigned nslot) {
+  ++epoch;
+  __builtin_amdgcn_s_barrier();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = epoch * nslot;
+    for (int spin = 0; spin < (1 << 14); ++spin) {
+      if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __builtin_amdgcn_s_barrier();
+}
+
+struct Pacer {
+  unsigned* ctr = nullptr;  // null: no pacing
+  unsigned epoch = 0;
+  unsigned nslot = 0;
+  int every = 0;            // K steps between pacing points inside a tile (0: none)
+};
+
 template <int NST, int DIAG, bool SAME, int ILV>
 __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int64_t cstride, int ns, int nt, int i0,
                                           int j0, int m, char* smem, uint8_t* __restrict__ dst, int ldp,
-                                          int accumulate) {
+                                          int accumulate, Pacer* pacer = nullptr) {
   constexpr int STG = 2 * PANEL;
   constexpr int Q = SAME ? 2 : 4;  // DMA instructions per wave per stage
   constexpr int D = NST - 2;       // DMA lead in K steps beyond the one being read
@@ -439,7 +465,11 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int64
       if (ILV == 0 || idle)
         if (t + D + 1 < nt) issue(t + D + 1);
     }
-    if (idle) return;
+    if (idle) {
+      if (pacer && pacer->every > 0 && (t + 1) % pacer->every == 0 && t + 1 < nt)
+        pace_xcd(pacer->ctr, pacer->epoch, pacer->nslot);
+      return;
+    }
     const int dt = ILV != 0 && t + D + 1 < nt ? t + D + 1 : -1;
     mma_rows(ac, bc, 0, ILV == 4 ? -1 : dt, 0, ILV == 2 ? 2 : 1);
     __builtin_amdgcn_sched_barrier(0);
@@ -447,6 +477,8 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int64
     __builtin_amdgcn_sched_barrier(0);
     mma_rows(ac, bc, 4, ILV == 2 || ILV == 4 ? dt : -1, ILV == 2 ? 2 : 0, ILV == 2 ? 2 : 1);
     fold(t);
+    if (pacer && pacer->every > 0 && (t + 1) % pacer->every == 0 && t + 1 < nt)
+      pace_xcd(pacer->ctr, pacer->epoch, pacer->nslot);
   };
   int t = 0;
   for (; t + 1 < nt; t += 2) {
@@ -499,6 +531,46 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8(const int8_t* __restrict__ R
     syrk_tile<NST, DIAG, true, ILV>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
   else
     syrk_tile<NST, DIAG, false, ILV>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
+}
+
+// The persistent, XCD-paced form (r5): one 512-thread workgroup per CU, workgroup b on XCD b % 8
+// (dispatch deals blocks round-robin over the XCDs) as slot b / 8 of nslot.  XCD x's items (its
+// share of every modulus' lower tiles and K splits, host-ordered so that one round -- nslot
+// consecutive items -- is a compact block of tiles of one modulus and split) are taken in rounds,
+// slot s taking item r * nslot + s of round r, with a soft pacing point after every round and,
+// with pace_every > 0, every pace_every K steps inside a tile: the workgroups that share an L2
+// then stream the same K window of the same panels (the launch-per-item form let them drift apart
+// over the 17 rounds at C3, and the XCD's 4 MB L2 held the union of their windows: 54 % hits).
+template <int NST, int ILV>
+__global__ __launch_bounds__(512, 1) void k_syrk_i8_paced(const int8_t* __restrict__ R, int ns, int64_t ms, int64_t cs,
+                                                          int kcs, const int4* __restrict__ xitems, int per_xcd,
+                                                          int nsplit, uint8_t* __restrict__ P, int64_t pslab, int ldp,
+                                                          int accumulate, unsigned* __restrict__ pace_ctr,
+                                                          int pace_every) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int x = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  Pacer pc;
+  pc.ctr = pace_ctr + x * 32;  // one 128-B line per XCD
+  pc.nslot = gridDim.x >> 3;
+  pc.every = pace_every;
+  const int rounds = (per_xcd + (int)pc.nslot - 1) / (int)pc.nslot;
+  for (int r = 0; r < rounds; ++r) {
+    const int idx = r * (int)pc.nslot + slot;
+    const int4 it = idx < per_xcd ? xitems[(int64_t)x * per_xcd + idx] : make_int4(-1, -1, 0, 0);
+    if (it.x >= 0) {
+      const int bi = it.x, bj = it.y, sp = it.z, l = it.w;
+      const int8_t* base = R + (int64_t)l * ms + (int64_t)sp * kcs * cs;
+      uint8_t* dst = P + (int64_t)(l * nsplit + sp) * pslab;
+      const int m = modulus(l);
+      if (bi == bj)
+        syrk_tile<NST, 0, true, ILV>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate, &pc);
+      else
+        syrk_tile<NST, 0, false, ILV>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate, &pc);
+    } else if (pace_every > 0) {  // an empty slot still keeps the tile's pacing points
+      for (int t = pace_every; t < kcs; t += pace_every) pace_xcd(pc.ctr, pc.epoch, pc.nslot);
+    }
+    pace_xcd(pc.ctr, pc.epoch, pc.nslot);
+  }
 }
 
 // ---- CRT reconstruction ----------------------------------------------------------------------
@@ -813,6 +885,59 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
   const int64_t cs = ilv ? (int64_t)NMOD * ns * KC : (int64_t)ns * KC;
   const int ldp = (ns + 63) / 64 * 64;
   const int64_t pslab = (int64_t)ns * ldp;
+  // PODS_SYRK_PACE (A/B): "p" = the persistent XCD-paced kernel (k_syrk_i8_paced) with a pacing
+  // point after every round of items; "p<N>" = also every N K steps inside a tile
+  int paced = 0, pace_every = 0;
+  if (const char* v = std::getenv("PODS_SYRK_PACE")) {
+    if (v[0] == 'p') {
+      paced = 1;
+      pace_every = v[1] ? std::atoi(v + 1) : 0;
+    }
+  }
+  std::vector<int> xit;
+  int per_xcd = 0, nslot = 0;
+  struct Buf {
+    void* p = nullptr;
+    size_t bytes = 0;
+  };
+  static thread_local Buf xbuf, pbuf;  // the paced kernel's item table and pacing counters
+  if (paced) {
+    int dev = 0, cus = 0;
+    e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    nslot = std::max(1, cus / 8);
+    // XCD x's items in grid order (item 8k + x of every modulus), empty slots dropped
+    std::vector<std::vector<int>> per(8);
+    std::vector<int> h((size_t)p.nitems * 4);
+    e = hipMemcpy(h.data(), items, h.size() * sizeof(int), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return e;
+    for (int l = 0; l < NMOD; ++l)
+      for (int k = 0; k < p.nitems; ++k) {
+        const int x = k & 7;
+        if (h[4 * k] < 0) continue;
+        per[x].insert(per[x].end(), {h[4 * k], h[4 * k + 1], h[4 * k + 2], l});
+      }
+    for (int x = 0; x < 8; ++x) per_xcd = std::max(per_xcd, (int)per[x].size() / 4);
+    xit.assign((size_t)8 * per_xcd * 4, -1);
+    for (int x = 0; x < 8; ++x) std::copy(per[x].begin(), per[x].end(), xit.begin() + (size_t)x * per_xcd * 4);
+    auto ens = [](Buf& b, size_t bytes) -> hipError_t {
+      if (b.bytes >= bytes) return hipSuccess;
+      if (b.p) (void)hipFree(b.p);
+      b.p = nullptr;
+      b.bytes = 0;
+      hipError_t r = hipMalloc(&b.p, bytes);
+      if (r == hipSuccess) b.bytes = bytes;
+      return r;
+    };
+    e = ens(xbuf, xit.size() * sizeof(int));
+    if (e == hipSuccess) e = ens(pbuf, 8 * 32 * sizeof(unsigned));
+    if (e == hipSuccess) e = hipMemcpyAsync(xbuf.p, xit.data(), xit.size() * sizeof(int), hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_syrk_i8_paced<5, 1>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)(5 * 2 * PANEL));
+    if (e != hipSuccess) return e;
+  }
   if (syrk_begin && p.nlaunch > 1) e = hipEventRecord(syrk_begin, st);
   if (e != hipSuccess) return e;
   for (int li = 0; li < p.nlaunch; ++li) {
@@ -839,7 +964,13 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
     // the events bracket the SYRK launch (with several launches: the first residue pass to the last SYRK)
     if (syrk_begin && p.nlaunch == 1) e = hipEventRecord(syrk_begin, st);
     if (e != hipSuccess) return e;
-    {
+    if (paced) {
+      e = hipMemsetAsync(pbuf.p, 0, 8 * 32 * sizeof(unsigned), st);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL((k_syrk_i8_paced<5, 1>), dim3(8 * nslot), dim3(512), 5 * 2 * PANEL, st,
+                         (const int8_t*)R, ns, ms, cs, p.kcs, reinterpret_cast<const int4*>(xbuf.p), per_xcd,
+                         p.nsplit, P, pslab, ldp, li > 0 ? 1 : 0, static_cast<unsigned*>(pbuf.p), pace_every);
+    } else {
       const int ldp_ = ldp;
       const int acc_ = li > 0 ? 1 : 0;
       const char* ord = std::getenv("PODS_CORR_ORDER");
