@@ -289,6 +289,85 @@ __device__ __forceinline__ void residues_body(const double* __restrict__ AT, int
   });
 }
 
+// Half-width variant (A/B, PODS_RES_I8=2): thread (chunk kc, snapshot i, eighth h) converts the
+// 8 rows r = 64 kc + 8 h + e (half of one 16-row run) and stores 8 bytes per modulus -- half the
+// registers (a[8], 4 limb pairs), so twice the waves per SIMD to keep the HBM writes in flight.
+__device__ __forceinline__ void residues_half(const double* __restrict__ AT, int ns, int64_t rowlen,
+                                              int64_t rowpad, const double* __restrict__ mean,
+                                              const double* __restrict__ devmax, int bbits, int64_t kc0,
+                                              int64_t nkc, int8_t* __restrict__ R, int64_t ms, int64_t cs) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int h = (int)(t & 7);
+  const int64_t rest = t >> 3;
+  if (rest >= nkc * ns) return;
+  const int i = (int)(rest % ns);
+  const int64_t kcl = rest / ns;
+  const int64_t r0 = (kc0 + kcl) * 64 + h * 8;
+  double a[8];
+  if (r0 < rowpad) {
+    const double2* src = reinterpret_cast<const double2*>(AT + ((((r0 >> 4) * ns) + i) << 4) + (r0 & 15));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const double2 v = src[e];
+      a[2 * e] = v.x;
+      a[2 * e + 1] = v.y;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = r0 + e < rowlen ? a[e] - mean[r0 + e] : 0.0;  // main() :1494
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = 0.0;
+  }
+  const int sg = scale_exp(*devmax, bbits);
+  int8_t* const rb = R + kcl * cs;
+  const uint32_t doff = (uint32_t)(i * 64 + h * 8);
+  constexpr float MAG = 12582912.0f;
+  float Fs[5][8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const double z = rint(ldexp(a[e], sg)) + 0x1p52;
+    const double hh = floor(z * 0x1p-32);
+    const uint32_t lo = (uint32_t)__builtin_fma(-hh, 0x1p32, z), hi = (uint32_t)hh;
+    Fs[0][e] = (float)(lo & 0x7FFu);
+    Fs[1][e] = (float)((lo >> 11) & 0x7FFu);
+    Fs[2][e] = (float)(((lo >> 22) | (hi << 10)) & 0x7FFu);
+    Fs[3][e] = (float)((hi >> 1) & 0x7FFu);
+    Fs[4][e] = (float)(hi >> 12);
+  }
+  f32x2 F[5][4];
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+#pragma unroll
+    for (int pr = 0; pr < 4; ++pr) F[k][pr] = (f32x2){Fs[k][2 * pr], Fs[k][2 * pr + 1]};
+  sfor<0, NMOD>([&](auto L) {
+    constexpr int l = decltype(L)::value;
+    constexpr float m = (float)kT.m[l], inv = 1.0f / (float)kT.m[l], o = (float)kT.off[l];
+    constexpr float c1 = (float)kT.p11[l][1], c2 = (float)kT.p11[l][2], c3 = (float)kT.p11[l][3],
+                    c4 = (float)kT.p11[l][4];
+    f32x2 sv[4];
+#pragma unroll
+    for (int pr = 0; pr < 4; ++pr) {
+      f32x2 v = __builtin_elementwise_fma(F[1][pr], (f32x2){c1, c1}, F[0][pr]);
+      v = __builtin_elementwise_fma(F[2][pr], (f32x2){c2, c2}, v);
+      v = __builtin_elementwise_fma(F[3][pr], (f32x2){c3, c3}, v);
+      v = __builtin_elementwise_fma(F[4][pr], (f32x2){c4, c4}, v);
+      v = v + (f32x2){o, o};
+      f32x2 qv = __builtin_elementwise_fma(v, (f32x2){inv, inv}, (f32x2){MAG, MAG}) - (f32x2){MAG, MAG};
+      v = __builtin_elementwise_fma(-qv, (f32x2){m, m}, v);
+      sv[pr] = v + (f32x2){MAG, MAG};
+    }
+    uint32_t w[2];
+#pragma unroll
+    for (int pq = 0; pq < 2; ++pq) {
+      const f32x2 u = sv[2 * pq], v = sv[2 * pq + 1];
+      const uint32_t h0 = __builtin_amdgcn_perm(__float_as_uint(u.y), __float_as_uint(u.x), 0x0C0C0400u);
+      const uint32_t h1 = __builtin_amdgcn_perm(__float_as_uint(v.y), __float_as_uint(v.x), 0x0C0C0400u);
+      w[pq] = h0 | (h1 << 16);
+    }
+    *reinterpret_cast<uint2*>(rb + (int64_t)l * ms + doff) = make_uint2(w[0], w[1]);
+  });
+}
+
 #define PODS_RES_ARGS const double* __restrict__ AT, int ns, int64_t rowlen, int64_t rowpad, \
     const double* __restrict__ mean, const double* __restrict__ devmax, int bbits, int64_t kc0, int64_t nkc, \
     int8_t* __restrict__ R, int64_t ms, int64_t cs
@@ -297,6 +376,7 @@ template <int V>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) void k_residues(PODS_RES_ARGS) {
   residues_body<V>(PODS_RES_PASS);
 }
+__global__ __launch_bounds__(256) void k_residues_half(PODS_RES_ARGS) { residues_half(PODS_RES_PASS); }
 #undef PODS_RES_ARGS
 #undef PODS_RES_PASS
 
@@ -345,17 +425,12 @@ __device__ __forceinline__ void pace_xcd(unsigned* ctr, unsigned& epoch, unsigne
   __builtin_amdgcn_s_barrier();
 }
 
-struct Pacer {
-  unsigned* ctr = nullptr;  // null: no pacing
-  unsigned epoch = 0;
-  unsigned nslot = 0;
-  int every = 0;            // K steps between pacing points inside a tile (0: none)
-};
 
 template <int NST, int DIAG, bool SAME, int ILV>
 __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int64_t cstride, int ns, int nt, int i0,
                                           int j0, int m, char* smem, uint8_t* __restrict__ dst, int ldp,
-                                          int accumulate, Pacer* pacer = nullptr) {
+                                          int accumulate, unsigned* pctr = nullptr, unsigned pslot = 0,
+                                          int pevery = 0, unsigned* pepoch = nullptr) {
   constexpr int STG = 2 * PANEL;
   constexpr int Q = SAME ? 2 : 4;  // DMA instructions per wave per stage
   constexpr int D = NST - 2;       // DMA lead in K steps beyond the one being read
@@ -465,11 +540,7 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int64
       if (ILV == 0 || idle)
         if (t + D + 1 < nt) issue(t + D + 1);
     }
-    if (idle) {
-      if (pacer && pacer->every > 0 && (t + 1) % pacer->every == 0 && t + 1 < nt)
-        pace_xcd(pacer->ctr, pacer->epoch, pacer->nslot);
-      return;
-    }
+    if (idle) return;
     const int dt = ILV != 0 && t + D + 1 < nt ? t + D + 1 : -1;
     mma_rows(ac, bc, 0, ILV == 4 ? -1 : dt, 0, ILV == 2 ? 2 : 1);
     __builtin_amdgcn_sched_barrier(0);
@@ -477,13 +548,13 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int64
     __builtin_amdgcn_sched_barrier(0);
     mma_rows(ac, bc, 4, ILV == 2 || ILV == 4 ? dt : -1, ILV == 2 ? 2 : 0, ILV == 2 ? 2 : 1);
     fold(t);
-    if (pacer && pacer->every > 0 && (t + 1) % pacer->every == 0 && t + 1 < nt)
-      pace_xcd(pacer->ctr, pacer->epoch, pacer->nslot);
   };
   int t = 0;
   for (; t + 1 < nt; t += 2) {
     step(t, a0, b0, a1, b1);
     step(t + 1, a1, b1, a0, b0);
+    // a pacing point of the persistent kernel (pevery even), between two K steps
+    if (pevery > 0 && (t + 2) % pevery == 0 && t + 2 < nt) pace_xcd(pctr, *pepoch, pslot);
   }
   if (t < nt) step(t, a0, b0, a1, b1);
   const int fr = lane & 15, fq = lane >> 4;
@@ -541,7 +612,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8(const int8_t* __restrict__ R
 // with pace_every > 0, every pace_every K steps inside a tile: the workgroups that share an L2
 // then stream the same K window of the same panels (the launch-per-item form let them drift apart
 // over the 17 rounds at C3, and the XCD's 4 MB L2 held the union of their windows: 54 % hits).
-template <int NST, int ILV>
+template <int NST, int ILV, bool MID>
 __global__ __launch_bounds__(512, 1) void k_syrk_i8_paced(const int8_t* __restrict__ R, int ns, int64_t ms, int64_t cs,
                                                           int kcs, const int4* __restrict__ xitems, int per_xcd,
                                                           int nsplit, uint8_t* __restrict__ P, int64_t pslab, int ldp,
@@ -549,13 +620,13 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8_paced(const int8_t* __restri
                                                           int pace_every) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int x = blockIdx.x & 7, slot = blockIdx.x >> 3;
-  Pacer pc;
-  pc.ctr = pace_ctr + x * 32;  // one 128-B line per XCD
-  pc.nslot = gridDim.x >> 3;
-  pc.every = pace_every;
-  const int rounds = (per_xcd + (int)pc.nslot - 1) / (int)pc.nslot;
+  unsigned* const ctr = pace_ctr + x * 32;  // one 128-B line per XCD
+  const unsigned nslot = gridDim.x >> 3;
+  unsigned epoch = 0;
+  const int rounds = (per_xcd + (int)nslot - 1) / (int)nslot;
+#pragma clang loop unroll(disable)
   for (int r = 0; r < rounds; ++r) {
-    const int idx = r * (int)pc.nslot + slot;
+    const int idx = r * (int)nslot + slot;
     const int4 it = idx < per_xcd ? xitems[(int64_t)x * per_xcd + idx] : make_int4(-1, -1, 0, 0);
     if (it.x >= 0) {
       const int bi = it.x, bj = it.y, sp = it.z, l = it.w;
@@ -563,13 +634,15 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8_paced(const int8_t* __restri
       uint8_t* dst = P + (int64_t)(l * nsplit + sp) * pslab;
       const int m = modulus(l);
       if (bi == bj)
-        syrk_tile<NST, 0, true, ILV>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate, &pc);
+        syrk_tile<NST, 0, true, ILV>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate, ctr, nslot,
+                                     MID ? pace_every : 0, &epoch);
       else
-        syrk_tile<NST, 0, false, ILV>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate, &pc);
-    } else if (pace_every > 0) {  // an empty slot still keeps the tile's pacing points
-      for (int t = pace_every; t < kcs; t += pace_every) pace_xcd(pc.ctr, pc.epoch, pc.nslot);
+        syrk_tile<NST, 0, false, ILV>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate, ctr, nslot,
+                                      MID ? pace_every : 0, &epoch);
+    } else if (MID && pace_every > 0) {  // an empty slot still keeps the tile's pacing points
+      for (int t = pace_every; t < kcs; t += pace_every) pace_xcd(ctr, epoch, nslot);
     }
-    pace_xcd(pc.ctr, pc.epoch, pc.nslot);
+    pace_xcd(ctr, epoch, nslot);
   }
 }
 
@@ -934,18 +1007,23 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
     if (e == hipSuccess) e = ens(pbuf, 8 * 32 * sizeof(unsigned));
     if (e == hipSuccess) e = hipMemcpyAsync(xbuf.p, xit.data(), xit.size() * sizeof(int), hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_syrk_i8_paced<5, 1>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)(5 * 2 * PANEL));
-    if (e != hipSuccess) return e;
+    for (const void* f : {reinterpret_cast<const void*>(&k_syrk_i8_paced<5, 1, false>),
+                          reinterpret_cast<const void*>(&k_syrk_i8_paced<5, 1, true>)}) {
+      e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(5 * 2 * PANEL));
+      if (e != hipSuccess) return e;
+    }
   }
   if (syrk_begin && p.nlaunch > 1) e = hipEventRecord(syrk_begin, st);
   if (e != hipSuccess) return e;
   for (int li = 0; li < p.nlaunch; ++li) {
     const int64_t kc0 = (int64_t)li * p.chunks;
-    const int64_t thr = p.chunks * ns * 4;
-    // PODS_RES_I8=1 (A/B runs): the signed 14-bit-limb residues (measured the same)
+    // PODS_RES_I8=1 (A/B runs): the signed 14-bit-limb residues (measured the same); =2 the
+    // half-width threads (8 rows each)
     const char* rv = std::getenv("PODS_RES_I8");
-    const void* rk = rv && rv[0] == '1' ? reinterpret_cast<const void*>(&k_residues<1>)
+    const bool half = rv && rv[0] == '2';
+    const int64_t thr = p.chunks * ns * (half ? 8 : 4);
+    const void* rk = half ? reinterpret_cast<const void*>(&k_residues_half)
+                   : rv && rv[0] == '1' ? reinterpret_cast<const void*>(&k_residues<1>)
                                         : reinterpret_cast<const void*>(&k_residues<0>);
     {
       const double* AT_ = AT;
@@ -967,9 +1045,14 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
     if (paced) {
       e = hipMemsetAsync(pbuf.p, 0, 8 * 32 * sizeof(unsigned), st);
       if (e != hipSuccess) return e;
-      hipLaunchKernelGGL((k_syrk_i8_paced<5, 1>), dim3(8 * nslot), dim3(512), 5 * 2 * PANEL, st,
-                         (const int8_t*)R, ns, ms, cs, p.kcs, reinterpret_cast<const int4*>(xbuf.p), per_xcd,
-                         p.nsplit, P, pslab, ldp, li > 0 ? 1 : 0, static_cast<unsigned*>(pbuf.p), pace_every);
+      if (pace_every > 0)
+        hipLaunchKernelGGL((k_syrk_i8_paced<5, 1, true>), dim3(8 * nslot), dim3(512), 5 * 2 * PANEL, st,
+                           (const int8_t*)R, ns, ms, cs, p.kcs, reinterpret_cast<const int4*>(xbuf.p), per_xcd,
+                           p.nsplit, P, pslab, ldp, li > 0 ? 1 : 0, static_cast<unsigned*>(pbuf.p), pace_every);
+      else
+        hipLaunchKernelGGL((k_syrk_i8_paced<5, 1, false>), dim3(8 * nslot), dim3(512), 5 * 2 * PANEL, st,
+                           (const int8_t*)R, ns, ms, cs, p.kcs, reinterpret_cast<const int4*>(xbuf.p), per_xcd,
+                           p.nsplit, P, pslab, ldp, li > 0 ? 1 : 0, static_cast<unsigned*>(pbuf.p), 0);
     } else {
       const int ldp_ = ldp;
       const int acc_ = li > 0 ? 1 : 0;
