@@ -28,7 +28,7 @@ hipError_t launch_mt_chains(int mode, const uint32_t* st0, const int64_t* b0, co
                             int64_t ntot, int64_t S, int Kp, int rlo, int rhi, int64_t Sl, double low, double range,
                             double* out, hipStream_t st);
 hipError_t launch_filter_x(int NX, const double* R, const double* bx, int ns, int64_t Sl, int ncomp,
-                           int chunk, double* T1, hipStream_t st);
+                           int chunk, double* T1, hipStream_t st, int s0 = 0, int s1 = -1);
 // lund_sj: 0 = one row of 9 x K parameters for every j (plain layout lund[e * Pl + k]);
 // otherwise the table is j-varying and in the chunk-major layout below
 inline int64_t lund_chunk_index(int64_t j, int e, int k, int K) {
@@ -39,7 +39,7 @@ inline int64_t lund_chunk_size(int64_t jl, int K) { return jl * 9 * 16 * (int64_
 hipError_t launch_filter_yz(int NY, const double* T1, const double* by, const double* bz, int NZ,
                             int ns, int jl, int K, int Kp, int64_t Sl, int ncomp,
                             const double* lund, int64_t lund_sj, int lund_mode, const double* rot,
-                            int rotate, double* AT, hipStream_t st);
+                            int rotate, double* AT, hipStream_t st, int s0 = 0, int s1 = -1);
 int filter_yz_max_K(int Kp);
 hipError_t launch_lund_apply(double* yu, double* yv, double* yw, int64_t P, const double* lund,
                              int lund_mode, const double* rot, int rotate, hipStream_t st);

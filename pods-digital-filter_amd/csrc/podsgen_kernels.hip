@@ -512,15 +512,16 @@ template <int NX, int PD, bool NT = false>
 __global__ __launch_bounds__(256) void k_filter_x2(const double* __restrict__ R,
                                                    const double* __restrict__ bx, int ns,
                                                    int64_t Sl, int steps_per_chunk,
-                                                   double* __restrict__ T1, int nbx, int ncomp, int nch) {
+                                                   double* __restrict__ T1, int nbx, int ncomp, int nch,
+                                                   int s0, int s1) {
   // virtual blocks (point block, component, step chunk), one per workgroup
   const int nvb = nbx * ncomp * nch;
   for (int vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
   const int bxi = vb % nbx, c = (vb / nbx) % ncomp, bz = vb / (ncomp * nbx);
   const int64_t pp = (int64_t)bxi * 256 + threadIdx.x;  // point pair
   if (2 * pp >= Sl) continue;
-  const int i0 = bz * steps_per_chunk;
-  const int i1 = min(ns, i0 + steps_per_chunk);
+  const int i0 = s0 + bz * steps_per_chunk;  // steps [s0, s1) of the ns (a chunk of the generation)
+  const int i1 = min(s1, i0 + steps_per_chunk);
   if (i0 >= i1) continue;
   double b[NX];
 #pragma unroll
@@ -585,7 +586,7 @@ __global__ __launch_bounds__(NT) void k_filter_yz(
     const double* __restrict__ T1, const double* __restrict__ by, const double* __restrict__ bz,
     int NZr, int ns, int jl, int K, int Kp, int64_t Sl, int ncomp,
     const double* __restrict__ lund, int64_t lund_sj, int lund_mode, const double* __restrict__ rot,
-    int rotate, double* __restrict__ AT, int nsb, int KB) {
+    int rotate, double* __restrict__ AT, int nsb, int KB, int s0, int s1) {
   extern __shared__ __attribute__((aligned(16))) double t2[];  // TJ x ldt
   constexpr int YR = TJ < 16 ? TJ : 16;  // rows per y-pass item
   constexpr int NZMAX = NZC > 0 ? NZC : 25;
@@ -639,8 +640,8 @@ __global__ __launch_bounds__(NT) void k_filter_yz(
   }
   // NSB consecutive steps per block: each thread's stores for one snapshot-row group then
   // land on consecutive 128-B lines of the K-tiled layout (steps are contiguous there)
-  const int ib = group_y * nsb;
-  const int ie = min(ns, ib + nsb);
+  const int ib = s0 + group_y * nsb;  // steps [s0, s1) of the ns
+  const int ie = min(s1, ib + nsb);
 #pragma clang loop unroll(disable)
   for (int i = ib; i < ie; ++i) {
     // the Lund table pointer is re-materialised per step: otherwise the (step-invariant)
@@ -1350,8 +1351,9 @@ hipError_t launch_mt_generate(const uint32_t* states, int G, int64_t Bs, int64_t
 
 template <int NX>
 static hipError_t launch_fx(const double* R, const double* bx, int ns, int64_t Sl, int ncomp,
-                            int chunk, double* T1, hipStream_t st) {
+                            int chunk, double* T1, hipStream_t st, int s0, int s1) {
   if (Sl % 2 == 0 && ((uintptr_t)R & 15) == 0 && ((uintptr_t)T1 & 15) == 0) {
+    const int nsr = s1 - s0;  // steps of this launch
     // point pairs: half the threads, so twice the step chunks keep the same parallelism
     // with PD loads in flight per wave, about four resident workgroups per CU suffice: step
     // chunks so the grid is one round of ~1024 workgroups (a partial second round of a
@@ -1359,9 +1361,9 @@ static hipError_t launch_fx(const double* R, const double* bx, int ns, int64_t S
     (void)chunk;
     const int64_t bx_ = (Sl / 2 + 255) / 256;
     const int64_t want = 1024;
-    const int64_t nch0 = std::max<int64_t>(1, std::min<int64_t>(ns, want / std::max<int64_t>(1, bx_ * ncomp)));
-    const int chunk2 = (int)((ns + nch0 - 1) / nch0);
-    const int nch = (ns + chunk2 - 1) / chunk2;
+    const int64_t nch0 = std::max<int64_t>(1, std::min<int64_t>(nsr, want / std::max<int64_t>(1, bx_ * ncomp)));
+    const int chunk2 = (int)((nsr + nch0 - 1) / nch0);
+    const int nch = (nsr + chunk2 - 1) / chunk2;
     const int64_t nvb = bx_ * ncomp * nch;
     const int64_t grid = nvb;
     // nontemporal plane loads / T1 stores: 8.15 vs 8.22 ms of main-stream generation at C3
@@ -1372,12 +1374,13 @@ static hipError_t launch_fx(const double* R, const double* bx, int ns, int64_t S
     }();
     if (nt)
       hipLaunchKernelGGL((k_filter_x2<NX, 8, true>), dim3((unsigned)grid), dim3(256), 0, st, R, bx, ns, Sl, chunk2,
-                         T1, (int)bx_, ncomp, nch);
+                         T1, (int)bx_, ncomp, nch, s0, s1);
     else
       hipLaunchKernelGGL((k_filter_x2<NX, 8>), dim3((unsigned)grid), dim3(256), 0, st, R, bx, ns, Sl, chunk2, T1,
-                         (int)bx_, ncomp, nch);
+                         (int)bx_, ncomp, nch, s0, s1);
     return hipGetLastError();
   }
+  if (s0 != 0 || s1 != ns) return hipErrorInvalidValue;  // step ranges: the point-pair kernel only
   const int nch = (ns + chunk - 1) / chunk;
   dim3 grid((unsigned)((Sl + 255) / 256), (unsigned)ncomp, (unsigned)nch);
   hipLaunchKernelGGL(k_filter_x<NX>, grid, dim3(256), 0, st, R, bx, ns, Sl, chunk, T1);
@@ -1385,11 +1388,12 @@ static hipError_t launch_fx(const double* R, const double* bx, int ns, int64_t S
 }
 
 hipError_t launch_filter_x(int NX, const double* R, const double* bx, int ns, int64_t Sl, int ncomp,
-                           int chunk, double* T1, hipStream_t st) {
+                           int chunk, double* T1, hipStream_t st, int s0, int s1) {
+  if (s1 < 0) s1 = ns;
   switch (NX) {
 #define PODS_FX(n) \
   case n:          \
-    return launch_fx<n>(R, bx, ns, Sl, ncomp, chunk, T1, st);
+    return launch_fx<n>(R, bx, ns, Sl, ncomp, chunk, T1, st, s0, s1);
     PODS_FX(1) PODS_FX(3) PODS_FX(5) PODS_FX(7) PODS_FX(9) PODS_FX(11) PODS_FX(13) PODS_FX(15)
     PODS_FX(17) PODS_FX(19) PODS_FX(21) PODS_FX(23) PODS_FX(25) PODS_FX(27) PODS_FX(29)
     PODS_FX(31) PODS_FX(33) PODS_FX(35) PODS_FX(37) PODS_FX(39) PODS_FX(41) PODS_FX(43)
@@ -1412,8 +1416,9 @@ template <int NY, int NZC>
 static hipError_t launch_fyz_t(const double* T1, const double* by, const double* bz, int NZ, int ns,
                                int jl, int K, int Kp, int64_t Sl, int ncomp, const double* lund,
                                int64_t lund_sj, int lund_mode, const double* rot, int rotate,
-                               double* AT, hipStream_t st) {
+                               double* AT, hipStream_t st, int s0, int s1) {
   constexpr int TJ = YZ_TJ, NT = YZ_NT;
+  const int nsr = s1 - s0;
   const int KB = std::min(K, YZ_KB);
   const int ldt = (KB + NZ - 1 + 16) + ((KB + NZ - 1 + 16) >> 4) + 1;
   const int ldl = KB + (KB >> 4) + 1;
@@ -1424,10 +1429,10 @@ static hipError_t launch_fyz_t(const double* T1, const double* by, const double*
   // enough blocks to fill the chip twice over, at most 16 steps each
   const int tiles = (jl + TJ - 1) / TJ;
   const int ktiles = (K + KB - 1) / KB;
-  const int nsb = (int)std::max<int64_t>(1, std::min<int64_t>(16, (int64_t)tiles * ktiles * ns / 512));
-  const dim3 grid((unsigned)tiles, (unsigned)((ns + nsb - 1) / nsb), (unsigned)ktiles);
+  const int nsb = (int)std::max<int64_t>(1, std::min<int64_t>(16, (int64_t)tiles * ktiles * nsr / 512));
+  const dim3 grid((unsigned)tiles, (unsigned)((nsr + nsb - 1) / nsb), (unsigned)ktiles);
   hipLaunchKernelGGL((k_filter_yz<TJ, NY, NZC, NT>), grid, dim3(NT), lds, st, T1, by, bz, NZ, ns, jl, K,
-                     Kp, Sl, ncomp, lund, lund_sj, lund_mode, rot, rotate, AT, nsb, KB);
+                     Kp, Sl, ncomp, lund, lund_sj, lund_mode, rot, rotate, AT, nsb, KB, s0, s1);
   return hipGetLastError();
 }
 
@@ -1435,23 +1440,25 @@ template <int NY>
 static hipError_t launch_fyz(const double* T1, const double* by, const double* bz, int NZ, int ns,
                              int jl, int K, int Kp, int64_t Sl, int ncomp, const double* lund,
                              int64_t lund_sj, int lund_mode, const double* rot, int rotate,
-                             double* AT, hipStream_t st) {
+                             double* AT, hipStream_t st, int s0, int s1) {
   if (NZ > 25) return hipErrorInvalidValue;
   if (NZ == NY)  // isotropic y/z widths: the z taps are compile-time too
     return launch_fyz_t<NY, NY>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj, lund_mode, rot,
-                                rotate, AT, st);
+                                rotate, AT, st, s0, s1);
   return launch_fyz_t<NY, 0>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj, lund_mode, rot, rotate,
-                             AT, st);
+                             AT, st, s0, s1);
 }
 
 hipError_t launch_filter_yz(int NY, const double* T1, const double* by, const double* bz, int NZ,
                             int ns, int jl, int K, int Kp, int64_t Sl, int ncomp,
                             const double* lund, int64_t lund_sj, int lund_mode, const double* rot,
-                            int rotate, double* AT, hipStream_t st) {
+                            int rotate, double* AT, hipStream_t st, int s0, int s1) {
+  if (s1 < 0) s1 = ns;
   switch (NY) {
 #define PODS_FYZ(n) \
   case n:           \
-    return launch_fyz<n>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj, lund_mode, rot, rotate, AT, st);
+    return launch_fyz<n>(T1, by, bz, NZ, ns, jl, K, Kp, Sl, ncomp, lund, lund_sj, lund_mode, rot, rotate, AT, st, \
+                         s0, s1);
     PODS_FYZ(1) PODS_FYZ(3) PODS_FYZ(5) PODS_FYZ(7) PODS_FYZ(9) PODS_FYZ(11) PODS_FYZ(13)
     PODS_FYZ(15) PODS_FYZ(17) PODS_FYZ(19) PODS_FYZ(21) PODS_FYZ(23) PODS_FYZ(25)
 #undef PODS_FYZ
