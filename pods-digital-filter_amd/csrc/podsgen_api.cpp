@@ -694,7 +694,8 @@ int pods_df_set_exchange(pods_ctx* c, int world, int rank, const int* j0s, const
   X.rank = rank;
   X.blocks = (ntot + 311) / 312;
   // the owners' substreams are 1/world of the one-GPU length, so a chain is as long as ... / world
-  X.Bs = std::max<int64_t>(64, (c->layout.Bs + world - 1) / world);
+  // (short streams: at least 8 substreams per rank)
+  X.Bs = std::max<int64_t>(1, std::min<int64_t>((c->layout.Bs + world - 1) / world, X.blocks / (8 * (int64_t)world)));
   X.G = (int)((X.blocks + X.Bs - 1) / X.Bs);
   if (X.G < world) return fail(PODS_ERR_UNSUPPORTED, "pods_df_set_exchange: stream too short for the ranks");
   std::vector<int> glo(world + 1);

@@ -17,11 +17,27 @@ J, K, NS = (int(a) for a in sys.argv[1:4]) if len(sys.argv) > 3 else (256, 256, 
 WORLDS = [int(w) for w in sys.argv[4].split(",")] if len(sys.argv) > 4 else [1, 2, 4, 8]
 s = podsgen.DFSetup(jma=J, kma=K, ns=NS, seed=12345)
 ctx = E.Context(0)
+MODES = [("plain", False, False), ("prefetched", True, False), ("exchange", True, True)]
 for world in WORLDS:
-    gen = E.Generator(s, rank=0, world=world, ctx=ctx)
+  for mode, ahead, xch in MODES:
+    if xch and world == 1:
+        continue
+    gen = E.Generator(s, rank=0, world=world, ctx=ctx, exchange=False)
+    a2a = ""
+    if xch:
+        # the MT19937 state exchange (pods_df_set_exchange): this rank's own substreams, then the
+        # all_to_all -- emulated on one GPU by a local copy of this rank's records (the twist is
+        # data-independent); its bytes are printed for the xGMI estimate
+        gen.enable_exchange()
+        n_s, n_r = sum(gen._xch[0]), sum(gen._xch[1])
+
+        def local_a2a(gen=gen, n=min(n_s, n_r)):
+            gen._recv[:n].copy_(gen._send[:n])
+        gen.exchange_states = local_a2a
+        a2a = "  all_to_all %.1f MB out / %.1f MB in per rank (not timed here)" % (n_s / 1e6, n_r / 1e6)
     C = torch.empty((NS, NS), dtype=torch.float64, device="cuda")
     mean = torch.empty(gen.rowlen, dtype=torch.float64, device="cuda")
-    for ahead in (False, True):
+    if True:
         reps, walls = 5, []
         for rep in range(reps):
             tm = E.StageTimer()
@@ -43,8 +59,8 @@ for world in WORLDS:
             walls.append((time.perf_counter() - t) * 1e3)
             if rep == reps - 2:
                 st = tm.summary()
-        print("world %d rows [%d,%d) %s: %s  step wall %.2f ms" % (
-            world, gen.j0, gen.j1, "prefetched" if ahead else "plain",
-            {k: round(v, 2) for k, v in st.items()}, sum(walls[1:-1]) / (reps - 2)), flush=True)
+        print("world %d rows [%d,%d) %s: %s  step wall %.2f ms%s" % (
+            world, gen.j0, gen.j1, mode,
+            {k: round(v, 2) for k, v in st.items()}, sum(walls[1:-1]) / (reps - 2), a2a), flush=True)
     del gen, C, mean
     torch.cuda.empty_cache()
