@@ -401,7 +401,9 @@ def main():
         kern_ms = k_ms.value / k_n.value
         ops = 2.0 * CORR_NMOD * 3 * P_local * ns * (ns + 1) / 2
         achieved = ops / (kern_ms * 1e-3) / 1e12
-        roofline = {"kernel": "k_syrk_i8 (pods_corr's %d residue SYRKs on int8 MFMA), rank 0" % CORR_NMOD,
+        paced = os.environ.get("PODS_SYRK_PACE", "") != "0"
+        roofline = {"kernel": "%s (pods_corr's %d residue SYRKs on int8 MFMA), rank 0"
+                              % ("k_syrk_i8_paced" if paced else "k_syrk_i8", CORR_NMOD),
                     "bound": "mfma", "dtype": "i8", "achieved": round(achieved, 1), "peak": round(I8_MFMA_PEAK_TOPS, 1),
                     "unit": "TOP/s", "frac": round(achieved / I8_MFMA_PEAK_TOPS, 4), "traffic": traffic,
                     "launch_ms": round(kern_ms, 3), "ops_per_launch": ops, "launches": k_n.value,
@@ -413,7 +415,8 @@ def main():
                     "bound_note": ("the int8 pipe is fed by LDS-DMA: 214 GB L2->LDS per launch at C3; measured "
                                    "(DESIGN.md s3): MFMAs alone 16.9 ms (the chip holds ~1.7-1.94 GHz under "
                                    "this load), the kernel with an L2-resident K window 19.3 ms; MFMA pipe "
-                                   "busy 66 % of the real kernel")}
+                                   "busy 66 % of the r4 kernel; r5: one persistent workgroup per CU, the 32 "
+                                   "of an XCD paced round by round over the same panels")}
     else:
         achieved = flops / (corr_ms * 1e-3) / 1e12
         roofline = {"kernel": "pods_corr (k_syrk_g128 + k_syrk_reduce), rank 0",

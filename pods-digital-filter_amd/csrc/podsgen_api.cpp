@@ -323,7 +323,8 @@ struct pods_ctx {
   int corr_mode = 1;
   DevBuf devmax;           // max |fl(a - mean)| (k_mean / k_absdev), the int8 path's scale
   bool dev_valid = false;  // devmax belongs to the current snapshots and mean
-  DevBuf i8_res, i8_part, i8_items;
+  DevBuf i8_res, i8_part, i8_items, i8_xitems, i8_pace;  // + the persistent SYRK's table, counters
+  int i8_per_xcd = 0;
   // the int8 plan's inputs, compared field by field (every one of them changes the plan)
   struct I8Key {
     int ns = -1;
@@ -519,7 +520,7 @@ int pods_destroy(pods_ctx* c) {
   for (EigvalSlot& sl : c->eslots)
     for (DevBuf* b : {&sl.wm, &sl.x, &sl.flags, &sl.det, &sl.v, &sl.cnt, &sl.lam, &sl.ws2}) release(*b);
   release(c->inv_lam);
-  for (DevBuf* b : {&c->devmax, &c->i8_res, &c->i8_part, &c->i8_items}) release(*b);
+  for (DevBuf* b : {&c->devmax, &c->i8_res, &c->i8_part, &c->i8_items, &c->i8_xitems, &c->i8_pace}) release(*b);
   for (auto& ev : c->corr_ev) {
     (void)hipEventDestroy(ev.first);
     (void)hipEventDestroy(ev.second);
@@ -1072,6 +1073,10 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
       c->i8_plan.nitems = (int)(items.size() / 4);  // the order decides the (padded) item count
       PODS_HIP(ensure(c->i8_items, items.size() * sizeof(int)));
       PODS_HIP(hipMemcpy(c->i8_items.p, items.data(), items.size() * sizeof(int), hipMemcpyHostToDevice));
+      const std::vector<int> xit = pods::corr_i8_xcd_items(items, c->i8_plan.nitems, &c->i8_per_xcd);
+      PODS_HIP(ensure(c->i8_xitems, xit.size() * sizeof(int)));
+      PODS_HIP(hipMemcpy(c->i8_xitems.p, xit.data(), xit.size() * sizeof(int), hipMemcpyHostToDevice));
+      PODS_HIP(ensure(c->i8_pace, 8 * 32 * sizeof(unsigned)));
       c->i8_key = key;
     }
     PODS_HIP(ensure(c->i8_res, (size_t)c->i8_plan.r_bytes));
@@ -1094,9 +1099,15 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
       e1 = c->corr_ev[c->corr_ev_used].second;
       ++c->corr_ev_used;
     }
+    // the persistent XCD-paced SYRK unless PODS_SYRK_PACE=0 ("p<N>": also every N K steps in a tile)
+    const char* pv = std::getenv("PODS_SYRK_PACE");
+    const bool paced = !(pv && pv[0] == '0');
+    const int every = pv && pv[0] == 'p' && pv[1] ? std::atoi(pv + 1) : 0;
     PODS_HIP(pods::launch_corr_i8(c->A.as<double>(), ns, c->rowlen, c->rowpad, mean, c->devmax.as<double>(),
                                   c->i8_plan, c->i8_items.as<int>(), c->i8_res.as<int8_t>(),
-                                  c->i8_part.as<uint8_t>(), C_dev, ns, divide, c->stream, e0, e1));
+                                  c->i8_part.as<uint8_t>(), C_dev, ns, divide, c->stream, e0, e1,
+                                  paced ? c->i8_xitems.as<int>() : nullptr, c->i8_per_xcd,
+                                  paced ? c->i8_pace.as<unsigned>() : nullptr, every));
     return PODS_OK;
   }
   int64_t ksplit = 0;

@@ -914,10 +914,28 @@ hipError_t launch_absdev(const double* AT, int ns, int64_t rowlen, int64_t rowpa
   return hipGetLastError();
 }
 
+// The persistent kernel's table: XCD x's items of every modulus in grid order (item 8k + x of the
+// grid table), empty slots dropped, as {bi, bj, split, modulus}; per_xcd items per XCD (padded
+// with empty items to the longest list)
+std::vector<int> corr_i8_xcd_items(const std::vector<int>& items, int nitems, int* per_xcd) {
+  std::vector<std::vector<int>> per(8);
+  for (int l = 0; l < i8::NMOD; ++l)
+    for (int k = 0; k < nitems; ++k) {
+      if (items[4 * k] < 0) continue;
+      per[k & 7].insert(per[k & 7].end(), {items[4 * k], items[4 * k + 1], items[4 * k + 2], l});
+    }
+  int px = 0;
+  for (int x = 0; x < 8; ++x) px = std::max(px, (int)per[x].size() / 4);
+  std::vector<int> out((size_t)8 * px * 4, -1);
+  for (int x = 0; x < 8; ++x) std::copy(per[x].begin(), per[x].end(), out.begin() + (size_t)x * px * 4);
+  *per_xcd = px;
+  return out;
+}
+
 hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowpad, const double* mean,
                           const double* devmax, const CorrI8Plan& p, const int* items, int8_t* R, uint8_t* P,
                           double* C, int64_t ldc, int divide, hipStream_t st, hipEvent_t syrk_begin,
-                          hipEvent_t syrk_end) {
+                          hipEvent_t syrk_end, const int* xitems, int per_xcd, unsigned* pace_ctr, int pace_every) {
   using namespace i8;
   // default: 5 ring stages, each wave's DMA pieces one after each of its first MFMA rows (ILV 1;
   // 22.0-22.8 ms at C3 against 24.0 for the pieces back to back after the barrier,
@@ -958,55 +976,18 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
   const int64_t cs = ilv ? (int64_t)NMOD * ns * KC : (int64_t)ns * KC;
   const int ldp = (ns + 63) / 64 * 64;
   const int64_t pslab = (int64_t)ns * ldp;
-  // PODS_SYRK_PACE (A/B): "p" = the persistent XCD-paced kernel (k_syrk_i8_paced) with a pacing
-  // point after every round of items; "p<N>" = also every N K steps inside a tile
-  int paced = 0, pace_every = 0;
-  if (const char* v = std::getenv("PODS_SYRK_PACE")) {
-    if (v[0] == 'p') {
-      paced = 1;
-      pace_every = v[1] ? std::atoi(v + 1) : 0;
-    }
-  }
-  std::vector<int> xit;
-  int per_xcd = 0, nslot = 0;
-  struct Buf {
-    void* p = nullptr;
-    size_t bytes = 0;
-  };
-  static thread_local Buf xbuf, pbuf;  // the paced kernel's item table and pacing counters
+  // default (r5): the persistent XCD-paced kernel (k_syrk_i8_paced: 22.34 vs 22.89 ms at C3 for
+  // the launch-per-item grid, profiles/r5/pace_ab.log) when the caller passes the per-XCD item
+  // table; pace_every > 0 adds pacing points inside a tile (measured no better: 22.54 at 256 K
+  // steps, 22.59 at 96).  PODS_SYRK_PACE=0 (A/B) or no table: the grid form below
+  const bool paced = xitems != nullptr && pace_ctr != nullptr;
+  int nslot = 0;
   if (paced) {
     int dev = 0, cus = 0;
     e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return e;
     nslot = std::max(1, cus / 8);
-    // XCD x's items in grid order (item 8k + x of every modulus), empty slots dropped
-    std::vector<std::vector<int>> per(8);
-    std::vector<int> h((size_t)p.nitems * 4);
-    e = hipMemcpy(h.data(), items, h.size() * sizeof(int), hipMemcpyDeviceToHost);
-    if (e != hipSuccess) return e;
-    for (int l = 0; l < NMOD; ++l)
-      for (int k = 0; k < p.nitems; ++k) {
-        const int x = k & 7;
-        if (h[4 * k] < 0) continue;
-        per[x].insert(per[x].end(), {h[4 * k], h[4 * k + 1], h[4 * k + 2], l});
-      }
-    for (int x = 0; x < 8; ++x) per_xcd = std::max(per_xcd, (int)per[x].size() / 4);
-    xit.assign((size_t)8 * per_xcd * 4, -1);
-    for (int x = 0; x < 8; ++x) std::copy(per[x].begin(), per[x].end(), xit.begin() + (size_t)x * per_xcd * 4);
-    auto ens = [](Buf& b, size_t bytes) -> hipError_t {
-      if (b.bytes >= bytes) return hipSuccess;
-      if (b.p) (void)hipFree(b.p);
-      b.p = nullptr;
-      b.bytes = 0;
-      hipError_t r = hipMalloc(&b.p, bytes);
-      if (r == hipSuccess) b.bytes = bytes;
-      return r;
-    };
-    e = ens(xbuf, xit.size() * sizeof(int));
-    if (e == hipSuccess) e = ens(pbuf, 8 * 32 * sizeof(unsigned));
-    if (e == hipSuccess) e = hipMemcpyAsync(xbuf.p, xit.data(), xit.size() * sizeof(int), hipMemcpyHostToDevice, st);
-    if (e != hipSuccess) return e;
     for (const void* f : {reinterpret_cast<const void*>(&k_syrk_i8_paced<5, 1, false>),
                           reinterpret_cast<const void*>(&k_syrk_i8_paced<5, 1, true>)}) {
       e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(5 * 2 * PANEL));
@@ -1043,16 +1024,16 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
     if (syrk_begin && p.nlaunch == 1) e = hipEventRecord(syrk_begin, st);
     if (e != hipSuccess) return e;
     if (paced) {
-      e = hipMemsetAsync(pbuf.p, 0, 8 * 32 * sizeof(unsigned), st);
+      e = hipMemsetAsync(pace_ctr, 0, 8 * 32 * sizeof(unsigned), st);
       if (e != hipSuccess) return e;
       if (pace_every > 0)
         hipLaunchKernelGGL((k_syrk_i8_paced<5, 1, true>), dim3(8 * nslot), dim3(512), 5 * 2 * PANEL, st,
-                           (const int8_t*)R, ns, ms, cs, p.kcs, reinterpret_cast<const int4*>(xbuf.p), per_xcd,
-                           p.nsplit, P, pslab, ldp, li > 0 ? 1 : 0, static_cast<unsigned*>(pbuf.p), pace_every);
+                           (const int8_t*)R, ns, ms, cs, p.kcs, reinterpret_cast<const int4*>(xitems), per_xcd,
+                           p.nsplit, P, pslab, ldp, li > 0 ? 1 : 0, pace_ctr, pace_every);
       else
         hipLaunchKernelGGL((k_syrk_i8_paced<5, 1, false>), dim3(8 * nslot), dim3(512), 5 * 2 * PANEL, st,
-                           (const int8_t*)R, ns, ms, cs, p.kcs, reinterpret_cast<const int4*>(xbuf.p), per_xcd,
-                           p.nsplit, P, pslab, ldp, li > 0 ? 1 : 0, static_cast<unsigned*>(pbuf.p), 0);
+                           (const int8_t*)R, ns, ms, cs, p.kcs, reinterpret_cast<const int4*>(xitems), per_xcd,
+                           p.nsplit, P, pslab, ldp, li > 0 ? 1 : 0, pace_ctr, 0);
     } else {
       const int ldp_ = ldp;
       const int acc_ = li > 0 ? 1 : 0;

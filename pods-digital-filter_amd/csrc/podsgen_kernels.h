@@ -66,7 +66,10 @@ hipError_t launch_absdev(const double* AT, int ns, int64_t rowlen, int64_t rowpa
 hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowpad, const double* mean,
                           const double* devmax, const CorrI8Plan& p, const int* items, int8_t* R, uint8_t* P,
                           double* C, int64_t ldc, int divide, hipStream_t st, hipEvent_t syrk_begin = nullptr,
-                          hipEvent_t syrk_end = nullptr);
+                          hipEvent_t syrk_end = nullptr, const int* xitems = nullptr, int per_xcd = 0,
+                          unsigned* pace_ctr = nullptr, int pace_every = 0);
+// the persistent SYRK's per-XCD item table from the grid-order one (per_xcd: items per XCD)
+std::vector<int> corr_i8_xcd_items(const std::vector<int>& items, int nitems, int* per_xcd);
 // Split-K SYRK (k_syrk_g128 + k_syrk_reduce).  Plan: returns the number of K splits (work
 // slabs of ns*ns doubles).
 int syrk_plan(int ns, int64_t Kdim, int64_t* ksplit);
