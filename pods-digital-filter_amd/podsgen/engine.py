@@ -227,20 +227,25 @@ class Generator:
         check(lib.pods_df_exchange_bind(h, ptr(self._send), ptr(self._recv)), "pods_df_exchange_bind")
         self._xch = ([int(x) for x in sb], [int(x) for x in rb])
 
-    def exchange_states(self):
+    _a2a = None   # finisher of an all_to_all issued ahead (prefetch_jump)
+
+    def exchange_states(self, async_op=False):
         """The all_to_all of the segment-start states (2.5 KB per rank and plane; every rank calls
-        generate() together).  RCCL moves device buffers; gloo (CPU transport, e.g. several ranks on
-        one GPU) goes through host copies."""
+        generate() / prefetch_jump() together).  RCCL moves device buffers, ordered after the
+        current stream; with async_op the call returns a finisher that makes the current stream
+        wait for it.  gloo (CPU transport, e.g. several ranks on one GPU) goes through host copies."""
         sb, rb = self._xch
         d = self.dist
         n_s, n_r = sum(sb), sum(rb)
         if d.get_backend() == "nccl":
-            d.all_to_all_single(self._recv[:n_r], self._send[:n_s], output_split_sizes=rb, input_split_sizes=sb)
-        else:
-            send = self._send[:n_s].cpu()
-            recv = torch.empty(n_r, dtype=torch.uint8)
-            d.all_to_all_single(recv, send, output_split_sizes=rb, input_split_sizes=sb)
-            self._recv[:n_r].copy_(recv)
+            work = d.all_to_all_single(self._recv[:n_r], self._send[:n_s], output_split_sizes=rb,
+                                       input_split_sizes=sb, async_op=async_op)
+            return (lambda: work.wait()) if async_op else None
+        send = self._send[:n_s].cpu()
+        recv = torch.empty(n_r, dtype=torch.uint8)
+        d.all_to_all_single(recv, send, output_split_sizes=rb, input_split_sizes=sb)
+        self._recv[:n_r].copy_(recv, non_blocking=False)
+        return (lambda: None) if async_op else None
 
     _ahead = None      # event behind the next run's prefetched parts (prefetch_*)
     _ahead_parts = 0   # which parts: PODS_GEN_JUMP, + PODS_GEN_PLANES
@@ -258,7 +263,11 @@ class Generator:
             pre = (_lib.PODS_GEN_JUMP | _lib.PODS_GEN_RECORD) & ~done
             if pre:
                 check(self.ctx.lib.pods_df_generate_parts(self.ctx.h, pre), "pods_df_generate_parts")
-            self.exchange_states()
+            if self._a2a is not None:   # issued ahead, beside the previous step's work
+                self._a2a()
+                self._a2a = None
+            else:
+                self.exchange_states()
             rest = _lib.PODS_GEN_PLANES | _lib.PODS_GEN_XPASS | _lib.PODS_GEN_YZPASS
             check(self.ctx.lib.pods_df_generate_parts(self.ctx.h, rest), "pods_df_generate_parts")
         elif self._ahead is not None:
@@ -293,9 +302,13 @@ class Generator:
         its time -- both stream 7-13 GB through HBM -- and beside the SYRK they took 10.9 ms
         instead of 2.4 and cost the SYRK 2.7 ms, no net gain; spread over 64-256 workgroups they
         took 46-77 ms, each substream being a latency-bound twist chain.)"""
-        # with the state exchange the owned substreams' records too (they need only the seed)
+        # with the state exchange the owned substreams' records too (they need only the seed), and
+        # the all_to_all of the records, ordered behind them on the gen stream
         parts = _lib.PODS_GEN_JUMP | (_lib.PODS_GEN_RECORD if self._xch is not None else 0)
         self._on_gen_stream(parts, timer, "gen_jump_ahead")
+        if self._xch is not None and self.dist is not None:
+            with torch.cuda.stream(self.ctx.gen_stream()):
+                self._a2a = self.exchange_states(async_op=True)
 
     def prefetch_planes_beside_solver(self, timer=None):
         """Enqueue the NEXT run's random planes on the gen stream behind the marker the current
@@ -1221,7 +1234,8 @@ class ShardedSteps:
     leading pairs on its own stream behind the event of step k-1's all-reduce, so the device runs
     that latency-bound solve beside step k's HBM / MFMA-bound kernels; the other ranks run their
     spectrum units; broadcasts of lambda and T; every rank's spatial modes of step k-1 from bank
-    (k-1) % 2; the Fourier stage on rank 0), and only then step k's all-reduce.  Every result is
+    (k-1) % 2; the Fourier stage on rank 0), and then issues step k's all-reduce asynchronously
+    (the next step's generation runs beside it; the tail waits for it and unpacks C).  Every result is
     that of the unpipelined order bit for bit (same kernels on the same inputs); pipelined=False
     (PODS_PIPELINE=0) runs each step's tail right after its own all-reduce.  results[k] is step
     k's PODResult once its tail has run; flush() runs the last tail."""
@@ -1260,21 +1274,32 @@ class ShardedSteps:
         if self.pending is not None:
             self._tail(timer)
         check(ctx.lib.pods_select_snapshots(ctx.h, bank), "pods_select_snapshots")
+        finish = None
         if self.world > 1:
             ctx.detect_sharing(self.dist)
+            # the packed partial C goes out now; with the pipeline the main stream does not wait for
+            # it (the next step's generation runs beside the all-reduce) -- its tail unpacks it
+            pack, unpack = device_triangle_ops(ctx)
             with tm("allreduce"):
-                allreduce_correlation(self.dist, C, snap.ns, *device_triangle_ops(ctx))
-        ready = torch.cuda.Event()
-        ready.record()
-        self.pending = (bank, snap, C, mean, ready)
+                packed = pack(C)
+                work = self.dist.all_reduce(packed, async_op=True)
+
+            def finish(packed=packed, work=work, unpack=unpack, C=C):
+                work.wait()
+                unpack(packed, C)
+        self.pending = [bank, snap, C, mean, finish]
         self.k += 1
         if not self.pipelined:
             self._tail(timer)
 
     def _tail(self, timer):
-        bank, snap, C, mean, ready = self.pending
+        bank, snap, C, mean, finish = self.pending
         self.pending = None
         ctx = self.gen.ctx
+        if finish is not None:
+            finish()   # the main stream waits for this step's all-reduce, then unpacks C
+        ready = torch.cuda.Event()
+        ready.record()
         s = self.setup
         self.gen.join_ahead()   # the persistent spectrum kernels must not find generator workgroups
         check(ctx.lib.pods_select_snapshots(ctx.h, bank), "pods_select_snapshots")
