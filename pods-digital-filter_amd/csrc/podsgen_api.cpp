@@ -270,10 +270,6 @@ struct pods_ctx {
     bool have_snapshots = false, mean_valid = false, centered = false, dev_valid = false;
   } alt;
   int bank = 0;
-  // the x pass's own stream when the generation runs its x / y-z passes in step chunks
-  // (PODS_GEN_CHUNKS): chunk k's y/z pass on the context's stream beside chunk k+1's x pass
-  hipStream_t xstream = nullptr;
-  std::vector<hipEvent_t> xev;
   DevBuf R, T1, A, mean, lund, taps, rot, prog_mean, prog_dft, mag, lam, cwork, items, spwork, prog_rank;
   DevBuf e_wm, e_x, e_flags, e_det, e_v, e_t, e_part, e_w2, e_inv, e_cnt;  // pods_syev workspace
   int e_G = 0;
@@ -511,8 +507,6 @@ int pods_destroy(pods_ctx* c) {
   c->rng.free_all();
   c->xch.free_all();
   for (DevBuf* b : {&c->alt.A, &c->alt.mean, &c->alt.devmax}) release(*b);
-  for (hipEvent_t ev : c->xev) (void)hipEventDestroy(ev);
-  if (c->xstream) (void)hipStreamDestroy(c->xstream);
   release(c->sub_part);
   release(c->sub_R);
   release(c->sub_cheb);
@@ -864,39 +858,6 @@ int pods_df_generate_parts(pods_ctx* c, int parts) {
                                       c->stream, (parts & PODS_GEN_BESIDE_SOLVER) ? 2 : 0));
   }
   const double* taps = c->taps.as<double>();
-  // x and y/z passes in step chunks on two streams: chunk k's y/z pass (latency / VALU bound)
-  // beside chunk k+1's x pass (HBM bound).  PODS_GEN_CHUNKS = chunks (1: one launch each)
-  int nchunk = 1;
-  if (const char* gc = std::getenv("PODS_GEN_CHUNKS")) nchunk = std::max(1, std::atoi(gc));
-  if ((parts & PODS_GEN_XPASS) && (parts & PODS_GEN_YZPASS) && nchunk > 1 && p.ns >= 16 * nchunk) {
-    if (!c->xstream) PODS_HIP(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
-    while ((int)c->xev.size() < nchunk + 1) {
-      hipEvent_t ev = nullptr;
-      PODS_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-      c->xev.push_back(ev);
-    }
-    PODS_HIP(hipEventRecord(c->xev[nchunk], c->stream));  // the planes are on the context's stream
-    PODS_HIP(hipStreamWaitEvent(c->xstream, c->xev[nchunk], 0));
-    const int64_t pts = 3 * c->Sl;
-    for (int k = 0; k < nchunk; ++k) {
-      const int s0 = (int)((int64_t)p.ns * k / nchunk), s1 = (int)((int64_t)p.ns * (k + 1) / nchunk);
-      PODS_HIP(pods::launch_filter_x(c->NX, c->R.as<double>(), taps, p.ns, c->Sl, 3, (int)std::max<int64_t>(1, pts),
-                                     c->T1.as<double>(), c->xstream, s0, s1));
-      PODS_HIP(hipEventRecord(c->xev[k], c->xstream));
-    }
-    for (int k = 0; k < nchunk; ++k) {
-      const int s0 = (int)((int64_t)p.ns * k / nchunk), s1 = (int)((int64_t)p.ns * (k + 1) / nchunk);
-      PODS_HIP(hipStreamWaitEvent(c->stream, c->xev[k], 0));
-      PODS_HIP(pods::launch_filter_yz(c->NY, c->T1.as<double>(), taps + c->NX, taps + c->NX + c->NY, c->NZ, p.ns,
-                                      c->jl, p.kma, c->Kp, c->Sl, 3, c->lund.as<double>(), c->lund_sj, p.lund_mode,
-                                      c->rot.as<double>(), p.rotate, c->A.as<double>(), c->stream, s0, s1));
-    }
-    c->have_snapshots = true;
-    c->mean_valid = false;
-    c->dev_valid = false;
-    c->centered = false;
-    return PODS_OK;
-  }
   if (parts & PODS_GEN_XPASS) {
     // x pass: enough (component, point, step-chunk) threads to fill the chip
     const int64_t pts = 3 * c->Sl;

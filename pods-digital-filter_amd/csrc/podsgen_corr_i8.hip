@@ -289,85 +289,6 @@ __device__ __forceinline__ void residues_body(const double* __restrict__ AT, int
   });
 }
 
-// Half-width variant (A/B, PODS_RES_I8=2): thread (chunk kc, snapshot i, eighth h) converts the
-// 8 rows r = 64 kc + 8 h + e (half of one 16-row run) and stores 8 bytes per modulus -- half the
-// registers (a[8], 4 limb pairs), so twice the waves per SIMD to keep the HBM writes in flight.
-__device__ __forceinline__ void residues_half(const double* __restrict__ AT, int ns, int64_t rowlen,
-                                              int64_t rowpad, const double* __restrict__ mean,
-                                              const double* __restrict__ devmax, int bbits, int64_t kc0,
-                                              int64_t nkc, int8_t* __restrict__ R, int64_t ms, int64_t cs) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int h = (int)(t & 7);
-  const int64_t rest = t >> 3;
-  if (rest >= nkc * ns) return;
-  const int i = (int)(rest % ns);
-  const int64_t kcl = rest / ns;
-  const int64_t r0 = (kc0 + kcl) * 64 + h * 8;
-  double a[8];
-  if (r0 < rowpad) {
-    const double2* src = reinterpret_cast<const double2*>(AT + ((((r0 >> 4) * ns) + i) << 4) + (r0 & 15));
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const double2 v = src[e];
-      a[2 * e] = v.x;
-      a[2 * e + 1] = v.y;
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) a[e] = r0 + e < rowlen ? a[e] - mean[r0 + e] : 0.0;  // main() :1494
-  } else {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) a[e] = 0.0;
-  }
-  const int sg = scale_exp(*devmax, bbits);
-  int8_t* const rb = R + kcl * cs;
-  const uint32_t doff = (uint32_t)(i * 64 + h * 8);
-  constexpr float MAG = 12582912.0f;
-  float Fs[5][8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const double z = rint(ldexp(a[e], sg)) + 0x1p52;
-    const double hh = floor(z * 0x1p-32);
-    const uint32_t lo = (uint32_t)__builtin_fma(-hh, 0x1p32, z), hi = (uint32_t)hh;
-    Fs[0][e] = (float)(lo & 0x7FFu);
-    Fs[1][e] = (float)((lo >> 11) & 0x7FFu);
-    Fs[2][e] = (float)(((lo >> 22) | (hi << 10)) & 0x7FFu);
-    Fs[3][e] = (float)((hi >> 1) & 0x7FFu);
-    Fs[4][e] = (float)(hi >> 12);
-  }
-  f32x2 F[5][4];
-#pragma unroll
-  for (int k = 0; k < 5; ++k)
-#pragma unroll
-    for (int pr = 0; pr < 4; ++pr) F[k][pr] = (f32x2){Fs[k][2 * pr], Fs[k][2 * pr + 1]};
-  sfor<0, NMOD>([&](auto L) {
-    constexpr int l = decltype(L)::value;
-    constexpr float m = (float)kT.m[l], inv = 1.0f / (float)kT.m[l], o = (float)kT.off[l];
-    constexpr float c1 = (float)kT.p11[l][1], c2 = (float)kT.p11[l][2], c3 = (float)kT.p11[l][3],
-                    c4 = (float)kT.p11[l][4];
-    f32x2 sv[4];
-#pragma unroll
-    for (int pr = 0; pr < 4; ++pr) {
-      f32x2 v = __builtin_elementwise_fma(F[1][pr], (f32x2){c1, c1}, F[0][pr]);
-      v = __builtin_elementwise_fma(F[2][pr], (f32x2){c2, c2}, v);
-      v = __builtin_elementwise_fma(F[3][pr], (f32x2){c3, c3}, v);
-      v = __builtin_elementwise_fma(F[4][pr], (f32x2){c4, c4}, v);
-      v = v + (f32x2){o, o};
-      f32x2 qv = __builtin_elementwise_fma(v, (f32x2){inv, inv}, (f32x2){MAG, MAG}) - (f32x2){MAG, MAG};
-      v = __builtin_elementwise_fma(-qv, (f32x2){m, m}, v);
-      sv[pr] = v + (f32x2){MAG, MAG};
-    }
-    uint32_t w[2];
-#pragma unroll
-    for (int pq = 0; pq < 2; ++pq) {
-      const f32x2 u = sv[2 * pq], v = sv[2 * pq + 1];
-      const uint32_t h0 = __builtin_amdgcn_perm(__float_as_uint(u.y), __float_as_uint(u.x), 0x0C0C0400u);
-      const uint32_t h1 = __builtin_amdgcn_perm(__float_as_uint(v.y), __float_as_uint(v.x), 0x0C0C0400u);
-      w[pq] = h0 | (h1 << 16);
-    }
-    *reinterpret_cast<uint2*>(rb + (int64_t)l * ms + doff) = make_uint2(w[0], w[1]);
-  });
-}
-
 #define PODS_RES_ARGS const double* __restrict__ AT, int ns, int64_t rowlen, int64_t rowpad, \
     const double* __restrict__ mean, const double* __restrict__ devmax, int bbits, int64_t kc0, int64_t nkc, \
     int8_t* __restrict__ R, int64_t ms, int64_t cs
@@ -376,7 +297,6 @@ template <int V>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) void k_residues(PODS_RES_ARGS) {
   residues_body<V>(PODS_RES_PASS);
 }
-__global__ __launch_bounds__(256) void k_residues_half(PODS_RES_ARGS) { residues_half(PODS_RES_PASS); }
 #undef PODS_RES_ARGS
 #undef PODS_RES_PASS
 
@@ -966,14 +886,11 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
   const size_t lds = (size_t)(variant == 5 || (variant >= 45 && variant <= 47) ? 5 : 4) * 2 * PANEL;
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  // residue layout: modulus l's K chunk kc at R + l * ms + kc * cs.  Default: one matrix per
-  // modulus ([NMOD][chunks][ns][64]).  PODS_RES_LAYOUT=1 (A/B): the moduli interleaved per K
-  // chunk ([chunks][NMOD][ns][64]), so a residue wave's 16 stores land in one 16 * ns * 64-byte
-  // window instead of 16 matrices apart
-  const char* lay = std::getenv("PODS_RES_LAYOUT");
-  const bool ilv = lay && lay[0] == '1';
-  const int64_t ms = ilv ? (int64_t)ns * KC : p.chunks * ns * KC;
-  const int64_t cs = ilv ? (int64_t)NMOD * ns * KC : (int64_t)ns * KC;
+  // residue layout: modulus l's K chunk kc at R + l * ms + kc * cs, one matrix per modulus
+  // ([NMOD][chunks][ns][64]); the moduli interleaved per chunk ([chunks][NMOD][ns][64], a residue
+  // wave's 16 stores in one window) measured no faster (r5, profiles/r5/residue_layout_ab.log)
+  const int64_t ms = p.chunks * ns * KC;
+  const int64_t cs = (int64_t)ns * KC;
   const int ldp = (ns + 63) / 64 * 64;
   const int64_t pslab = (int64_t)ns * ldp;
   // default (r5): the persistent XCD-paced kernel (k_syrk_i8_paced: 22.34 vs 22.89 ms at C3 for
@@ -998,13 +915,11 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
   if (e != hipSuccess) return e;
   for (int li = 0; li < p.nlaunch; ++li) {
     const int64_t kc0 = (int64_t)li * p.chunks;
-    // PODS_RES_I8=1 (A/B runs): the signed 14-bit-limb residues (measured the same); =2 the
-    // half-width threads (8 rows each)
+    // PODS_RES_I8=1 (A/B runs): the signed 14-bit-limb residues (measured the same; so were 8-row
+    // threads at 60 VGPRs / 8 waves per SIMD, r5, profiles/r5/pace_ab.log)
     const char* rv = std::getenv("PODS_RES_I8");
-    const bool half = rv && rv[0] == '2';
-    const int64_t thr = p.chunks * ns * (half ? 8 : 4);
-    const void* rk = half ? reinterpret_cast<const void*>(&k_residues_half)
-                   : rv && rv[0] == '1' ? reinterpret_cast<const void*>(&k_residues<1>)
+    const int64_t thr = p.chunks * ns * 4;
+    const void* rk = rv && rv[0] == '1' ? reinterpret_cast<const void*>(&k_residues<1>)
                                         : reinterpret_cast<const void*>(&k_residues<0>);
     {
       const double* AT_ = AT;

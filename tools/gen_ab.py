@@ -15,12 +15,12 @@ import podsgen  # noqa: E402
 from podsgen import _lib  # noqa: E402
 from podsgen import engine as E  # noqa: E402
 
-KEYS = ("PODS_MT_GEN", "PODS_MT_SUBSTREAMS", "PODS_GEN_CHUNKS")
+KEYS = ("PODS_MT_GEN", "PODS_MT_SUBSTREAMS")
 rounds = int(sys.argv[1])
 J, K, NS = (int(a) for a in sys.argv[2:5])
 worlds = [int(w) for w in sys.argv[5].split(",")]
 configs = sys.argv[6:]
-# the x and y/z passes in one call (PODS_GEN_CHUNKS runs them as step chunks on two streams)
+# the x and y/z passes in one call
 PARTS = [("jump", _lib.PODS_GEN_JUMP), ("planes", _lib.PODS_GEN_PLANES),
          ("xyz", _lib.PODS_GEN_XPASS | _lib.PODS_GEN_YZPASS)]
 s = podsgen.DFSetup(jma=J, kma=K, ns=NS, seed=4242)
