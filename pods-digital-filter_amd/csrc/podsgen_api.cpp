@@ -327,9 +327,10 @@ struct pods_ctx {
     int64_t rowlen = -1, rowpad = -1, budget = -1;
     int force = -1;
     char order = 0;
+    int wide = 0;
     bool operator==(const I8Key& o) const {
       return ns == o.ns && rowlen == o.rowlen && rowpad == o.rowpad && budget == o.budget && force == o.force &&
-             order == o.order;
+             order == o.order && wide == o.wide;
     }
   } i8_key;
   pods::CorrI8Plan i8_plan{};
@@ -1027,6 +1028,10 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
     key.budget = budget;
     key.force = force;
     key.order = ord ? ord[0] : 0;
+    // PODS_SYRK_WIDE=1: the persistent SYRK with 256 x 384 tiles (corr_i8_xcd_items_wide)
+    const char* wv = std::getenv("PODS_SYRK_WIDE");
+    const int wide = wv && wv[0] == '1' ? 1 : 0;
+    key.wide = wide;
     if (!(c->i8_key == key)) {
       if (pods::corr_i8_plan(ns, c->rowlen, c->rowpad, budget, &c->i8_plan, force) != 0)
         return fail(PODS_ERR_UNSUPPORTED, "pods_corr: K too large for the int8 correlation (PODS_CORR=f64)");
@@ -1034,13 +1039,14 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
       c->i8_plan.nitems = (int)(items.size() / 4);  // the order decides the (padded) item count
       PODS_HIP(ensure(c->i8_items, items.size() * sizeof(int)));
       PODS_HIP(hipMemcpy(c->i8_items.p, items.data(), items.size() * sizeof(int), hipMemcpyHostToDevice));
-      const std::vector<int> xit = pods::corr_i8_xcd_items(items, c->i8_plan.nitems, &c->i8_per_xcd);
+      const std::vector<int> xit = wide ? pods::corr_i8_xcd_items_wide(ns, c->i8_plan, &c->i8_per_xcd)
+                                        : pods::corr_i8_xcd_items(items, c->i8_plan.nitems, &c->i8_per_xcd);
       PODS_HIP(ensure(c->i8_xitems, xit.size() * sizeof(int)));
       PODS_HIP(hipMemcpy(c->i8_xitems.p, xit.data(), xit.size() * sizeof(int), hipMemcpyHostToDevice));
       PODS_HIP(ensure(c->i8_pace, 8 * 32 * sizeof(unsigned)));
       c->i8_key = key;
     }
-    PODS_HIP(ensure(c->i8_res, (size_t)c->i8_plan.r_bytes));
+    PODS_HIP(ensure(c->i8_res, (size_t)(c->i8_plan.r_bytes + pods::CORR_I8_RPAD)));
     PODS_HIP(ensure(c->i8_part, (size_t)c->i8_plan.p_bytes));
     PODS_HIP(ensure(c->devmax, sizeof(double)));
     if (!c->dev_valid) {
@@ -1068,7 +1074,7 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
                                   c->i8_plan, c->i8_items.as<int>(), c->i8_res.as<int8_t>(),
                                   c->i8_part.as<uint8_t>(), C_dev, ns, divide, c->stream, e0, e1,
                                   paced ? c->i8_xitems.as<int>() : nullptr, c->i8_per_xcd,
-                                  paced ? c->i8_pace.as<unsigned>() : nullptr, every));
+                                  paced ? c->i8_pace.as<unsigned>() : nullptr, every, paced ? wide : 0));
     return PODS_OK;
   }
   int64_t ksplit = 0;

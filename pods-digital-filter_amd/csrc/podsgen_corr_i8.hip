@@ -346,14 +346,17 @@ __device__ __forceinline__ void pace_xcd(unsigned* ctr, unsigned& epoch, unsigne
 }
 
 
-template <int NST, int DIAG, bool SAME, int ILV>
+template <int NST, int DIAG, bool SAME, int ILV, int LD = 0>
 __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int64_t cstride, int ns, int nt, int i0,
                                           int j0, int m, char* smem, uint8_t* __restrict__ dst, int ldp,
                                           int accumulate, unsigned* pctr = nullptr, unsigned pslot = 0,
                                           int pevery = 0, unsigned* pepoch = nullptr) {
   constexpr int STG = 2 * PANEL;
   constexpr int Q = SAME ? 2 : 4;  // DMA instructions per wave per stage
-  constexpr int D = NST - 2;       // DMA lead in K steps beyond the one being read
+  // DMA lead in K steps beyond the one being read: NST - 2, or with LD = 1 NST - 1 (the slot of
+  // step t itself is refilled during step t: its fragments were read during step t - 1 and are
+  // waited for before step t's barrier), one more stage in flight
+  constexpr int D = NST - 2 + LD;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   // LDS rows are 64 B (four 16-B slots); row R keeps logical slot s at physical slot
   // s ^ g((R >> 2) & 3), g = {0, 2, 3, 1}: ds_read_b128 serves a wave in the lane groups
@@ -455,6 +458,7 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int64
     if (t + 1 < nt) {
       if (t + D < nt) wait_vm<Q * (D - 1)>();
       else wait_vm<0>();
+      if constexpr (LD == 1) __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's reads of slot t done
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       if (ILV == 0 || idle)
@@ -486,6 +490,184 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int64
       for (int r = 0; r < 4; ++r) {
         const int gi = i0 + wr * 128 + a * 16 + 4 * fq + r;
         const int gj = j0 + wc * 64 + b * 16 + fr;
+        if (gi < ns && gj <= gi) {
+          int v = acc[a][b][r] % m;
+          if (v < 0) v += m;
+          uint8_t* p = dst + (int64_t)gi * ldp + gj;
+          if (accumulate) {
+            v += *p;
+            if (v >= m) v -= m;
+          }
+          *p = (uint8_t)v;
+        }
+      }
+}
+
+// A 256 x 384 tile of one modulus over one K split (r5): rows i0 .. i0+255, columns j0 .. j0+383,
+// strictly below the diagonal blocks (j0 + 384 <= i0, or the columns clamp at ns), so no idle waves
+// and no SAME panel.  40 KB of operands per K step for 384 MFMAs: 17 % fewer L2 -> LDS bytes per MAC
+// than the 256 x 256 tile (32 KB for 256).  8 waves as 2 x 4, each 128 x 96 = 8 x 6 blocks (192
+// accumulator registers).  Registers do not allow the 256-tile's double-buffered fragments, so the
+// B fragments come in three column groups of two through two 2-fragment buffers -- group g of step
+// t in buffer (3t + g) & 1, the next group read while the current group's 16 MFMAs run -- and the
+// A fragment of row a of step t + 1 is read right behind row a's last MFMA of step t.  4-stage ring
+// of 40 KB (X panel 16 KB, Y panel 24 KB), D = 2 steps of DMA lead, 5 pieces per wave per step,
+// one after each of the first five MFMA rows of group 0.
+template <int NST>
+__device__ __forceinline__ void syrk_tile_wide(const int8_t* __restrict__ base, int64_t cstride, int ns, int nt,
+                                               int i0, int j0, int m, char* smem, uint8_t* __restrict__ dst, int ldp,
+                                               int accumulate) {
+  constexpr int YP = 384 * KC;       // the column panel: 24 KB
+  constexpr int STG = PANEL + YP;    // 40 KB per stage
+  constexpr int Q = 5;               // DMA pieces per wave per stage (2 X + 3 Y)
+  constexpr int D = NST - 2;
+  static_assert(NST * STG <= 160 * 1024, "LDS");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // a piece is 16 rows x 64 B: its row block is wave-uniform (a scalar base) and every lane's
+  // offset in it the same for all pieces (the swizzle of row R depends on (R >> 2) & 3 only,
+  // i.e. on lane >> 4 here), so one 32-bit VGPR addresses all five.  No clamp at ns: the rows past
+  // ns only feed outputs past ns, which are not stored, and the residue buffer is padded
+  // (CORR_I8_RPAD) so the last row block reads inside the allocation.
+  // The DMA goes through buffer_load ... lds (MUBUF), not global_load_lds: the compiler's wait-count
+  // pass takes a pending global_load_lds for a FLAT access that may complete out of order with
+  // the LDS reads, and then waits lgkmcnt(0) before every MFMA whose fragment read is younger
+  // than that DMA -- an exposed LDS latency per column group (measured 30 % slower).  The
+  // buffer's range (the split's K chunks) also bounds the reads past ns: 0 comes back.
+  // (every operand of the buffer instruction wave-uniform by construction, or the compiler wraps
+  // it in a readfirstlane loop)
+  i0 = __builtin_amdgcn_readfirstlane(i0);
+  j0 = __builtin_amdgcn_readfirstlane(j0);
+  const uint64_t bu = (uint64_t)(uintptr_t)base;
+  const int8_t* ubase = (const int8_t*)(uintptr_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(bu >> 32)) << 32) |
+                                                   (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bu));
+  // (integer arithmetic only: HIP's min over int64 went through f64 on the VALU, and a VGPR
+  // range word made every DMA a readfirstlane loop)
+  const int64_t nbytes = (int64_t)nt * cstride;
+  const int nrec = __builtin_amdgcn_readfirstlane(nbytes >= 0xFFFFFFFFll ? (int)0xFFFFFFFFu : (int)(uint32_t)nbytes);
+  const int cst = __builtin_amdgcn_readfirstlane((int)cstride);
+  const uint32_t lo = (uint32_t)((lane >> 2) * KC + (((lane & 3) ^ swz((lane >> 4) & 3)) * 16));
+
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+  auto piece = [&](int t, int q) {
+    const uint32_t sb = lds0 + (uint32_t)((t % NST) * STG) + (q < 2 ? (wave * 2 + q) * 1024 : PANEL + (wave * 3 + q - 2) * 1024);
+    const int rb = q < 2 ? i0 + (wave * 2 + q) * 16 : j0 + (wave * 3 + q - 2) * 16;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(ubase), 0, nrec, 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(uintptr_t)sb, 16, (int)lo,
+                                             t * cst + rb * KC, 0, 0);
+  };
+  i32x4 acc[8][6];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 6; ++b) acc[a][b] = (i32x4){0, 0, 0, 0};
+  const int wr = wave >> 2, wc = wave & 3;
+  const int fo = (lane & 15) * KC + (((lane >> 4) ^ swz((lane >> 2) & 3)) * 16);
+  auto rdA = [&](int t, int a) -> i32x4 {
+    return *reinterpret_cast<const i32x4*>(smem + (t % NST) * STG + (wr * 128 + a * 16) * KC + fo);
+  };
+  auto rdB = [&](int t, int b) -> i32x4 {
+    return *reinterpret_cast<const i32x4*>(smem + (t % NST) * STG + PANEL + (wc * 96 + b * 16) * KC + fo);
+  };
+  i32x4 av[8], bb[2][2];
+  // The K loop is branch-free so the compiler's wait counts stay exact across it: the DMA of a
+  // step past the end re-loads the last chunk into its own slot (the same bytes: a benign
+  // overwrite), the reads past the end read a stale slot (unused), and the mod-m folds sit between
+  // K loops of FOLD steps.
+#pragma unroll
+  for (int t = 0; t <= D; ++t) {
+    const int tc = min(t, nt - 1);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) piece(tc, q);  // (the slot of min(t, nt-1): a repeat writes the same bytes)
+  }
+  wait_vm<Q * D>();
+  // retire every scalar load still pending (kernel arguments the epilogue needs): an SMEM load
+  // completes out of order with the LDS reads on the same counter, so while one is pending the
+  // compiler can only wait for lgkmcnt(0) before an MFMA whose fragments are in flight
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int a = 0; a < 8; ++a) av[a] = rdA(0, a);
+  bb[0][0] = rdB(0, 0);
+  bb[0][1] = rdB(0, 1);
+  // step t of parity P: groups 0, 1, 2 in buffers P, P^1, P
+  auto step = [&](int t, auto PC) {
+    constexpr int P = decltype(PC)::value;
+    wait_vm<Q * (D - 1)>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const int dt = min(t + D + 1, nt - 1);
+    // group 0 (buffer P); group 1's fragments into buffer P^1
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[a], bb[P][b], acc[a][b], 0, 0, 0);
+      if (a == 1) {  // (behind the first row: the DMA pieces follow rows 0-4)
+        __builtin_amdgcn_sched_barrier(0);
+        bb[P ^ 1][0] = rdB(t, 2);
+        bb[P ^ 1][1] = rdB(t, 3);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (a < Q) {
+        __builtin_amdgcn_sched_barrier(0);
+        piece(dt, a);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // group 1 (buffer P^1); group 2's fragments into buffer P
+    bb[P][0] = rdB(t, 4);
+    bb[P][1] = rdB(t, 5);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        acc[a][2 + b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[a], bb[P ^ 1][b], acc[a][2 + b], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    // group 2 (buffer P); step t+1's group 0 into buffer P^1, its A rows behind each row
+    bb[P ^ 1][0] = rdB(t + 1, 0);
+    bb[P ^ 1][1] = rdB(t + 1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        acc[a][4 + b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[a], bb[P][b], acc[a][4 + b], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      av[a] = rdA(t + 1, a);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // |acc| stays < m + FOLD * 64 * 127^2 < 2^31 between the folds
+  static_assert(FOLD % 2 == 0, "fold");
+  int t = 0;
+  for (int tf = 0; tf < nt; tf += FOLD) {
+    const int te = min(tf + FOLD, nt);
+    for (; t + 1 < te; t += 2) {
+      step(t, std::integral_constant<int, 0>{});
+      step(t + 1, std::integral_constant<int, 1>{});
+    }
+    if (te < nt) {
+#pragma unroll
+      for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 6; ++b)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[a][b][r] %= m;
+    }
+  }
+  if (t < nt) step(t, std::integral_constant<int, 0>{});
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 6; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gi = i0 + wr * 128 + a * 16 + 4 * fq + r;
+        const int gj = j0 + wc * 96 + b * 16 + fr;
         if (gi < ns && gj <= gi) {
           int v = acc[a][b][r] % m;
           if (v < 0) v += m;
@@ -532,7 +714,7 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8(const int8_t* __restrict__ R
 // with pace_every > 0, every pace_every K steps inside a tile: the workgroups that share an L2
 // then stream the same K window of the same panels (the launch-per-item form let them drift apart
 // over the 17 rounds at C3, and the XCD's 4 MB L2 held the union of their windows: 54 % hits).
-template <int NST, int ILV, bool MID>
+template <int NST, int ILV, bool MID, bool WIDE = false, int LD = 0>
 __global__ __launch_bounds__(512, 1) void k_syrk_i8_paced(const int8_t* __restrict__ R, int ns, int64_t ms, int64_t cs,
                                                           int kcs, const int4* __restrict__ xitems, int per_xcd,
                                                           int nsplit, uint8_t* __restrict__ P, int64_t pslab, int ldp,
@@ -553,12 +735,14 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8_paced(const int8_t* __restri
       const int8_t* base = R + (int64_t)l * ms + (int64_t)sp * kcs * cs;
       uint8_t* dst = P + (int64_t)(l * nsplit + sp) * pslab;
       const int m = modulus(l);
-      if (bi == bj)
-        syrk_tile<NST, 0, true, ILV>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate, ctr, nslot,
-                                     MID ? pace_every : 0, &epoch);
+      if (WIDE && bj >= 0x10000)
+        syrk_tile_wide<4>(base, cs, ns, kcs, bi * TB, (bj & 0xffff) * 128, m, smem, dst, ldp, accumulate);
+      else if (bi == bj)
+        syrk_tile<NST, 0, true, ILV, LD>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate, ctr,
+                                         nslot, MID ? pace_every : 0, &epoch);
       else
-        syrk_tile<NST, 0, false, ILV>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate, ctr, nslot,
-                                      MID ? pace_every : 0, &epoch);
+        syrk_tile<NST, 0, false, ILV, LD>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate, ctr,
+                                          nslot, MID ? pace_every : 0, &epoch);
     } else if (MID && pace_every > 0) {  // an empty slot still keeps the tile's pacing points
       for (int t = pace_every; t < kcs; t += pace_every) pace_xcd(ctr, epoch, nslot);
     }
@@ -852,10 +1036,66 @@ std::vector<int> corr_i8_xcd_items(const std::vector<int>& items, int nitems, in
   return out;
 }
 
+// The 256 x 384 table: per row block bi, its diagonal 256 tile, and the 2 bi 128-column units left
+// of it as 256 x 384 tiles from column 0, with one or two 256 tiles next to the diagonal when 2 bi
+// mod 3 leaves 2 or 1 units (2 bi = 1 mod 3 only for bi >= 2).  The same MACs as the 256-tile
+// grid, 13.7 % fewer operand bytes at ns = 4096 (3,536 vs 4,096 KB per K step and modulus).  The
+// tiles in Morton order of (row, column start) are cut into 8 / S compact groups of equal cost
+// (MFMA rows: 1.5 for a wide tile, 1 for a 256 tile, 0.75 for a diagonal one); XCD x takes split x
+// mod S and group x / S, its items ordered wide tiles first, then 256 tiles, then diagonal ones
+// (each kind modulus by modulus), so a round of nslot items is one kind of one modulus.
+std::vector<int> corr_i8_xcd_items_wide(int ns, const CorrI8Plan& p, int* per_xcd) {
+  struct T {
+    uint64_t key;
+    int bi, code, kind;  // kind 0 wide, 1 square, 2 diagonal
+  };
+  std::vector<T> t;
+  const int nb = (ns + i8::TB - 1) / i8::TB;
+  auto morton = [](uint32_t r, uint32_t c) {
+    uint64_t k = 0;
+    for (int b = 0; b < 20; ++b) k |= ((uint64_t)((r >> b) & 1u) << (2 * b + 1)) | ((uint64_t)((c >> b) & 1u) << (2 * b));
+    return k;
+  };
+  for (int bi = 0; bi < nb; ++bi) {
+    const int u = 2 * bi, r = u % 3;
+    const int nsq = r == 0 ? 0 : (r == 2 ? 1 : 2);
+    const int nw = (u - 2 * nsq) / 3;
+    for (int w = 0; w < nw; ++w) t.push_back({morton(2 * bi, 3 * w), bi, 0x10000 | (3 * w), 0});
+    for (int q = 0; q < nsq; ++q) t.push_back({morton(2 * bi, 2 * (bi - 1 - q)), bi, bi - 1 - q, 1});
+    t.push_back({morton(2 * bi, 2 * bi), bi, bi, 2});
+  }
+  std::stable_sort(t.begin(), t.end(), [](const T& a, const T& b) { return a.key < b.key; });
+  static const double cost[3] = {1.5, 1.0, 0.75};
+  double total = 0.0;
+  for (const T& x : t) total += cost[x.kind];
+  const int S = (8 % p.nsplit == 0) ? p.nsplit : 1;
+  const int ngrp = 8 / S;
+  std::vector<int> grp(t.size());
+  double run = 0.0;
+  for (size_t k = 0; k < t.size(); ++k) {
+    grp[k] = std::min(ngrp - 1, (int)((run + 0.5 * cost[t[k].kind]) * ngrp / total));
+    run += cost[t[k].kind];
+  }
+  std::vector<std::vector<int>> per(8);
+  for (int x = 0; x < 8; ++x)
+    for (int sp = x % S; sp < p.nsplit; sp += S)  // S = 1 when 8 % nsplit != 0: every split on every XCD
+      for (int kind = 0; kind < 3; ++kind)
+        for (int l = 0; l < i8::NMOD; ++l)
+          for (size_t k = 0; k < t.size(); ++k)
+            if (grp[k] == x / S && t[k].kind == kind) per[x].insert(per[x].end(), {t[k].bi, t[k].code, sp, l});
+  int px = 0;
+  for (int x = 0; x < 8; ++x) px = std::max(px, (int)per[x].size() / 4);
+  std::vector<int> out((size_t)8 * px * 4, -1);
+  for (int x = 0; x < 8; ++x) std::copy(per[x].begin(), per[x].end(), out.begin() + (size_t)x * px * 4);
+  *per_xcd = px;
+  return out;
+}
+
 hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowpad, const double* mean,
                           const double* devmax, const CorrI8Plan& p, const int* items, int8_t* R, uint8_t* P,
                           double* C, int64_t ldc, int divide, hipStream_t st, hipEvent_t syrk_begin,
-                          hipEvent_t syrk_end, const int* xitems, int per_xcd, unsigned* pace_ctr, int pace_every) {
+                          hipEvent_t syrk_end, const int* xitems, int per_xcd, unsigned* pace_ctr, int pace_every,
+                          int wide) {
   using namespace i8;
   // default: 5 ring stages, each wave's DMA pieces one after each of its first MFMA rows (ILV 1;
   // 22.0-22.8 ms at C3 against 24.0 for the pieces back to back after the barrier,
@@ -906,7 +1146,9 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
     if (e != hipSuccess) return e;
     nslot = std::max(1, cus / 8);
     for (const void* f : {reinterpret_cast<const void*>(&k_syrk_i8_paced<5, 1, false>),
-                          reinterpret_cast<const void*>(&k_syrk_i8_paced<5, 1, true>)}) {
+                          reinterpret_cast<const void*>(&k_syrk_i8_paced<5, 1, true>),
+                          reinterpret_cast<const void*>(&k_syrk_i8_paced<5, 1, false, true>),
+                          reinterpret_cast<const void*>(&k_syrk_i8_paced<5, 1, false, false, 1>)}) {
       e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(5 * 2 * PANEL));
       if (e != hipSuccess) return e;
     }
@@ -941,7 +1183,21 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
     if (paced) {
       e = hipMemsetAsync(pace_ctr, 0, 8 * 32 * sizeof(unsigned), st);
       if (e != hipSuccess) return e;
-      if (pace_every > 0)
+      // default: one more ring stage in flight (LD = 1: 21.89 vs 22.12 ms at C3, 7 interleaved rounds,
+      // profiles/r5/syrk_lead_wide_ab.log); PODS_SYRK_LEAD=0 (A/B) the r4 lead.  PODS_SYRK_WIDE=1
+      // (A/B): 256 x 384 tiles, 22.08 ms (their B fragments are read during the step, so they cannot
+      // take the extra stage; with LD = 1 on their 256 tiles 22.23)
+      const char* lv = std::getenv("PODS_SYRK_LEAD");
+      const bool lead = !(lv && lv[0] == '0');
+      if (lead && !wide && pace_every <= 0)
+        hipLaunchKernelGGL((k_syrk_i8_paced<5, 1, false, false, 1>), dim3(8 * nslot), dim3(512), 5 * 2 * PANEL, st,
+                           (const int8_t*)R, ns, ms, cs, p.kcs, reinterpret_cast<const int4*>(xitems), per_xcd,
+                           p.nsplit, P, pslab, ldp, li > 0 ? 1 : 0, pace_ctr, 0);
+      else if (wide)
+        hipLaunchKernelGGL((k_syrk_i8_paced<5, 1, false, true>), dim3(8 * nslot), dim3(512), 5 * 2 * PANEL, st,
+                           (const int8_t*)R, ns, ms, cs, p.kcs, reinterpret_cast<const int4*>(xitems), per_xcd,
+                           p.nsplit, P, pslab, ldp, li > 0 ? 1 : 0, pace_ctr, 0);
+      else if (pace_every > 0)
         hipLaunchKernelGGL((k_syrk_i8_paced<5, 1, true>), dim3(8 * nslot), dim3(512), 5 * 2 * PANEL, st,
                            (const int8_t*)R, ns, ms, cs, p.kcs, reinterpret_cast<const int4*>(xitems), per_xcd,
                            p.nsplit, P, pslab, ldp, li > 0 ? 1 : 0, pace_ctr, pace_every);

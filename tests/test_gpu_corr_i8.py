@@ -119,6 +119,28 @@ def test_corr_i8_splits_chunks_and_fold(ctx, monkeypatch):
     del snap
 
 
+def test_corr_i8_syrk_variants_exact(ctx, monkeypatch):
+    """Every SYRK schedule computes the exact integer product, so all equal the host's exact C bit
+    for bit: the default (persistent, XCD-paced, one extra ring stage), the r4 ring lead
+    (PODS_SYRK_LEAD=0), 256 x 384 tiles (PODS_SYRK_WIDE=1: at ns = 800 row block 3 takes two of
+    them, its rows 800-1023 past ns), pacing inside tiles (p64) and the launch-per-item grid
+    (PODS_SYRK_PACE=0); K splits and several residue launches with the extra stage."""
+    rng = np.random.default_rng(17)
+    ns, rows = 800, 9000   # 141 K chunks: three 64-chunk launches under the small budget
+    A = rng.standard_normal((rows, ns)) * np.linspace(0.5, 3.0, ns)[None, :] + np.arange(rows)[:, None] * 1e-3
+    snap, mean = load(ctx, A)
+    ref = exact_corr(A, mean, ns)
+    for env in ({}, {"PODS_SYRK_LEAD": "0"}, {"PODS_SYRK_WIDE": "1"}, {"PODS_SYRK_PACE": "p64"},
+                {"PODS_SYRK_PACE": "0"}, {"PODS_CORR_SPLITS": "3", "PODS_CORR_BUDGET_GB": "0.0001"},
+                {"PODS_SYRK_WIDE": "1", "PODS_CORR_SPLITS": "3", "PODS_CORR_BUDGET_GB": "0.0001"}):
+        for k in ("PODS_SYRK_LEAD", "PODS_SYRK_WIDE", "PODS_SYRK_PACE", "PODS_CORR_SPLITS", "PODS_CORR_BUDGET_GB"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        check_exact(corr(ctx, ns, 1), ref)
+    del snap
+
+
 def test_corr_i8_degenerate(ctx):
     """A zero matrix and rows constant in time (A - mean = 0): C = 0 exactly; a single
     non-zero element: C has one entry, exactly a^2 / ns."""
