@@ -12,7 +12,7 @@ import torch  # noqa: E402
 import podsgen  # noqa: E402
 from podsgen import engine as E  # noqa: E402
 
-KEYS = ("PODS_SYRK_I8", "PODS_CORR_ORDER", "PODS_CORR_SPLITS", "PODS_RES_I8", "PODS_RES_LAYOUT", "PODS_SYRK_PACE", "PODS_SYRK_WIDE", "PODS_SYRK_LEAD")
+KEYS = ("PODS_SYRK_I8", "PODS_CORR_ORDER", "PODS_CORR_SPLITS", "PODS_RES_I8", "PODS_RES_LAYOUT", "PODS_SYRK_PACE", "PODS_SYRK_WIDE", "PODS_SYRK_LEAD", "PODS_SYRK_DMA")
 rounds = int(sys.argv[1])
 configs = sys.argv[2:]
 J, K, NS = 256, 256, 4096
