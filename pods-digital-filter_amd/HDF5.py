@@ -124,11 +124,12 @@ def write_HDF5(i_d, filename="PODFS/PODFS.hdf5"):
         np.save(os.path.join(tmp, "N_FC.npy"), np.asarray(i_d.N_FC))
         np.save(os.path.join(tmp, "FC.npy"), np.asarray(i_d.FC, dtype=np.float64))
         np.save(os.path.join(tmp, "mean.npy"), np.asarray(i_d.mean, dtype=np.float64))
-        if hasattr(modes, "spatial") and hasattr(modes, "points"):
+        if hasattr(modes, "spatial") and hasattr(modes, "points") and not getattr(modes.spatial, "streamed", False):
             # the writer assembles each mode from these two (no (nm, P, 6) copy on either side)
             np.save(os.path.join(tmp, "points.npy"), modes.points)
             np.save(os.path.join(tmp, "spatial.npy"), np.asarray(modes.spatial, dtype=np.float64))
         else:
+            # one mode at a time (a multi-rank run's modes arrive per mode: digitalfilters.SlabColumns)
             for i in range(nm):
                 np.save(os.path.join(tmp, "mode_%04d.npy" % i), np.asarray(modes[i], dtype=np.float64))
         script = os.path.join(tmp, "writer.py")

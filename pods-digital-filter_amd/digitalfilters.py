@@ -361,21 +361,99 @@ def main(argv=None):
                       "false", i_d.grid, None, s.dt_eff, "velocity", 1, s.ns, 1, 1, i_d,
                       dist=dist if world > 1 else None)
     mean_local = pod_res.mean.cpu().numpy()
+    local_modes = i_d.spatial_modes
     if world > 1:
-        both = gather_row_slabs(dist, s, np.concatenate([mean_local[:, None], i_d.spatial_modes], axis=1))
-        mean_field, spatial = (both[:, 0].copy(), both[:, 1:].copy()) if rank == 0 else (None, None)
+        # the mean in one gather; the spatial modes streamed to rank 0 one mode at a time as its
+        # .prf / HDF5 writers ask for them (SlabColumns), so no host holds all nm modes of the
+        # whole inlet (C5: 20 x 3 x 1 M doubles = 0.5 GB) -- the other ranks serve the requests
+        mean_field = gather_row_slabs(dist, s, mean_local)
+        spatial = SlabColumns(dist, s, local_modes) if rank == 0 else None
     else:
-        mean_field, spatial = mean_local, i_d.spatial_modes
+        mean_field, spatial = mean_local, local_modes
     i_d.mean_field = mean_field
     i_d.spatial_modes = spatial
     if rank == 0:
-        pod.fourier_coefficients(i_d)
-        pod.pod2prf(i_d)
-        if options.hdf5:
-            HDF5.write_HDF5(i_d)
+        try:
+            pod.fourier_coefficients(i_d)
+            pod.pod2prf(i_d)
+            if options.hdf5:
+                HDF5.write_HDF5(i_d)
+        finally:
+            if world > 1:
+                spatial.close()
+    elif world > 1:
+        serve_slab_columns(dist, s, local_modes)
     if world > 1:
         dist.barrier()
     return i_d
+
+
+def _bcast_int(dist, v):
+    """Rank 0's integer to every rank (nccl: a device tensor, gloo: a host one)."""
+    import torch
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([0 if v is None else int(v)], dtype=torch.int64, device=dev)
+    dist.broadcast(t, src=0)
+    return int(t.item())
+
+
+class SlabColumns:
+    """Rank 0's view of a (3P, m) array whose rows lie in the ranks' row slabs (the spatial modes
+    after a multi-rank POD), gathered one column at a time: a[:, i] broadcasts i and gathers that
+    column's slabs (gather_row_slabs) while every other rank sits in serve_slab_columns; close()
+    releases them.  Only the last column is kept.  np.asarray(a) gathers every column (the whole
+    array, as the reference holds it)."""
+    streamed = True
+
+    def __init__(self, dist, s, local):
+        self.dist, self.s = dist, s
+        self.local = np.asarray(local, dtype=np.float64)
+        self.shape = (3 * s.P, self.local.shape[1])
+        self.ndim = 2
+        self._last = (None, None)
+        self._open = True
+
+    def column(self, i):
+        i = int(i)
+        if not -self.shape[1] <= i < self.shape[1]:
+            raise IndexError(i)
+        i %= self.shape[1]
+        if self._last[0] == i:
+            return self._last[1]
+        if not self._open:
+            raise RuntimeError("SlabColumns: the other ranks were released (close())")
+        _bcast_int(self.dist, i)
+        col = gather_row_slabs(self.dist, self.s, self.local[:, i])
+        self._last = (i, col)
+        return col
+
+    def __getitem__(self, idx):
+        if (isinstance(idx, tuple) and len(idx) == 2 and isinstance(idx[0], slice) and idx[0] == slice(None)
+                and isinstance(idx[1], (int, np.integer))):
+            return self.column(idx[1])
+        return np.asarray(self)[idx]
+
+    def __array__(self, dtype=None, copy=None):
+        out = np.empty(self.shape, dtype=np.float64)
+        for i in range(self.shape[1]):
+            out[:, i] = self.column(i)
+        return out if dtype is None else out.astype(dtype)
+
+    def close(self):
+        if self._open:
+            _bcast_int(self.dist, -1)
+            self._open = False
+
+
+def serve_slab_columns(dist, s, local):
+    """The ranks other than 0 while rank 0 reads a SlabColumns: send this rank's slab of each
+    requested column until rank 0 closes it."""
+    local = np.asarray(local, dtype=np.float64)
+    while True:
+        i = _bcast_int(dist, None)
+        if i < 0:
+            return
+        gather_row_slabs(dist, s, local[:, i])
 
 
 def gather_row_slabs(dist, s, local):

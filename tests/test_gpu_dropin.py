@@ -258,6 +258,11 @@ def test_sharded_pipeline_two_ranks_one_device():
         assert np.max(np.abs(c_sg * out[0]["c"][:, m] - fo.c[:, m])) <= 1e-6 * np.max(np.abs(fo.c[:, m]))
 
 
+def _h5py_ok():
+    import HDF5
+    return HDF5._h5py_python() is not None
+
+
 def _verbose_worker(rank, world, port, wdir, out):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
@@ -265,7 +270,7 @@ def _verbose_worker(rank, world, port, wdir, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     os.chdir(wdir)
     import digitalfilters as df
-    i_d = df.main(["-n", "6", "--seed", "19", "-j", "9", "-k", "8", "-v"])
+    i_d = df.main(["-n", "6", "--seed", "19", "-j", "9", "-k", "8", "-v"] + (["-5"] if _h5py_ok() else []))
     out[rank] = dict(nm=i_d.nm, mean=None if rank else i_d.mean_field)
     dist.destroy_process_group()
 
@@ -311,6 +316,22 @@ def test_verbose_cli_two_ranks_one_device(tmp_path):
         sg = np.sign(np.dot(a[:, 1], b[:, 1]))
         assert np.max(np.abs(a[:, 1] - sg * b[:, 1])) <= 1e-9 * np.max(np.abs(a[:, 1])), n
     assert (single / "PODFS" / "PODFS_mean.prf").read_text() == (multi / "PODFS" / "PODFS_mean.prf").read_text()
+    if _h5py_ok():   # the HDF5 file written from the modes streamed to rank 0 one at a time
+        import subprocess
+        import HDF5
+        reader = ("import h5py, numpy as np, sys\n"
+                  "a, b = (h5py.File(x, 'r')['main'] for x in sys.argv[1:3])\n"
+                  "assert np.array_equal(a['mean'][:], b['mean'][:]) and sorted(a['modes']) == sorted(b['modes'])\n"
+                  "for k in a['modes']:\n"
+                  "    x, y = a['modes'][k][:], b['modes'][k][:]\n"
+                  "    P = x.size // 6\n"
+                  "    assert np.array_equal(x[:3 * P], y[:3 * P])\n"
+                  "    sg = np.sign(np.dot(x[3 * P:], y[3 * P:]))\n"
+                  "    assert np.max(np.abs(x[3 * P:] - sg * y[3 * P:])) <= 1e-9 * np.max(np.abs(x[3 * P:])), k\n"
+                  "print('ok', len(a['modes']))\n")
+        r = subprocess.run([HDF5._h5py_python(), "-c", reader, str(single / "PODFS" / "PODFS.hdf5"),
+                            str(multi / "PODFS" / "PODFS.hdf5")], capture_output=True, text=True)
+        assert r.stdout.split() == ["ok", str(ref["nm"])], r.stderr
 
 
 def test_pack_unpack_lower_kernels():

@@ -375,6 +375,75 @@ def test_hdf5_streamed_modes_identical(tmp_path):
     assert out.stdout.split() == ["same", str(nm)], out.stderr
 
 
+def _c5_hdf5_worker(rank, world, port, fn, out):
+    """One rank of the streamed multi-rank HDF5 write at C5 size: rank 0 writes through a
+    ModeStack over digitalfilters.SlabColumns, the others serve their row slabs per mode."""
+    import hashlib
+    import types
+    import torch.distributed as dist
+    import HDF5
+    import PODFS
+    import digitalfilters as df
+    import podsgen
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    J = K = 1024
+    nm, P = 4, 1024 * 1024
+    s = types.SimpleNamespace(jma=J, kma=K, P=P)
+    rng = np.random.default_rng(123)
+    spatial = rng.standard_normal((3 * P, nm))    # the whole inlet's modes, sliced per rank
+    j0, j1 = podsgen.row_slab(J, rank, world)
+    rows = np.concatenate([np.arange(c * P + j0 * K, c * P + j1 * K) for c in range(3)])
+    local = spatial[rows]
+    if rank == 0:
+        points = rng.standard_normal((P, 3))
+        cols = df.SlabColumns(dist, s, local)
+        i_d = types.SimpleNamespace(nm=nm, period=0.5, num_points=P, N_FC=np.array([2, 1, 1, 1]),
+                                    FC=np.arange(15, dtype=np.float64).reshape(5, 3),
+                                    mean=np.zeros((P, 6)), modes=PODFS.ModeStack(points, cols, nm))
+        try:
+            HDF5.write_HDF5(i_d, fn)
+        finally:
+            cols.close()
+        want = []
+        for i in range(nm):
+            m = np.empty((P, 6))
+            m[:, 0:3] = points
+            m[:, 3:] = spatial[:, i].reshape((P, 3), order="F")
+            want.append(hashlib.sha1(m.reshape(P * 6, order="F").tobytes()).hexdigest())
+        out[0] = want
+    else:
+        df.serve_slab_columns(dist, s, local)
+    dist.destroy_process_group()
+
+
+@pytest.mark.skipif(_h5py_python() is None, reason="no interpreter with h5py")
+def test_hdf5_c5_size_streamed_two_ranks(tmp_path):
+    """BASELINE config 5's streamed HDF5 write at its size (1024 x 1024 inlet, 4 modes of 6 x 1 M
+    doubles, 0.2 GB), from two ranks holding row slabs: every mode dataset equals the mode built
+    from the whole array (SHA-1 of its bytes), and rank 0 only ever held one mode."""
+    import multiprocessing as mp
+    fn = str(tmp_path / "PODFS_c5.hdf5")
+    mgr = mp.Manager()
+    out = mgr.dict()
+    ctx = mp.get_context("spawn")
+    port = 29900 + os.getpid() % 90
+    procs = [ctx.Process(target=_c5_hdf5_worker, args=(r, 2, port, fn, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(600)
+        assert p.exitcode == 0
+    reader = ("import h5py, hashlib, numpy as np, sys\n"
+              "f = h5py.File(sys.argv[1], 'r')['main']\n"
+              "print(' '.join(hashlib.sha1(f['modes'][k][:].tobytes()).hexdigest() for k in sorted(f['modes'])))\n"
+              "print(f['mean'].attrs['Np'], f.attrs['N_POD'])\n")
+    r = subprocess.run([_h5py_python(), "-c", reader, fn], capture_output=True, text=True)
+    lines = r.stdout.split("\n")
+    assert lines[0].split() == list(out[0]), r.stderr
+    assert lines[1].split() == [str(1024 * 1024), "4"]
+
+
 def _gloo_worker(rank, world, port, A, out):
     """One rank of the product's multi-GPU host path on gloo/CPU tensors:
     engine.allreduce_correlation (packed lower-triangle all-reduce, divide, mirror) and
