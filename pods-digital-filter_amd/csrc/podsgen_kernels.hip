@@ -874,6 +874,8 @@ __global__ __launch_bounds__(256) void k_mean(const double* __restrict__ AT, int
         double r0 = ld(0), r1 = ld(16), r2 = ld(32), r3 = ld(48);
         double r4 = ld(64), r5 = ld(80), r6 = ld(96), r7 = ld(112);
         int i = 8;
+        // two iterations' 16 loads in flight per wave (the adds keep numpy's order)
+#pragma unroll 2
         for (; i < n - (n % 8); i += 8) {
           const int64_t b = (int64_t)i * 16;
           r0 = r0 + ld(b);
