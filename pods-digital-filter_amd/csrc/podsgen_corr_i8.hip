@@ -138,8 +138,8 @@ __global__ __launch_bounds__(256) void k_absdev(const double* __restrict__ AT, i
 // i (one 128-B run of the K-tiled fp64 A) and writes 16 bytes per modulus at
 // R_l[kc][i][16 q ..]: a wave covers 16 snapshots x 64 rows = 1 KB contiguous per modulus.
 // V: 0 = unsigned 11-bit limbs, 1 = signed 14-bit limbs (two packed ops fewer per element pair
-// and modulus), 7 / 8 = 0 / 1 with the mean through LDS (ns % 16 == 0; 8 the default); 4, 6:
-// other load paths (A/B); 2 / 3: measurement only.  r5 counters (profiles/r5/residues_pmc.json):
+// and modulus), 7 / 8 = 0 / 1 with the mean through LDS (ns % 16 == 0; 8 the default); 2 / 3:
+// measurement only.  r5 counters (profiles/r5/residues_pmc.json):
 // ~2,000 VALU instructions per wave (4 cycles each) make a ~3 ms VALU floor at C3 -- not the HBM
 // traffic, as r4 thought: without stores the kernel ran as long, without loads 3.1 ms -- and the
 // 16 per-lane mean loads of the r4 kernel, each behind its own branch and vmcnt(0), were two
@@ -148,9 +148,8 @@ template <int V>
 __device__ __forceinline__ void residues_body(const double* __restrict__ AT, int ns, int64_t rowlen,
                                               int64_t rowpad, const double* __restrict__ mean,
                                               const double* __restrict__ devmax, int bbits, int64_t kc0,
-                                              int64_t nkc, int8_t* __restrict__ R, int64_t ms, int64_t cs,
-                                              int64_t t = -1, const double2* pre = nullptr) {
-  if (t < 0) t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+                                              int64_t nkc, int8_t* __restrict__ R, int64_t ms, int64_t cs) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int q = (int)(t & 3);
   const int64_t rest = t >> 2;
   if (rest >= nkc * ns) return;
@@ -168,55 +167,9 @@ __device__ __forceinline__ void residues_body(const double* __restrict__ AT, int
 #pragma unroll
     for (int e = 0; e < 16; ++e) x[e] = r0 + e < rowlen ? x[e] - mv[e] : 0.0;
   };
-  if constexpr (V == 6) {  // the record and its mean slice loaded ahead by k_residues_pipe
-    if (r0 < rowpad) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        a[2 * e] = pre[e].x;
-        a[2 * e + 1] = pre[e].y;
-      }
-#pragma unroll
-      for (int e = 0; e < 16; ++e) a[e] = r0 + e < rowlen ? a[e] - pre[8 + e / 2][e & 1] : 0.0;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) a[e] = 0.0;
-    }
-  } else if constexpr (V == 2) {  // measurement only (PODS_RES_I8=2): no A loads
+  if constexpr (V == 2) {  // measurement only (PODS_RES_I8=2): no A loads
 #pragma unroll
     for (int e = 0; e < 16; ++e) a[e] = (double)(i + e) * 0.37 - (double)r0;
-  } else if constexpr (V == 4) {
-    // Coalesced loads through LDS (ns % 16 == 0: a wave's 16 snapshots x 4 quarters are four
-    // contiguous 2 KB blocks).  A thread's own 128-B record loaded directly makes every load
-    // instruction touch 64 cache lines 16 B each (lanes 128 B apart), the same lines again for
-    // each of its 8 instructions -- the kernel ran as fast with no stores at all (r5).  Here load
-    // k reads 1 KB contiguous (block k / 2, half k % 2), lanes write it to the wave's 8 KB of LDS
-    // (record rec = q * 16 + snapshot, its 16-B chunk c at column c ^ key(rec), key = (rec & 7) ^
-    // (rec >> 4): conflict-free for ds_read_b128's lane groups), and each thread reads back its
-    // record.
-    extern __shared__ __attribute__((aligned(16))) char res_lds[];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    char* W = res_lds + wv * 8192;
-    const int64_t wbase = ((int64_t)blockIdx.x * 256 + wv * 64) >> 2;  // first (chunk, snapshot) of the wave
-    const int i0 = (int)(wbase % ns);
-    const int64_t kw = wbase / ns;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int qq = k >> 1, h = k & 1;
-      const int64_t rq = (kc0 + kw) * 64 + qq * 16;
-      const int rec = qq * 16 + h * 8 + (lane >> 3), c = lane & 7;
-      double2 v = make_double2(0.0, 0.0);
-      if (rq < rowpad)
-        v = reinterpret_cast<const double2*>(AT + (((rq >> 4) * ns + i0) << 4))[h * 64 + lane];
-      *reinterpret_cast<double2*>(W + rec * 128 + ((c ^ ((rec & 7) ^ (rec >> 4))) * 16)) = v;
-    }
-    const int rec = q * 16 + (lane >> 2), key = (rec & 7) ^ (rec >> 4);
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const double2 v = *reinterpret_cast<const double2*>(W + rec * 128 + ((c ^ key) * 16));
-      a[2 * c] = v.x;
-      a[2 * c + 1] = v.y;
-    }
-    sub_mean(a);
   } else if constexpr (V == 7 || V == 8) {
     // the mean through LDS (ns % 16 == 0: one K chunk per wave): one 8-B load per lane fetches
     // the wave's 64 mean values, instead of 16 per-lane loads of 4 distinct slices (two thirds of
@@ -392,37 +345,6 @@ __device__ __forceinline__ void residues_body(const double* __restrict__ AT, int
 template <int V>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) void k_residues(PODS_RES_ARGS) {
   residues_body<V>(PODS_RES_PASS);
-}
-// Software-pipelined form (r5, PODS_RES_I8=5): a grid-stride loop whose threads load the next
-// item's 128-B record before computing the current one, so the loads of one item overlap the
-// ~9,000 VALU cycles per wave of the previous (the plain kernel ran 3.1 ms without its loads and
-// 4.6 with them: the waves waited on their loads with nothing else to do).
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) void k_residues_pipe(PODS_RES_ARGS) {
-  const int64_t total = nkc * ns * 4, stride = (int64_t)gridDim.x * 256;
-  // v[0..7]: the record, v[8..15]: mean[r0 .. r0+15] (index clamped; unused past rowlen)
-  auto load = [&](int64_t t, double2 (&v)[16]) {
-    const int q = (int)(t & 3);
-    const int64_t rest = t >> 2;
-    const int i = (int)(rest % ns);
-    const int64_t r0 = (kc0 + rest / ns) * 64 + q * 16;
-    const int64_t tt = t < total ? t : total - 1;
-    const int64_t r0c = r0 < rowpad ? r0 : 0;
-    const double2* src = reinterpret_cast<const double2*>(AT + ((((r0c >> 4) * ns) + (tt < total ? i : 0)) << 4));
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = src[e];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) v[8 + e / 2][e & 1] = mean[r0 + e < rowlen ? r0 + e : rowlen - 1];
-  };
-  int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  double2 nv[16];
-  load(t, nv);
-  for (; t < total; t += stride) {
-    double2 cv[16];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) cv[e] = nv[e];
-    load(t + stride, nv);
-    residues_body<6>(PODS_RES_PASS, t, cv);
-  }
 }
 #undef PODS_RES_ARGS
 #undef PODS_RES_PASS
@@ -1287,9 +1209,10 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
     // default (r5), ns % 16 == 0: k_residues<8> -- the wave's 64 mean values through LDS and the
     // signed 14-bit limbs, 3.72 vs 4.37 ms at C3 (profiles/r5/residues_ab.log); otherwise <0>.
     // PODS_RES_I8 (A/B runs): 0 / 1 the r4 kernel (unsigned 11-bit / signed 14-bit limbs), 7 the
-    // LDS mean with unsigned limbs (3.83), 4 loads coalesced through an LDS transpose (slower), 5
-    // a software-pipelined grid-stride form (no faster); 2 / 3 measurement only (no loads / no
-    // stores: 3.1 / 4.5 ms, the kernel is VALU-bound at ~3 ms plus its load stalls)
+    // LDS mean with unsigned limbs (3.83); 2 / 3 measurement only (no loads / no stores: 3.1 / 4.5
+    // ms, the kernel is VALU-bound at ~3 ms plus its load stalls).  Measured slower and removed
+    // (DESIGN.md s3): record loads coalesced through an LDS transpose, software-pipelined
+    // grid-stride forms prefetching the next record (and its mean)
     const char* rv = std::getenv("PODS_RES_I8");
     const int64_t thr = p.chunks * ns * 4;
     const bool r8 = ns % 16 == 0 && !(rv && rv[0] && rv[0] != '8');
@@ -1297,24 +1220,10 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
                      : rv && rv[0] == '1' ? reinterpret_cast<const void*>(&k_residues<1>)
                      : rv && rv[0] == '2' ? reinterpret_cast<const void*>(&k_residues<2>)
                      : rv && rv[0] == '3' ? reinterpret_cast<const void*>(&k_residues<3>)
-                     : rv && rv[0] == '4' && ns % 16 == 0 ? reinterpret_cast<const void*>(&k_residues<4>)
                      : rv && rv[0] == '7' && ns % 16 == 0 ? reinterpret_cast<const void*>(&k_residues<7>)
                                           : reinterpret_cast<const void*>(&k_residues<0>);
-    const unsigned rlds = rk == reinterpret_cast<const void*>(&k_residues<4>)   ? 4 * 8192
-                          : rk == reinterpret_cast<const void*>(&k_residues<7>) ? 4 * 512
-                          : rk == reinterpret_cast<const void*>(&k_residues<8>) ? 4 * 512
-                                                                                : 0;
-    const bool pipe = rv && rv[0] == '5';
-    int rdev = 0, rcus = 0;
-    if (pipe) {
-      e = hipGetDevice(&rdev);
-      if (e == hipSuccess) e = hipDeviceGetAttribute(&rcus, hipDeviceAttributeMultiprocessorCount, rdev);
-      if (e != hipSuccess) return e;
-    }
-    // the pipelined form: 3 workgroups per CU (12 waves, its occupancy), each thread ~thr / (768 * 256) items
-    const unsigned rgrid = pipe ? (unsigned)std::min<int64_t>((thr + 255) / 256, (int64_t)rcus * 3)
-                                : (unsigned)((thr + 255) / 256);
-    if (pipe) rk = reinterpret_cast<const void*>(&k_residues_pipe);
+    const unsigned rlds = r8 || (rv && rv[0] == '7' && ns % 16 == 0) ? 4 * 512 : 0;
+    const unsigned rgrid = (unsigned)((thr + 255) / 256);
     {
       const double* AT_ = AT;
       const double* mean_ = mean;
