@@ -425,7 +425,7 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int64
   auto piece = [&](int t, int q) {
     if constexpr (DIAG == 2) return;
     const uint32_t sb = lds0 + (uint32_t)((t % NST) * STG);
-    const int8_t* g = base + (int64_t)(DIAG >= 3 ? (t & 7) : t) * cstride;  // DIAG 3/4: an L2-resident K window
+    const int8_t* g = base + (int64_t)(DIAG == 3 || DIAG == 4 ? (t & 7) : t) * cstride;  // DIAG 3/4: an L2-resident K window
     if (q < 2) dma16(g + xo[q], sb + (wave * 2 + q) * 1024);
     else dma16(g + yo[q - 2], sb + PANEL + (wave * 2 + q - 2) * 1024);
   };
@@ -508,7 +508,7 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int64
       if (t + D < nt) wait_vm<Q * (D - 1)>();
       else wait_vm<0>();
       if constexpr (LD == 1) __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's reads of slot t done
-      __builtin_amdgcn_s_barrier();
+      if constexpr (DIAG != 5) __builtin_amdgcn_s_barrier();  // DIAG 5 (measurement only): no per-step barrier
       __builtin_amdgcn_sched_barrier(0);
       if (ILV == 0 || idle)
         if (t + D + 1 < nt) issue(t + D + 1);
@@ -1157,7 +1157,7 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
     if (v[0] == '4') variant = 4;
     if (v[0] == '5') variant = 5;
     if (v[0] == 'i') variant = 40 + (v[1] ? v[1] - '0' : 1);
-    if (v[0] == '9') variant = v[1] == 'm' ? 91 : v[1] == 'w' ? 93 : v[1] == 'x' ? 94 : v[1] == 'y' ? 95 : 92;
+    if (v[0] == '9') variant = v[1] == 'm' ? 91 : v[1] == 'w' ? 93 : v[1] == 'x' ? 94 : v[1] == 'y' ? 95 : v[1] == 'b' ? 96 : 92;
   }
   const void* fn = variant == 5 ? reinterpret_cast<const void*>(&k_syrk_i8<5>)
                  : variant == 91 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 1>)
@@ -1168,11 +1168,12 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
                  : variant == 42 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 0, 2>)
                  : variant == 44 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 0, 4>)
                  : variant == 95 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 3, 1>)
+                 : variant == 96 ? reinterpret_cast<const void*>(&k_syrk_i8<5, 5, 1>)
                  : variant == 45 ? reinterpret_cast<const void*>(&k_syrk_i8<5, 0, 1>)
                  : variant == 46 ? reinterpret_cast<const void*>(&k_syrk_i8<5, 0, 2>)
                  : variant == 47 ? reinterpret_cast<const void*>(&k_syrk_i8<5, 0, 4>)
                                  : reinterpret_cast<const void*>(&k_syrk_i8<4>);
-  const size_t lds = (size_t)(variant == 5 || (variant >= 45 && variant <= 47) ? 5 : 4) * 2 * PANEL;
+  const size_t lds = (size_t)(variant == 5 || (variant >= 45 && variant <= 47) || variant == 96 ? 5 : 4) * 2 * PANEL;
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   // residue layout: modulus l's K chunk kc at R + l * ms + kc * cs, one matrix per modulus
