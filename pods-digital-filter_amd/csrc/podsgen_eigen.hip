@@ -527,14 +527,27 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
 #pragma unroll
     for (int h = 0; h < RL / RH; ++h) {
       double vr[RH], wr[RH];
-      bool live[RH];
+      // The group's multipliers and LDS slot values are read back to back before any use or
+      // write (r5): read one by one -- each behind its row's liveness branch, or after the
+      // previous element's LDS write -- they compiled to one LDS round trip each, serial.
+      double rv[RH], rw[RH];
+#pragma unroll
+      for (int q = 0; q < RH; ++q) {
+        rv[q] = rsv[I0 + h * RH + q];
+        rw[q] = rsw[I0 + h * RH + q];
+      }
+      double lv[RH][SL > 0 ? SL : 1];
+#pragma unroll
+      for (int q = 0; q < RH; ++q)
+#pragma unroll
+        for (int m = 0; m < SL; ++m) lv[q][m] = Al[(m * RL + h * RH + q) * TT + t];
 #pragma unroll
       for (int q = 0; q < RH; ++q) {
         const int i = I0 + h * RH + q;
         const int r = g + G * i;
-        live[q] = r >= j + 1 && r < n;
-        vr[q] = live[q] ? uniform(rsv[i]) : 0.0;
-        wr[q] = live[q] ? uniform(rsw[i]) : 0.0;
+        const bool live = r >= j + 1 && r < n;
+        vr[q] = uniform(live ? rv[q] : 0.0);
+        wr[q] = uniform(live ? rw[q] : 0.0);
       }
 #pragma unroll
       for (int m = K; m < S; ++m) {
@@ -548,7 +561,7 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
             __builtin_amdgcn_raw_buffer_store_b64(
                 __builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(rwm, 0, 0, 0)), nv), rwm, soff[m - K], so, 0);
           } else if (m < K + SG + SL) {
-            double& ref = Al[((m - K - SG) * RL + ii) * TT + t];
+            double& ref = lv[q][m - K - SG];
             ref = __builtin_fma(-vr[q], p[m], __builtin_fma(-wr[q], vp[m], ref));
           } else {
             double& ref = Ar[ii][m - K - SG - SL];
@@ -556,6 +569,10 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
           }
         }
       }
+#pragma unroll
+      for (int q = 0; q < RH; ++q)
+#pragma unroll
+        for (int m = 0; m < SL; ++m) Al[(m * RL + h * RH + q) * TT + t] = lv[q][m];
     }
     if (trace) trace[j * 8 + 7] = (int64_t)__builtin_amdgcn_s_memrealtime();
 #pragma unroll
