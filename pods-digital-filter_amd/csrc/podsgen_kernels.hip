@@ -1232,16 +1232,22 @@ __global__ __launch_bounds__(256) void k_spatial_modes(const double* __restrict_
     if (!valid) continue;
     const double2* src = reinterpret_cast<const double2*>(base + (int64_t)c0 * 16);
     double2 cur[U], nxt[U];
+    // The loads past lim re-read the chunk's last snapshot and are zeroed where they are used
+    // (r5), and the groups alternate between two register sets within one loop iteration: with
+    // the substitution at the load the compiler sank each prefetch load into its own branch,
+    // and with a loop-carried prefetch its wait counts lost their order at the loop head -- in
+    // both cases each group waited for its loads right after issuing them
+    auto load = [&](double2 (&v)[U], int g0) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) cur[u] = u < lim ? src[u * 8] : make_double2(m0, m1);
-    for (int g = 0; g < lim; g += U) {
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        nxt[u] = (g + U + u < lim) ? src[(g + U + u) * 8] : make_double2(m0, m1);
+      for (int u = 0; u < U; ++u) v[u] = src[min(g0 + u, lim - 1) * 8];
+      __builtin_amdgcn_sched_barrier(0);  // issued here, not sunk next to their uses
+    };
+    auto group = [&](const double2 (&v)[U], int g0) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const double a0 = cur[u].x - m0, a1 = cur[u].y - m1;  // zero past lim: Ts rows are 0 too
-        const double* tr = Ts[(g + u) & (CH - 1)];
+        const bool in = g0 + u < lim;  // zero past lim: Ts rows are 0 too
+        const double a0 = in ? v[u].x - m0 : 0.0, a1 = in ? v[u].y - m1 : 0.0;
+        const double* tr = Ts[(g0 + u) & (CH - 1)];
 #pragma unroll
         for (int m = 0; m < NMB; m += 2) {
           const double2 tv = *reinterpret_cast<const double2*>(tr + m);
@@ -1251,8 +1257,13 @@ __global__ __launch_bounds__(256) void k_spatial_modes(const double* __restrict_
           acc1[m + 1] = __builtin_fma(a1, tv.y, acc1[m + 1]);
         }
       }
-#pragma unroll
-      for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+    };
+    load(cur, 0);
+    for (int g = 0; g < lim; g += 2 * U) {
+      load(nxt, g + U);
+      group(cur, g);
+      load(cur, g + 2 * U);
+      group(nxt, g + U);
     }
   }
   if (part) {
