@@ -279,7 +279,7 @@ struct pods_ctx {
   int nitems = 0;
   int64_t items_key = -1;
   int64_t lund_sj = 0;  // j-stride of the Lund table (0: constant along j)
-  int nprog_mean = 0;
+  int nprog_mean = 0, nleaf_mean = 0;
   bool mean_valid = false;
   bool have_snapshots = false;  // A holds ns x rowlen snapshots (generated or loaded)
   bool centered = false;        // A holds A - mean (pods_center); consumers subtract zero
@@ -569,6 +569,14 @@ namespace {
 int upload_mean_program(pods_ctx* c, int ns) {
   std::vector<int> prog = pairwise_program(ns);
   c->nprog_mean = (int)prog.size() / 2;
+  // the leaves (start, length) in program order follow the program (k_mean_leaves)
+  int nleaf = 0;
+  for (int k = 0; k < c->nprog_mean; ++k)
+    if (prog[2 * k] >= 0) ++nleaf;
+  const std::vector<int> ops(prog);
+  for (int k = 0; k < c->nprog_mean; ++k)
+    if (ops[2 * k] >= 0) prog.insert(prog.end(), {ops[2 * k], ops[2 * k + 1]});
+  c->nleaf_mean = nleaf;
   PODS_HIP(ensure(c->prog_mean, prog.size() * sizeof(int)));
   PODS_HIP(hipMemcpy(c->prog_mean.p, prog.data(), prog.size() * sizeof(int), hipMemcpyHostToDevice));
   return PODS_OK;
@@ -991,7 +999,8 @@ int pods_mean(pods_ctx* c, double* mean_out, int out_is_device) {
   PODS_HIP(hipSetDevice(c->device));
   PODS_HIP(ensure(c->devmax, sizeof(double)));
   PODS_HIP(pods::launch_mean(c->A.as<double>(), c->rowlen, c->p.ns, c->prog_mean.as<int>(),
-                             c->nprog_mean, c->mean.as<double>(), c->stream, c->devmax.as<double>()));
+                             c->nprog_mean, c->mean.as<double>(), c->stream, c->devmax.as<double>(),
+                             c->nleaf_mean));
   c->mean_valid = true;
   c->dev_valid = true;
   if (mean_out) {

@@ -45,7 +45,7 @@ hipError_t launch_lund_apply(double* yu, double* yv, double* yw, int64_t P, cons
                              int lund_mode, const double* rot, int rotate, hipStream_t st);
 // devmax (nullable): also max |fl(a - mean)| over the matrix, as a double (zeroed here)
 hipError_t launch_mean(const double* AT, int64_t rowlen, int ns, const int* prog, int nprog,
-                       double* mean, hipStream_t st, double* devmax = nullptr);
+                       double* mean, hipStream_t st, double* devmax = nullptr, int nleaf = 0);
 // The correlation by exact int8-MFMA modular products + CRT (podsgen_corr_i8.hip).
 struct CorrI8Plan {
   int bbits;       // scaled elements are integers with |a'| <= 2^bbits

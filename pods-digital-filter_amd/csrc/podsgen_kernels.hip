@@ -907,6 +907,98 @@ __global__ __launch_bounds__(256) void k_mean(const double* __restrict__ AT, int
   }
 }
 
+// The same mean with the leaves spread over threads (r5): k_mean walks a row's whole program in
+// one thread (3 waves per SIMD at C3, each a chain of 256 dependent load groups plus a scratch
+// stack: latency-bound at ~5.3 TB/s).  Here a 256-thread block takes 16 rows; thread (row rl,
+// lane lg) sums leaves lg, lg + 16, ... of its row with k_mean's exact leaf arithmetic into LDS,
+// and one thread per row then replays the program over those leaf sums (stack in LDS) -- the
+// same additions in the same order, so the mean is bit-identical.  The leaves (start, length)
+// follow the program in prog (upload_mean_program); nleaf <= 256.
+template <int LN>
+__global__ __launch_bounds__(16 * LN) void k_mean_leaves(const double* __restrict__ AT, int64_t rowlen, int ns,
+                                                     const int* __restrict__ prog, int nprog, int nleaf,
+                                                     double* __restrict__ mean,
+                                                     unsigned long long* __restrict__ devmax) {
+  extern __shared__ __attribute__((aligned(16))) double ml[];
+  double* vals = ml;                        // [16][nleaf]
+  double* mxs = ml + 16 * nleaf;            // [16][LN]
+  double* mns = mxs + 16 * LN;              // [16][LN]
+  double* stk = mns + 16 * LN;              // [16][32]
+  const int rl = threadIdx.x & 15, lg = threadIdx.x >> 4;
+  const int64_t r = (int64_t)blockIdx.x * 16 + rl;
+  const bool valid = r < rowlen;
+  const int* leaves = prog + 2 * nprog;
+  double mx = -__builtin_huge_val(), mn = __builtin_huge_val();
+  if (valid) {
+    for (int lf = lg; lf < nleaf; lf += LN) {
+      const int s = leaves[2 * lf], n = leaves[2 * lf + 1];
+      const double* a = AT + at_off(r, s, ns);
+      auto ld = [&](int64_t k) -> double {
+        const double x = a[k];
+        mx = fmax(mx, x);
+        mn = fmin(mn, x);
+        return x;
+      };
+      double res;
+      if (n < 8) {
+        res = 0.0;
+        for (int i = 0; i < n; ++i) res = res + ld((int64_t)i * 16);
+      } else {
+        double r0 = ld(0), r1 = ld(16), r2 = ld(32), r3 = ld(48);
+        double r4 = ld(64), r5 = ld(80), r6 = ld(96), r7 = ld(112);
+        int i = 8;
+#pragma unroll 2
+        for (; i < n - (n % 8); i += 8) {
+          const int64_t b = (int64_t)i * 16;
+          r0 = r0 + ld(b);
+          r1 = r1 + ld(b + 16);
+          r2 = r2 + ld(b + 32);
+          r3 = r3 + ld(b + 48);
+          r4 = r4 + ld(b + 64);
+          r5 = r5 + ld(b + 80);
+          r6 = r6 + ld(b + 96);
+          r7 = r7 + ld(b + 112);
+        }
+        res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+        for (; i < n; ++i) res = res + ld((int64_t)i * 16);
+      }
+      vals[rl * nleaf + lf] = res;
+    }
+  }
+  mxs[rl * LN + lg] = mx;
+  mns[rl * LN + lg] = mn;
+  __syncthreads();
+  double dev = 0.0;
+  if (lg == 0 && valid) {
+    double* st = stk + rl * 32;
+    int sp = 0, k = 0;
+    for (int op = 0; op < nprog; ++op) {
+      if (prog[2 * op] < 0) {
+        const double bsum = st[--sp];
+        st[sp - 1] = st[sp - 1] + bsum;
+      } else {
+        st[sp++] = vals[rl * nleaf + k++];
+      }
+    }
+    const double mu = (0.0 + st[0]) / (double)ns;
+    mean[r] = mu;
+    for (int q = 0; q < LN; ++q) {
+      mx = fmax(mx, mxs[rl * LN + q]);
+      mn = fmin(mn, mns[rl * LN + q]);
+    }
+    dev = fmax(mx - mu, mu - mn);
+  }
+  if (devmax && threadIdx.x < 64) {  // the 16 row threads are lanes 0-15 of wave 0
+    unsigned long long u = (unsigned long long)__double_as_longlong(dev > 0.0 ? dev : 0.0);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long v = __shfl_xor(u, o);
+      u = v > u ? v : u;
+    }
+    if (threadIdx.x == 0) atomicMax(devmax, u);
+  }
+}
+
 // main() :1492-1495 (A[:, j] = A[:, j] - mean_field) in place on the K-tiled snapshot matrix:
 // element f of AT belongs to row r = (f / (16 ns)) * 16 + f % 16.  Two doubles per thread.
 // The subtraction is the one the SYRK and the spatial-mode kernels would otherwise repeat
@@ -1486,10 +1578,22 @@ int filter_yz_max_K(int Kp) {
 }
 
 hipError_t launch_mean(const double* AT, int64_t rowlen, int ns, const int* prog, int nprog,
-                       double* mean, hipStream_t st, double* devmax) {
+                       double* mean, hipStream_t st, double* devmax, int nleaf) {
   if (devmax) {
     const hipError_t e = hipMemsetAsync(devmax, 0, sizeof(double), st);
     if (e != hipSuccess) return e;
+  }
+  // default (r5): the leaves spread over threads when there are at least 2 (and <= 256);
+  // PODS_MEAN=row (A/B): one thread per row
+  const char* mv = std::getenv("PODS_MEAN");
+  if (nleaf >= 2 && nleaf <= 256 && !(mv && mv[0] == 'r')) {
+    // 16 leaf lanes per row (1.12-1.14 ms at C3; 32 lanes in 512-thread blocks 1.20, one thread
+    // per row 1.23: profiles/r5/mean_ab.log)
+    constexpr int LN = 16;
+    const size_t lds = ((size_t)16 * nleaf + 2 * 16 * LN + 16 * 32) * sizeof(double);
+    hipLaunchKernelGGL(k_mean_leaves<LN>, dim3((unsigned)((rowlen + 15) / 16)), dim3(16 * LN), lds, st, AT, rowlen,
+                       ns, prog, nprog, nleaf, mean, reinterpret_cast<unsigned long long*>(devmax));
+    return hipGetLastError();
   }
   hipLaunchKernelGGL(k_mean, dim3((unsigned)((rowlen + 255) / 256)), dim3(256), 0, st, AT, rowlen, ns,
                      prog, nprog, mean, reinterpret_cast<unsigned long long*>(devmax));
