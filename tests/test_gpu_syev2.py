@@ -146,11 +146,23 @@ def test_spectrum_queue_two_stage_spreads_and_matches(ctx):
     the end, each equal to pods_syev2's eigenvalues bit for bit."""
     n = 8192
     mats = [pod_like(n, seed=90 + i) for i in range(3)]
+    torch.cuda.synchronize()
+    free0, _ = torch.cuda.mem_get_info()
     q = E.SpectrumQueue(ctx, n, rank=1, world=3)
+    assert q.max_slots == 2   # two-stage slots (ns > 4096) are bounded (ADVICE r4)
+    grown = 0
     for C in mats:
         q.submit(C)
+        torch.cuda.synchronize()
+        grown = max(grown, free0 - torch.cuda.mem_get_info()[0])
     assert q.pending or q.finished
     q.drain()
+    torch.cuda.synchronize()
+    grown = max(grown, free0 - torch.cuda.mem_get_info()[0])
+    # device memory the queue added (its two-stage workspaces, ~1.5 n^2 doubles per slot, at most
+    # two slots): recorded, and bounded well below what 16 unbounded slots would take
+    print("SpectrumQueue two-stage n = %d: device memory grew %.2f GB" % (n, grown / 2 ** 30))
+    assert grown < 2 * 1.6 * n * n * 8 + 2 ** 30, grown
     got = q.results()
     owned = [s for s in range(len(mats)) if q.owner(s) == 1]
     assert sorted(got) == owned and owned
