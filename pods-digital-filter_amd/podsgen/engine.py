@@ -303,12 +303,42 @@ class Generator:
         instead of 2.4 and cost the SYRK 2.7 ms, no net gain; spread over 64-256 workgroups they
         took 46-77 ms, each substream being a latency-bound twist chain.)"""
         # with the state exchange the owned substreams' records too (they need only the seed), and
-        # the all_to_all of the records, ordered behind them on the gen stream
+        # the all_to_all of the records, ordered behind them on the gen stream; after
+        # prefetch_jump_early only the records (the jump is already on the gen stream)
         parts = _lib.PODS_GEN_JUMP | (_lib.PODS_GEN_RECORD if self._xch is not None else 0)
-        self._on_gen_stream(parts, timer, "gen_jump_ahead")
+        if self._early:
+            self._on_gen_stream(_lib.PODS_GEN_RECORD, timer, "gen_jump_ahead")
+            self._ahead_parts |= _lib.PODS_GEN_JUMP
+            self._early = False
+        else:
+            self._on_gen_stream(parts, timer, "gen_jump_ahead")
         if self._xch is not None and self.dist is not None:
             with torch.cuda.stream(self.ctx.gen_stream()):
                 self._a2a = self.exchange_states(async_op=True)
+
+    _early = False   # the next run's jump-ahead enqueued by prefetch_jump_early
+
+    def prefetch_jump_early(self, timer=None):
+        """With the state exchange: enqueue the NEXT run's jump-ahead on the gen stream BEFORE this
+        run's generation (call it first in the step; the following prefetch_jump then adds only the
+        records and the all_to_all).  The jump needs the jump-state buffer only, which this run's
+        records (prefetched in the previous step) have consumed, so it runs beside this run's
+        planes and x / y-z passes instead of spilling into the correlation: at N = 8 the rank's
+        mean and residues (~0.7 ms) are shorter than the jump (~0.8 ms), and its 50 KB-LDS
+        workgroups then held CUs the persistent SYRK's one-per-CU grid waited for (corr +0.5 ms,
+        profiles/r5/rank_probe_c3_final.log).  Does nothing unless this run's jump and records
+        were prefetched (its generation would otherwise run them on the main stream)."""
+        if self._xch is None or self._early or not (self._ahead_parts & _lib.PODS_GEN_RECORD):
+            return
+        tm = timer or (lambda name: _NullCtx())
+        gs = self.ctx.gen_stream()
+        # behind everything the main stream holds (the previous step's persistent spectrum
+        # kernels must not find generator workgroups in the way, as join_ahead ensures)
+        gs.wait_stream(torch.cuda.current_stream(self.ctx.device))
+        with self.ctx.on_stream(gs):
+            with tm("gen_jump_early"):
+                check(self.ctx.lib.pods_df_generate_parts(self.ctx.h, _lib.PODS_GEN_JUMP), "pods_df_generate_parts")
+        self._early = True
 
     def prefetch_planes_beside_solver(self, timer=None):
         """Enqueue the NEXT run's random planes on the gen stream behind the marker the current
@@ -1266,6 +1296,8 @@ class ShardedSteps:
             check(ctx.lib.pods_df_set_seed(ctx.h, int(seed) & 0xffffffff), "pods_df_set_seed")
         bank = self.k % 2 if self.pipelined else 0
         check(ctx.lib.pods_select_snapshots(ctx.h, bank), "pods_select_snapshots")
+        if prefetch_next and os.environ.get("PODS_JUMP_EARLY", "1") != "0":
+            self.gen.prefetch_jump_early(timer)   # the next step's jump beside this generation
         with tm("generate"):
             snap = self.gen.generate()
         if prefetch_next:

@@ -211,6 +211,66 @@ def test_pipelined_steps_bit_equal_two_ranks_one_device():
     assert out[0][True]["fc"][0] is not None
 
 
+def _prefetch_worker(rank, world, port, out):
+    """Three steps of one seed through engine.ShardedSteps with the next step's MT jump-ahead
+    prefetched (bench.py's order), the jump enqueued before the generation (PODS_JUMP_EARLY, the
+    default) or after it, and without any prefetch."""
+    import torch
+    import torch.distributed as dist
+    import podsgen
+    from podsgen import engine as E
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    s = podsgen.DFSetup(jma=48, kma=40, ns=1024, seed=21)
+    res = {}
+    for name, early, ahead in (("early", "1", True), ("late", "0", True), ("none", "1", False)):
+        os.environ["PODS_JUMP_EARLY"] = early
+        gen = E.Generator(s, device=0, rank=rank, world=world, dist=dist)
+        assert gen._xch is not None   # the MT state exchange is on with several ranks
+        spectrum = E.SpectrumQueue(gen.ctx, s.ns, rank, world)
+        run = E.ShardedSteps(s, gen, dist, spectrum, E.FourierBacklog())
+        for k in range(3):
+            run.step(prefetch_next=ahead and k < 2)
+        run.flush()
+        spectrum.drain()
+        torch.cuda.synchronize()
+        res[name] = dict(T=[p.T.cpu().numpy() for p in run.results], phi=[p.phi.cpu().numpy() for p in run.results],
+                         mean=[p.mean.cpu().numpy() for p in run.results], spectra=spectrum.results())
+        gen.ctx.close()
+    os.environ.pop("PODS_JUMP_EARLY", None)
+    out[rank] = res
+    dist.destroy_process_group()
+
+
+def test_jump_prefetch_early_bit_equal_two_ranks_one_device():
+    """The next step's jump-ahead enqueued before this step's generation (beside its planes and
+    x / y-z passes; Generator.prefetch_jump_early), after it, or not prefetched at all: on 2 ranks
+    with the MT state exchange (gloo, one GPU), every step's mean, T, Phi and spectrum are equal
+    bit for bit -- and, one seed for all steps, equal from step to step."""
+    import multiprocessing as mp
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = 29300 + os.getpid() % 500
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_prefetch_worker, args=(r, 2, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(600)
+        assert p.exitcode == 0
+    for r in range(2):
+        ref = out[r]["none"]
+        for name in ("early", "late"):
+            got = out[r][name]
+            for key in ("T", "phi", "mean"):
+                for k in range(3):
+                    assert np.array_equal(got[key][k], ref[key][k]), (r, name, key, k)
+                    assert np.array_equal(ref[key][k], ref[key][0]), (r, key, k)
+            assert sorted(got["spectra"]) == sorted(ref["spectra"])
+            for k in got["spectra"]:
+                assert np.array_equal(got["spectra"][k], ref["spectra"][k]), (r, name, k)
+
+
 def test_sharded_pipeline_two_ranks_one_device():
     """Row slabs on 2 ranks (gloo transport, one GPU) == the single-rank pipeline."""
     import multiprocessing as mp

@@ -17,9 +17,10 @@ J, K, NS = (int(a) for a in sys.argv[1:4]) if len(sys.argv) > 3 else (256, 256, 
 WORLDS = [int(w) for w in sys.argv[4].split(",")] if len(sys.argv) > 4 else [1, 2, 4, 8]
 s = podsgen.DFSetup(jma=J, kma=K, ns=NS, seed=12345)
 ctx = E.Context(0)
-MODES = [("plain", False, False), ("prefetched", True, False), ("exchange", True, True)]
+MODES = [("plain", False, False, False), ("prefetched", True, False, False), ("exchange", True, True, False),
+         ("exchange+early jump", True, True, True)]
 for world in WORLDS:
-  for mode, ahead, xch in MODES:
+  for mode, ahead, xch, early in MODES:
     if xch and world == 1:
         continue
     gen = E.Generator(s, rank=0, world=world, ctx=ctx, exchange=False)
@@ -43,6 +44,8 @@ for world in WORLDS:
             tm = E.StageTimer()
             torch.cuda.synchronize()
             t = time.perf_counter()
+            if early and ahead and rep < reps - 1:
+                gen.prefetch_jump_early(tm)
             with tm("generate"):
                 gen.generate()
             if ahead and rep < reps - 1:
