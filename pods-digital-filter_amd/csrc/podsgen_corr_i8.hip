@@ -338,6 +338,99 @@ __device__ __forceinline__ void residues_body(const double* __restrict__ AT, int
   });
 }
 
+// 8 K elements per thread (r5, PODS_RES_I8=e, ns % 8 == 0; A/B): k_residues<8>'s arithmetic (the
+// mean through LDS, signed 14-bit limbs) with twice the threads at half the registers, so twice
+// the waves per SIMD hide the loads; a wave covers 8 snapshots of one K chunk, each thread stores
+// 8 bytes per modulus (a wave: 512 contiguous bytes).
+__global__ __launch_bounds__(256) void k_residues_e8(const double* __restrict__ AT, int ns, int64_t rowlen,
+                                                     int64_t rowpad, const double* __restrict__ mean,
+                                                     const double* __restrict__ devmax, int bbits, int64_t kc0,
+                                                     int64_t nkc, int8_t* __restrict__ R, int64_t ms, int64_t cs) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int q = (int)(t & 7);
+  const int64_t rest = t >> 3;
+  if (rest >= nkc * ns) return;
+  const int i = (int)(rest % ns);
+  const int64_t kcl = rest / ns;
+  const int64_t r0 = (kc0 + kcl) * 64 + q * 8;
+  extern __shared__ __attribute__((aligned(16))) char res_lds[];
+  double* M = reinterpret_cast<double*>(res_lds) + (threadIdx.x >> 6) * 64;
+  const int lane = threadIdx.x & 63;
+  const int64_t rm = (kc0 + kcl) * 64 + lane;
+  M[lane] = mean[rm < rowlen ? rm : rowlen - 1];
+  double a[8];
+  if (r0 < rowpad) {
+    const double2* src = reinterpret_cast<const double2*>(AT + ((((r0 >> 4) * ns) + i) << 4) + (r0 & 15));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const double2 v = src[e];
+      a[2 * e] = v.x;
+      a[2 * e + 1] = v.y;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const double2* mq = reinterpret_cast<const double2*>(M + q * 8);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const double2 mv = mq[e];
+      a[2 * e] = r0 + 2 * e < rowlen ? a[2 * e] - mv.x : 0.0;
+      a[2 * e + 1] = r0 + 2 * e + 1 < rowlen ? a[2 * e + 1] - mv.y : 0.0;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = 0.0;
+  }
+  const int sg = scale_exp(*devmax, bbits);
+  int8_t* const rb = R + kcl * cs + (uint32_t)(i * 64 + q * 8);
+  constexpr float MAG = 12582912.0f;
+  f32x2 F[4][4];
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) {
+    float d[4][2];
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const double ap = rint(ldexp(a[e + h2], sg));
+      const double hh = rint(ap * 0x1p-28);
+      const double lo = __builtin_fma(-hh, 0x1p28, ap);
+      const double d3 = rint(hh * 0x1p-14), d1 = rint(lo * 0x1p-14);
+      d[3][h2] = (float)d3;
+      d[2][h2] = (float)__builtin_fma(-d3, 0x1p14, hh);
+      d[1][h2] = (float)d1;
+      d[0][h2] = (float)__builtin_fma(-d1, 0x1p14, lo);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) F[k][e / 2] = (f32x2){d[k][0], d[k][1]};
+  }
+  sfor<0, NMOD>([&](auto L) {
+    constexpr int l = decltype(L)::value;
+    constexpr float m = (float)kT.m[l], inv = 1.0f / (float)kT.m[l];
+    constexpr float c1 = (float)kT.p14[l][1], c2 = (float)kT.p14[l][2], c3 = (float)kT.p14[l][3];
+    f32x2 sv[4], qv[4];
+#pragma unroll
+    for (int pr = 0; pr < 4; ++pr) sv[pr] = __builtin_elementwise_fma(F[1][pr], (f32x2){c1, c1}, F[0][pr]);
+#pragma unroll
+    for (int pr = 0; pr < 4; ++pr) sv[pr] = __builtin_elementwise_fma(F[2][pr], (f32x2){c2, c2}, sv[pr]);
+#pragma unroll
+    for (int pr = 0; pr < 4; ++pr) sv[pr] = __builtin_elementwise_fma(F[3][pr], (f32x2){c3, c3}, sv[pr]);
+#pragma unroll
+    for (int pr = 0; pr < 4; ++pr) qv[pr] = __builtin_elementwise_fma(sv[pr], (f32x2){inv, inv}, (f32x2){MAG, MAG});
+#pragma unroll
+    for (int pr = 0; pr < 4; ++pr) qv[pr] = qv[pr] - (f32x2){MAG, MAG};
+#pragma unroll
+    for (int pr = 0; pr < 4; ++pr) sv[pr] = __builtin_elementwise_fma(-qv[pr], (f32x2){m, m}, sv[pr]);
+#pragma unroll
+    for (int pr = 0; pr < 4; ++pr) sv[pr] = sv[pr] + (f32x2){MAG, MAG};
+    uint32_t w[2];
+#pragma unroll
+    for (int pq = 0; pq < 2; ++pq) {
+      const f32x2 u = sv[2 * pq], v = sv[2 * pq + 1];
+      const uint32_t h0 = __builtin_amdgcn_perm(__float_as_uint(u.y), __float_as_uint(u.x), 0x0C0C0400u);
+      const uint32_t h1 = __builtin_amdgcn_perm(__float_as_uint(v.y), __float_as_uint(v.x), 0x0C0C0400u);
+      w[pq] = h0 | (h1 << 16);
+    }
+    *reinterpret_cast<uint2*>(rb + (int64_t)l * ms) = make_uint2(w[0], w[1]);
+  });
+}
+
 #define PODS_RES_ARGS const double* __restrict__ AT, int ns, int64_t rowlen, int64_t rowpad, \
     const double* __restrict__ mean, const double* __restrict__ devmax, int bbits, int64_t kc0, int64_t nkc, \
     int8_t* __restrict__ R, int64_t ms, int64_t cs
@@ -1217,14 +1310,16 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
     const char* rv = std::getenv("PODS_RES_I8");
     const int64_t thr = p.chunks * ns * 4;
     const bool r8 = ns % 16 == 0 && !(rv && rv[0] && rv[0] != '8');
+    const bool e8 = rv && rv[0] == 'e' && ns % 8 == 0;
     const void* rk = r8                   ? reinterpret_cast<const void*>(&k_residues<8>)
                      : rv && rv[0] == '1' ? reinterpret_cast<const void*>(&k_residues<1>)
                      : rv && rv[0] == '2' ? reinterpret_cast<const void*>(&k_residues<2>)
                      : rv && rv[0] == '3' ? reinterpret_cast<const void*>(&k_residues<3>)
                      : rv && rv[0] == '7' && ns % 16 == 0 ? reinterpret_cast<const void*>(&k_residues<7>)
                                           : reinterpret_cast<const void*>(&k_residues<0>);
-    const unsigned rlds = r8 || (rv && rv[0] == '7' && ns % 16 == 0) ? 4 * 512 : 0;
-    const unsigned rgrid = (unsigned)((thr + 255) / 256);
+    const unsigned rlds = r8 || e8 || (rv && rv[0] == '7' && ns % 16 == 0) ? 4 * 512 : 0;
+    const unsigned rgrid = (unsigned)((thr * (e8 ? 2 : 1) + 255) / 256);
+    if (e8) rk = reinterpret_cast<const void*>(&k_residues_e8);
     {
       const double* AT_ = AT;
       const double* mean_ = mean;
