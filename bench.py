@@ -39,6 +39,8 @@ import numpy as np  # noqa: E402
 CONFIGS = {
     # name: (J, K, ns, description)
     "c1": (32, 32, 64, "32x32 inlet x 64 snapshots (BASELINE config 1)"),
+    "c2": (256, 256, 4096, "256x256 inlet x 4096 snapshots, fp64, digital-filter convolution + Lund transform "
+                           "only (BASELINE config 2)"),
     "c3": (256, 256, 4096, "256x256 inlet x 4096 snapshots, digital filter + full PODFS (BASELINE config 3)"),
     "c4": (512, 512, 8192, "512x512 inlet x 8192 snapshots (BASELINE config 4)"),
     # BASELINE config 5: 1024^2 inlet, anisotropic length scales (-t: lnx = 2 ln -> nfx = 12,
@@ -254,7 +256,129 @@ def metric_name(config):
     J, K, ns, _ = CONFIGS[config]
     if config == "c3":  # BASELINE.json's headline metric
         return "filtered-snapshot Mpoints/s (gen+PODFS), 256^2 inlet x 4096 steps, 1/2/4/8 GPU"
+    if config == "c2":
+        return "filtered-snapshot Mpoints/s (generation only: filter + Lund), 256^2 inlet x 4096 steps (c2)"
     return "filtered-snapshot Mpoints/s (gen+PODFS), %dx%d inlet x %d steps (%s)" % (J, K, ns, config)
+
+
+# Algorithmic HBM bytes per unit (one inlet point at one step, 3 fp64 components) of the generator
+# kernels at C2/C3: the random planes written once (3 S (ns + 2nfx) doubles), the x pass
+# reading them and writing T1 (3 S ns), the y/z pass reading T1 and writing A (3 P ns)
+def gen_bytes_per_unit(J, K, ns, nfx, nfy, nfz):
+    S = (J + 2 * nfy) * (K + 2 * nfz)
+    units = float(J * K * ns)
+    planes = 3.0 * S * (ns + 2 * nfx) * 8 / units
+    t1 = 3.0 * S * ns * 8 / units
+    return {"gen_planes": planes, "gen_xpass": planes + t1, "gen_yzpass": t1 + 24.0, "output": 24.0}
+
+
+def load_gen_traffic(config):
+    """Per-kernel L2-miss bytes per launch of the generator kernels (profiles/pmc_gen_<config>.json)."""
+    path = os.path.join(ROOT, "profiles", "pmc_gen_%s.json" % config)
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except Exception:
+        return None
+
+
+def bench_generation(args, E, gen, setup, world, rank, dist):
+    """BASELINE config 2: the digital filter + Lund transform only (digitalfilters.py:1403-1481 without
+    the POD).  A step is one whole generation of the 256^2 x 4096 snapshot matrix, every kernel on the
+    main stream -- the MT19937 jump-ahead, the random planes, the x pass, the y/z pass (+ Lund) -- each
+    bracketed by its own HIP-event pair, so the stage times are the kernels' times."""
+    import torch
+    J, K, ns = setup.jma, setup.kma, setup.ns
+    for _ in range(args.warmup):
+        gen.generate()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    tm = E.StageTimer()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        gen.generate(timer=tm if world == 1 else None)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    if rank != 0:
+        return
+    ms = elapsed / args.steps * 1e3
+    units = float(J * K * ns)
+    stages = {k: v / args.steps for k, v in tm.summary().items()}
+    bpu = gen_bytes_per_unit(J, K, ns, setup.nfx, setup.nfy, setup.nfz)
+    pmc = load_gen_traffic(args.config) if world == 1 else None
+    kern = {"gen_jump": "k_mt_jump3", "gen_planes": "k_mt_generate_full", "gen_xpass": "k_filter_x2",
+            "gen_yzpass": "k_filter_yz"}
+    per_kernel = {}
+    for st, kname in kern.items():
+        if st not in stages:
+            continue
+        row = {"kernel": kname, "ms": round(stages[st], 3)}
+        if st in bpu:
+            gbs = bpu[st] * units / (stages[st] * 1e-3) / 1e9
+            row.update(algorithmic_bytes_per_unit=round(bpu[st], 2), achieved_GBps=round(gbs, 1),
+                       frac=round(gbs / (HBM_PEAK_TBS * 1e3), 4))
+        if pmc:
+            for k, v in pmc.get("kernels", {}).items():
+                if kname in k:
+                    row["traffic"] = v["bytes"]
+        per_kernel[st] = row
+    yz = per_kernel.get("gen_yzpass")
+    gen_gbs = 24.0 * units / (ms * 1e-3) / 1e9
+    out = {
+        "metric": metric_name(args.config), "value": round(units / (ms * 1e-3) / 1e6, 3), "unit": "Mpoints/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (seeded MT19937 random field, built tanh/top-hat profile)",
+        "config": {"workload": CONFIGS[args.config][3], "jma": J, "kma": K, "ns": ns,
+                   "nf": [setup.nfx, setup.nfy, setup.nfz], "parallelism": "row-slab dp%d" % world},
+        "roofline": None if yz is None else {
+            "kernel": "k_filter_yz (y/z filter passes + Lund transform + rotation, K-tiled snapshot store)",
+            "bound": "hbm", "achieved": yz["achieved_GBps"], "peak": HBM_PEAK_TBS * 1e3, "unit": "GB/s",
+            "frac": yz["frac"], "traffic": yz.get("traffic"),
+            "algorithmic_bytes_per_launch": round(bpu["gen_yzpass"] * units), "launch_ms": yz["ms"]},
+        "generation_roofline": {
+            "note": "the whole step against its output: 24 B per unit (A written once) / ms_per_step / 8 TB/s",
+            "achieved_GBps": round(gen_gbs, 1), "frac": round(gen_gbs / (HBM_PEAK_TBS * 1e3), 4),
+            "floor_ms": round(24.0 * units / (HBM_PEAK_TBS * 1e12) * 1e3, 3),
+            "kernel_traffic_GB": None if not pmc else round(sum(r.get("traffic", 0.0) for r in per_kernel.values())
+                                                          / 1e9, 2),
+            "algorithmic_kernel_GB": round(sum(bpu[k] for k in ("gen_planes", "gen_xpass", "gen_yzpass")) * units
+                                           / 1e9, 2)},
+        "kernels": per_kernel,
+        "stages_ms": {k: round(v, 3) for k, v in stages.items()},
+        "stages_note": "per-step means of HIP-event pairs around each generation kernel, main stream",
+    }
+    if world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline_generation(J, K, ns, args.cpu_budget)
+    print(json.dumps(out), flush=True)
+
+
+def cpu_baseline_generation(J, K, ns, budget=20.0):
+    """The oracle's reference-faithful generation loop (scipy convolve x3, adapt1d, rotate) on its first
+    steps, x ns / steps (per-step cost is constant)."""
+    from oracle import pods_oracle as O  # only the cpu_baseline leg imports the oracle
+    cfg = O.DFConfig(jma=J, kma=K, ns=ns, seed=1)
+    t = time.perf_counter()
+    O.generate(cfg, loops=True, steps=2)
+    per = (time.perf_counter() - t) / 2
+    m = max(2, min(64, int(budget / max(per, 1e-9))))
+    t = time.perf_counter()
+    O.generate(cfg, loops=True, steps=m)
+    sec = (time.perf_counter() - t) / m * ns
+    return {"value": J * K * ns / sec / 1e6, "unit": "Mpoints/s", "cores": 1, "kind": "port",
+            "sample": "oracle generation (reference-faithful Python loops, one core): first %d of %d steps, x ns/%d"
+                      % (m, ns, m), "seconds_full_job": round(sec, 2)}
 
 
 def main():
@@ -301,6 +425,11 @@ def main():
         torch.cuda.synchronize()
     setup_ms["dft_twiddles"] = (time.perf_counter() - t_setup) * 1e3
     d = dist if world > 1 else None
+    if args.config == "c2":
+        bench_generation(args, E, gen, setup, world, rank, d)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     # several ranks: the nm leading eigenpairs on the critical path (subspace iteration), the
     # rest of the spectrum spread over the ranks' following steps (engine.SpectrumQueue)
     split = (world > 1 or os.environ.get("PODS_EIGEN") == "split") and ns >= E.SPLIT_MIN_N
@@ -401,9 +530,7 @@ def main():
         kern_ms = k_ms.value / k_n.value
         ops = 2.0 * CORR_NMOD * 3 * P_local * ns * (ns + 1) / 2
         achieved = ops / (kern_ms * 1e-3) / 1e12
-        paced = os.environ.get("PODS_SYRK_PACE", "") != "0"
-        roofline = {"kernel": "%s (pods_corr's %d residue SYRKs on int8 MFMA), rank 0"
-                              % ("k_syrk_i8_paced" if paced else "k_syrk_i8", CORR_NMOD),
+        roofline = {"kernel": "k_syrk_i8_paced (pods_corr's %d residue SYRKs on int8 MFMA), rank 0" % CORR_NMOD,
                     "bound": "mfma", "dtype": "i8", "achieved": round(achieved, 1), "peak": round(I8_MFMA_PEAK_TOPS, 1),
                     "unit": "TOP/s", "frac": round(achieved / I8_MFMA_PEAK_TOPS, 4), "traffic": traffic,
                     "launch_ms": round(kern_ms, 3), "ops_per_launch": ops, "launches": k_n.value,

@@ -121,8 +121,9 @@ int pods_df_generate_parts(pods_ctx* ctx, int parts);
  * buffer after the chunks of ranks < r); and
  * PODS_GEN_PLANES regenerates this rank's segments from the received states.  The planes are
  * bit-identical to the single-stream generation.  j0s / j1s: every rank's slab [j0, j1) (this
- * rank's must equal the configured one).  world <= 1 turns the exchange off; pods_df_configure
- * does too. */
+ * rank's must equal the configured one).  world <= 0 turns the exchange off, as pods_df_configure
+ * does; world == 1 runs it for one rank (its all_to_all the identity: a single-device check of
+ * the collective path). */
 int pods_df_set_exchange(pods_ctx* ctx, int world, int rank, const int* j0s, const int* j1s);
 int pods_df_exchange_sizes(pods_ctx* ctx, int64_t* send_bytes, int64_t* recv_bytes);
 int pods_df_exchange_bind(pods_ctx* ctx, void* send_dev, void* recv_dev);

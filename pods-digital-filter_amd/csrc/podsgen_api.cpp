@@ -326,11 +326,10 @@ struct pods_ctx {
     int ns = -1;
     int64_t rowlen = -1, rowpad = -1, budget = -1;
     int force = -1;
-    char order = 0;
-    int wide = 0;
+    char order = 0;  // PODS_CORR_ORDER (diagnostic library only)
     bool operator==(const I8Key& o) const {
       return ns == o.ns && rowlen == o.rowlen && rowpad == o.rowpad && budget == o.budget && force == o.force &&
-             order == o.order && wide == o.wide;
+             order == o.order;
     }
   } i8_key;
   pods::CorrI8Plan i8_plan{};
@@ -683,7 +682,9 @@ int pods_df_set_exchange(pods_ctx* c, int world, int rank, const int* j0s, const
   if (!c->configured) return fail(PODS_ERR_STATE, "pods_df_set_exchange before pods_df_configure");
   Exchange& X = c->xch;
   X.free_all();
-  if (world <= 1) return PODS_OK;
+  if (world <= 0) return PODS_OK;  // off
+  // world == 1 is allowed (its all_to_all is the identity): a one-rank job can run the exchange
+  // path, e.g. to exercise a collective backend on a single device (tests)
   const pods_df_params& p = c->p;
   if (rank < 0 || rank >= world || !j0s || !j1s) return fail(PODS_ERR_ARG, "pods_df_set_exchange: bad rank/slabs");
   if (j0s[rank] != p.j0 || j1s[rank] != p.j1)
@@ -1029,18 +1030,15 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
     const int64_t budget = (int64_t)((bud ? std::atof(bud) : 16.0) * (double)(1LL << 30));
     const char* fsp = std::getenv("PODS_CORR_SPLITS");  // tests: a fixed number of K splits
     const int force = fsp ? std::max(0, std::atoi(fsp)) : 0;
-    const char* ord = std::getenv("PODS_CORR_ORDER");
     pods_ctx::I8Key key;
     key.ns = ns;
     key.rowlen = c->rowlen;
     key.rowpad = c->rowpad;
     key.budget = budget;
     key.force = force;
-    key.order = ord ? ord[0] : 0;
-    // PODS_SYRK_WIDE=1: the persistent SYRK with 256 x 384 tiles (corr_i8_xcd_items_wide)
-    const char* wv = std::getenv("PODS_SYRK_WIDE");
-    const int wide = wv && wv[0] == '1' ? 1 : 0;
-    key.wide = wide;
+#ifdef PODS_DIAG
+    if (const char* ord = std::getenv("PODS_CORR_ORDER")) key.order = ord[0];
+#endif
     if (!(c->i8_key == key)) {
       if (pods::corr_i8_plan(ns, c->rowlen, c->rowpad, budget, &c->i8_plan, force) != 0)
         return fail(PODS_ERR_UNSUPPORTED, "pods_corr: K too large for the int8 correlation (PODS_CORR=f64)");
@@ -1048,8 +1046,7 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
       c->i8_plan.nitems = (int)(items.size() / 4);  // the order decides the (padded) item count
       PODS_HIP(ensure(c->i8_items, items.size() * sizeof(int)));
       PODS_HIP(hipMemcpy(c->i8_items.p, items.data(), items.size() * sizeof(int), hipMemcpyHostToDevice));
-      const std::vector<int> xit = wide ? pods::corr_i8_xcd_items_wide(ns, c->i8_plan, &c->i8_per_xcd)
-                                        : pods::corr_i8_xcd_items(items, c->i8_plan.nitems, &c->i8_per_xcd);
+      const std::vector<int> xit = pods::corr_i8_xcd_items(items, c->i8_plan.nitems, &c->i8_per_xcd);
       PODS_HIP(ensure(c->i8_xitems, xit.size() * sizeof(int)));
       PODS_HIP(hipMemcpy(c->i8_xitems.p, xit.data(), xit.size() * sizeof(int), hipMemcpyHostToDevice));
       PODS_HIP(ensure(c->i8_pace, 8 * 32 * sizeof(unsigned)));
@@ -1075,15 +1072,10 @@ int pods_corr(pods_ctx* c, double* C_dev, int divide) {
       e1 = c->corr_ev[c->corr_ev_used].second;
       ++c->corr_ev_used;
     }
-    // the persistent XCD-paced SYRK unless PODS_SYRK_PACE=0 ("p<N>": also every N K steps in a tile)
-    const char* pv = std::getenv("PODS_SYRK_PACE");
-    const bool paced = !(pv && pv[0] == '0');
-    const int every = pv && pv[0] == 'p' && pv[1] ? std::atoi(pv + 1) : 0;
     PODS_HIP(pods::launch_corr_i8(c->A.as<double>(), ns, c->rowlen, c->rowpad, mean, c->devmax.as<double>(),
                                   c->i8_plan, c->i8_items.as<int>(), c->i8_res.as<int8_t>(),
                                   c->i8_part.as<uint8_t>(), C_dev, ns, divide, c->stream, e0, e1,
-                                  paced ? c->i8_xitems.as<int>() : nullptr, c->i8_per_xcd,
-                                  paced ? c->i8_pace.as<unsigned>() : nullptr, every, paced ? wide : 0));
+                                  c->i8_xitems.as<int>(), c->i8_per_xcd, c->i8_pace.as<unsigned>()));
     return PODS_OK;
   }
   int64_t ksplit = 0;

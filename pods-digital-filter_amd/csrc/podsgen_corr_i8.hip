@@ -137,13 +137,14 @@ __global__ __launch_bounds__(256) void k_absdev(const double* __restrict__ AT, i
 // Thread (chunk kc, snapshot i, quarter q) converts the 16 rows r = 64 kc + 16 q + e of snapshot
 // i (one 128-B run of the K-tiled fp64 A) and writes 16 bytes per modulus at
 // R_l[kc][i][16 q ..]: a wave covers 16 snapshots x 64 rows = 1 KB contiguous per modulus.
-// V: 0 = unsigned 11-bit limbs, 1 = signed 14-bit limbs (two packed ops fewer per element pair
-// and modulus), 7 / 8 = 0 / 1 with the mean through LDS (ns % 16 == 0; 8 the default); 2 / 3:
-// measurement only.  r5 counters (profiles/r5/residues_pmc.json):
-// ~2,000 VALU instructions per wave (4 cycles each) make a ~3 ms VALU floor at C3 -- not the HBM
-// traffic, as r4 thought: without stores the kernel ran as long, without loads 3.1 ms -- and the
-// 16 per-lane mean loads of the r4 kernel, each behind its own branch and vmcnt(0), were two
-// thirds of its L1 accesses and most of its load stalls.
+// V: 0 = unsigned 11-bit limbs, the mean per lane (any ns); 8 = signed 14-bit limbs (two packed
+// ops fewer per element pair and modulus) with the wave's mean through LDS (ns % 16 == 0, the
+// default: 3.72 vs 4.37 ms at C3, profiles/r5/residues_ab.log).  r5 counters
+// (profiles/r5/residues_pmc.json): ~2,000 VALU instructions per wave (4 cycles each) make a ~3 ms
+// VALU floor at C3 -- not the HBM traffic, as r4 thought -- and the 16 per-lane mean loads of the
+// r4 kernel, each behind its own branch and vmcnt(0), were two thirds of its L1 accesses and most
+// of its load stalls.  (Measured and removed in r6 as A/B variants: signed limbs with per-lane
+// means, unsigned limbs with the LDS mean, 8 elements per thread at 52 VGPRs -- none faster.)
 template <int V>
 __device__ __forceinline__ void residues_body(const double* __restrict__ AT, int ns, int64_t rowlen,
                                               int64_t rowpad, const double* __restrict__ mean,
@@ -167,10 +168,7 @@ __device__ __forceinline__ void residues_body(const double* __restrict__ AT, int
 #pragma unroll
     for (int e = 0; e < 16; ++e) x[e] = r0 + e < rowlen ? x[e] - mv[e] : 0.0;
   };
-  if constexpr (V == 2) {  // measurement only (PODS_RES_I8=2): no A loads
-#pragma unroll
-    for (int e = 0; e < 16; ++e) a[e] = (double)(i + e) * 0.37 - (double)r0;
-  } else if constexpr (V == 7 || V == 8) {
+  if constexpr (V == 8) {
     // the mean through LDS (ns % 16 == 0: one K chunk per wave): one 8-B load per lane fetches
     // the wave's 64 mean values, instead of 16 per-lane loads of 4 distinct slices (two thirds of
     // the kernel's L1 accesses)
@@ -228,14 +226,10 @@ __device__ __forceinline__ void residues_body(const double* __restrict__ AT, int
       w[pq] = h0 | (h1 << 16);
     }
     int8_t* base = rb + (int64_t)l * ms;
-    if constexpr (V == 3) {  // measurement only (PODS_RES_I8=3): no residue stores
-      if ((w[0] ^ w[1] ^ w[2] ^ w[3]) == 0x9E3779B9u && ns < 0) *reinterpret_cast<uint4*>(base + doff) = make_uint4(w[0], w[1], w[2], w[3]);
-      return;
-    }
     *reinterpret_cast<uint4*>(base + doff) = make_uint4(w[0], w[1], w[2], w[3]);
   };
   constexpr float MAG = 12582912.0f;  // 1.5 * 2^23
-  if constexpr (V == 1 || V == 8) {
+  if constexpr (V == 8) {
     // a' as four SIGNED 14-bit limbs, split in fp64 (every step exact): h = rint(a' 2^-28),
     // lo = a' - h 2^28 (|lo| <= 2^27), d3 = rint(h 2^-14), d2 = h - d3 2^14, d1 = rint(lo 2^-14),
     // d0 = lo - d1 2^14: |d0|, |d1|, |d2| <= 2^13, |d3| <= 2^10.  Per modulus, with the balanced
@@ -338,99 +332,6 @@ __device__ __forceinline__ void residues_body(const double* __restrict__ AT, int
   });
 }
 
-// 8 K elements per thread (r5, PODS_RES_I8=e, ns % 8 == 0; A/B): k_residues<8>'s arithmetic (the
-// mean through LDS, signed 14-bit limbs) with twice the threads at half the registers, so twice
-// the waves per SIMD hide the loads; a wave covers 8 snapshots of one K chunk, each thread stores
-// 8 bytes per modulus (a wave: 512 contiguous bytes).
-__global__ __launch_bounds__(256) void k_residues_e8(const double* __restrict__ AT, int ns, int64_t rowlen,
-                                                     int64_t rowpad, const double* __restrict__ mean,
-                                                     const double* __restrict__ devmax, int bbits, int64_t kc0,
-                                                     int64_t nkc, int8_t* __restrict__ R, int64_t ms, int64_t cs) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int q = (int)(t & 7);
-  const int64_t rest = t >> 3;
-  if (rest >= nkc * ns) return;
-  const int i = (int)(rest % ns);
-  const int64_t kcl = rest / ns;
-  const int64_t r0 = (kc0 + kcl) * 64 + q * 8;
-  extern __shared__ __attribute__((aligned(16))) char res_lds[];
-  double* M = reinterpret_cast<double*>(res_lds) + (threadIdx.x >> 6) * 64;
-  const int lane = threadIdx.x & 63;
-  const int64_t rm = (kc0 + kcl) * 64 + lane;
-  M[lane] = mean[rm < rowlen ? rm : rowlen - 1];
-  double a[8];
-  if (r0 < rowpad) {
-    const double2* src = reinterpret_cast<const double2*>(AT + ((((r0 >> 4) * ns) + i) << 4) + (r0 & 15));
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const double2 v = src[e];
-      a[2 * e] = v.x;
-      a[2 * e + 1] = v.y;
-    }
-    __builtin_amdgcn_wave_barrier();
-    const double2* mq = reinterpret_cast<const double2*>(M + q * 8);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const double2 mv = mq[e];
-      a[2 * e] = r0 + 2 * e < rowlen ? a[2 * e] - mv.x : 0.0;
-      a[2 * e + 1] = r0 + 2 * e + 1 < rowlen ? a[2 * e + 1] - mv.y : 0.0;
-    }
-  } else {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) a[e] = 0.0;
-  }
-  const int sg = scale_exp(*devmax, bbits);
-  int8_t* const rb = R + kcl * cs + (uint32_t)(i * 64 + q * 8);
-  constexpr float MAG = 12582912.0f;
-  f32x2 F[4][4];
-#pragma unroll
-  for (int e = 0; e < 8; e += 2) {
-    float d[4][2];
-#pragma unroll
-    for (int h2 = 0; h2 < 2; ++h2) {
-      const double ap = rint(ldexp(a[e + h2], sg));
-      const double hh = rint(ap * 0x1p-28);
-      const double lo = __builtin_fma(-hh, 0x1p28, ap);
-      const double d3 = rint(hh * 0x1p-14), d1 = rint(lo * 0x1p-14);
-      d[3][h2] = (float)d3;
-      d[2][h2] = (float)__builtin_fma(-d3, 0x1p14, hh);
-      d[1][h2] = (float)d1;
-      d[0][h2] = (float)__builtin_fma(-d1, 0x1p14, lo);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) F[k][e / 2] = (f32x2){d[k][0], d[k][1]};
-  }
-  sfor<0, NMOD>([&](auto L) {
-    constexpr int l = decltype(L)::value;
-    constexpr float m = (float)kT.m[l], inv = 1.0f / (float)kT.m[l];
-    constexpr float c1 = (float)kT.p14[l][1], c2 = (float)kT.p14[l][2], c3 = (float)kT.p14[l][3];
-    f32x2 sv[4], qv[4];
-#pragma unroll
-    for (int pr = 0; pr < 4; ++pr) sv[pr] = __builtin_elementwise_fma(F[1][pr], (f32x2){c1, c1}, F[0][pr]);
-#pragma unroll
-    for (int pr = 0; pr < 4; ++pr) sv[pr] = __builtin_elementwise_fma(F[2][pr], (f32x2){c2, c2}, sv[pr]);
-#pragma unroll
-    for (int pr = 0; pr < 4; ++pr) sv[pr] = __builtin_elementwise_fma(F[3][pr], (f32x2){c3, c3}, sv[pr]);
-#pragma unroll
-    for (int pr = 0; pr < 4; ++pr) qv[pr] = __builtin_elementwise_fma(sv[pr], (f32x2){inv, inv}, (f32x2){MAG, MAG});
-#pragma unroll
-    for (int pr = 0; pr < 4; ++pr) qv[pr] = qv[pr] - (f32x2){MAG, MAG};
-#pragma unroll
-    for (int pr = 0; pr < 4; ++pr) sv[pr] = __builtin_elementwise_fma(-qv[pr], (f32x2){m, m}, sv[pr]);
-#pragma unroll
-    for (int pr = 0; pr < 4; ++pr) sv[pr] = sv[pr] + (f32x2){MAG, MAG};
-    uint32_t w[2];
-#pragma unroll
-    for (int pq = 0; pq < 2; ++pq) {
-      const f32x2 u = sv[2 * pq], v = sv[2 * pq + 1];
-      const uint32_t h0 = __builtin_amdgcn_perm(__float_as_uint(u.y), __float_as_uint(u.x), 0x0C0C0400u);
-      const uint32_t h1 = __builtin_amdgcn_perm(__float_as_uint(v.y), __float_as_uint(v.x), 0x0C0C0400u);
-      w[pq] = h0 | (h1 << 16);
-    }
-    *reinterpret_cast<uint2*>(rb + (int64_t)l * ms) = make_uint2(w[0], w[1]);
-  });
-}
-
 #define PODS_RES_ARGS const double* __restrict__ AT, int ns, int64_t rowlen, int64_t rowpad, \
     const double* __restrict__ mean, const double* __restrict__ devmax, int bbits, int64_t kc0, int64_t nkc, \
     int8_t* __restrict__ R, int64_t ms, int64_t cs
@@ -491,8 +392,7 @@ __device__ __forceinline__ void pace_xcd(unsigned* ctr, unsigned& epoch, unsigne
 template <int NST, int DIAG, bool SAME, int ILV, int LD = 0>
 __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int64_t cstride, int ns, int nt, int i0,
                                           int j0, int m, char* smem, uint8_t* __restrict__ dst, int ldp,
-                                          int accumulate, unsigned* pctr = nullptr, unsigned pslot = 0,
-                                          int pevery = 0, unsigned* pepoch = nullptr) {
+                                          int accumulate) {
   constexpr int STG = 2 * PANEL;
   constexpr int Q = SAME ? 2 : 4;  // DMA instructions per wave per stage
   // DMA lead in K steps beyond the one being read: NST - 2, or with LD = 1 NST - 1 (the slot of
@@ -619,8 +519,6 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int64
   for (; t + 1 < nt; t += 2) {
     step(t, a0, b0, a1, b1);
     step(t + 1, a1, b1, a0, b0);
-    // a pacing point of the persistent kernel (pevery even), between two K steps
-    if (pevery > 0 && (t + 2) % pevery == 0 && t + 2 < nt) pace_xcd(pctr, *pepoch, pslot);
   }
   if (t < nt) step(t, a0, b0, a1, b1);
   const int fr = lane & 15, fq = lane >> 4;
@@ -645,184 +543,10 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int64
       }
 }
 
-// A 256 x 384 tile of one modulus over one K split (r5): rows i0 .. i0+255, columns j0 .. j0+383,
-// strictly below the diagonal blocks (j0 + 384 <= i0, or the columns clamp at ns), so no idle waves
-// and no SAME panel.  40 KB of operands per K step for 384 MFMAs: 17 % fewer L2 -> LDS bytes per MAC
-// than the 256 x 256 tile (32 KB for 256).  8 waves as 2 x 4, each 128 x 96 = 8 x 6 blocks (192
-// accumulator registers).  Registers do not allow the 256-tile's double-buffered fragments, so the
-// B fragments come in three column groups of two through two 2-fragment buffers -- group g of step
-// t in buffer (3t + g) & 1, the next group read while the current group's 16 MFMAs run -- and the
-// A fragment of row a of step t + 1 is read right behind row a's last MFMA of step t.  4-stage ring
-// of 40 KB (X panel 16 KB, Y panel 24 KB), D = 2 steps of DMA lead, 5 pieces per wave per step,
-// one after each of the first five MFMA rows of group 0.
-template <int NST>
-__device__ __forceinline__ void syrk_tile_wide(const int8_t* __restrict__ base, int64_t cstride, int ns, int nt,
-                                               int i0, int j0, int m, char* smem, uint8_t* __restrict__ dst, int ldp,
-                                               int accumulate) {
-  constexpr int YP = 384 * KC;       // the column panel: 24 KB
-  constexpr int STG = PANEL + YP;    // 40 KB per stage
-  constexpr int Q = 5;               // DMA pieces per wave per stage (2 X + 3 Y)
-  constexpr int D = NST - 2;
-  static_assert(NST * STG <= 160 * 1024, "LDS");
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // a piece is 16 rows x 64 B: its row block is wave-uniform (a scalar base) and every lane's
-  // offset in it the same for all pieces (the swizzle of row R depends on (R >> 2) & 3 only,
-  // i.e. on lane >> 4 here), so one 32-bit VGPR addresses all five.  No clamp at ns: the rows past
-  // ns only feed outputs past ns, which are not stored, and the residue buffer is padded
-  // (CORR_I8_RPAD) so the last row block reads inside the allocation.
-  // The DMA goes through buffer_load ... lds (MUBUF), not global_load_lds: the compiler's wait-count
-  // pass takes a pending global_load_lds for a FLAT access that may complete out of order with
-  // the LDS reads, and then waits lgkmcnt(0) before every MFMA whose fragment read is younger
-  // than that DMA -- an exposed LDS latency per column group (measured 30 % slower).  The
-  // buffer's range (the split's K chunks) also bounds the reads past ns: 0 comes back.
-  // (every operand of the buffer instruction wave-uniform by construction, or the compiler wraps
-  // it in a readfirstlane loop)
-  i0 = __builtin_amdgcn_readfirstlane(i0);
-  j0 = __builtin_amdgcn_readfirstlane(j0);
-  const uint64_t bu = (uint64_t)(uintptr_t)base;
-  const int8_t* ubase = (const int8_t*)(uintptr_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(bu >> 32)) << 32) |
-                                                   (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bu));
-  // (integer arithmetic only: HIP's min over int64 went through f64 on the VALU, and a VGPR
-  // range word made every DMA a readfirstlane loop)
-  const int64_t nbytes = (int64_t)nt * cstride;
-  const int nrec = __builtin_amdgcn_readfirstlane(nbytes >= 0xFFFFFFFFll ? (int)0xFFFFFFFFu : (int)(uint32_t)nbytes);
-  const int cst = __builtin_amdgcn_readfirstlane((int)cstride);
-  const uint32_t lo = (uint32_t)((lane >> 2) * KC + (((lane & 3) ^ swz((lane >> 4) & 3)) * 16));
-
-  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
-  auto piece = [&](int t, int q) {
-    const uint32_t sb = lds0 + (uint32_t)((t % NST) * STG) + (q < 2 ? (wave * 2 + q) * 1024 : PANEL + (wave * 3 + q - 2) * 1024);
-    const int rb = q < 2 ? i0 + (wave * 2 + q) * 16 : j0 + (wave * 3 + q - 2) * 16;
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(ubase), 0, nrec, 0x00020000);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(uintptr_t)sb, 16, (int)lo,
-                                             t * cst + rb * KC, 0, 0);
-  };
-  i32x4 acc[8][6];
-#pragma unroll
-  for (int a = 0; a < 8; ++a)
-#pragma unroll
-    for (int b = 0; b < 6; ++b) acc[a][b] = (i32x4){0, 0, 0, 0};
-  const int wr = wave >> 2, wc = wave & 3;
-  const int fo = (lane & 15) * KC + (((lane >> 4) ^ swz((lane >> 2) & 3)) * 16);
-  auto rdA = [&](int t, int a) -> i32x4 {
-    return *reinterpret_cast<const i32x4*>(smem + (t % NST) * STG + (wr * 128 + a * 16) * KC + fo);
-  };
-  auto rdB = [&](int t, int b) -> i32x4 {
-    return *reinterpret_cast<const i32x4*>(smem + (t % NST) * STG + PANEL + (wc * 96 + b * 16) * KC + fo);
-  };
-  i32x4 av[8], bb[2][2];
-  // The K loop is branch-free so the compiler's wait counts stay exact across it: the DMA of a
-  // step past the end re-loads the last chunk into its own slot (the same bytes: a benign
-  // overwrite), the reads past the end read a stale slot (unused), and the mod-m folds sit between
-  // K loops of FOLD steps.
-#pragma unroll
-  for (int t = 0; t <= D; ++t) {
-    const int tc = min(t, nt - 1);
-#pragma unroll
-    for (int q = 0; q < Q; ++q) piece(tc, q);  // (the slot of min(t, nt-1): a repeat writes the same bytes)
-  }
-  wait_vm<Q * D>();
-  // retire every scalar load still pending (kernel arguments the epilogue needs): an SMEM load
-  // completes out of order with the LDS reads on the same counter, so while one is pending the
-  // compiler can only wait for lgkmcnt(0) before an MFMA whose fragments are in flight
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int a = 0; a < 8; ++a) av[a] = rdA(0, a);
-  bb[0][0] = rdB(0, 0);
-  bb[0][1] = rdB(0, 1);
-  // step t of parity P: groups 0, 1, 2 in buffers P, P^1, P
-  auto step = [&](int t, auto PC) {
-    constexpr int P = decltype(PC)::value;
-    wait_vm<Q * (D - 1)>();
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    const int dt = min(t + D + 1, nt - 1);
-    // group 0 (buffer P); group 1's fragments into buffer P^1
-#pragma unroll
-    for (int a = 0; a < 8; ++a) {
-#pragma unroll
-      for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[a], bb[P][b], acc[a][b], 0, 0, 0);
-      if (a == 1) {  // (behind the first row: the DMA pieces follow rows 0-4)
-        __builtin_amdgcn_sched_barrier(0);
-        bb[P ^ 1][0] = rdB(t, 2);
-        bb[P ^ 1][1] = rdB(t, 3);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (a < Q) {
-        __builtin_amdgcn_sched_barrier(0);
-        piece(dt, a);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // group 1 (buffer P^1); group 2's fragments into buffer P
-    bb[P][0] = rdB(t, 4);
-    bb[P][1] = rdB(t, 5);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-        acc[a][2 + b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[a], bb[P ^ 1][b], acc[a][2 + b], 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    // group 2 (buffer P); step t+1's group 0 into buffer P^1, its A rows behind each row
-    bb[P ^ 1][0] = rdB(t + 1, 0);
-    bb[P ^ 1][1] = rdB(t + 1, 1);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int a = 0; a < 8; ++a) {
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-        acc[a][4 + b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[a], bb[P][b], acc[a][4 + b], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      av[a] = rdA(t + 1, a);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  // |acc| stays < m + FOLD * 64 * 127^2 < 2^31 between the folds
-  static_assert(FOLD % 2 == 0, "fold");
-  int t = 0;
-  for (int tf = 0; tf < nt; tf += FOLD) {
-    const int te = min(tf + FOLD, nt);
-    for (; t + 1 < te; t += 2) {
-      step(t, std::integral_constant<int, 0>{});
-      step(t + 1, std::integral_constant<int, 1>{});
-    }
-    if (te < nt) {
-#pragma unroll
-      for (int a = 0; a < 8; ++a)
-#pragma unroll
-        for (int b = 0; b < 6; ++b)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[a][b][r] %= m;
-    }
-  }
-  if (t < nt) step(t, std::integral_constant<int, 0>{});
-  const int fr = lane & 15, fq = lane >> 4;
-#pragma unroll
-  for (int a = 0; a < 8; ++a)
-#pragma unroll
-    for (int b = 0; b < 6; ++b)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gi = i0 + wr * 128 + a * 16 + 4 * fq + r;
-        const int gj = j0 + wc * 96 + b * 16 + fr;
-        if (gi < ns && gj <= gi) {
-          int v = acc[a][b][r] % m;
-          if (v < 0) v += m;
-          uint8_t* p = dst + (int64_t)gi * ldp + gj;
-          if (accumulate) {
-            v += *p;
-            if (v >= m) v -= m;
-          }
-          *p = (uint8_t)v;
-        }
-      }
-}
-
+#ifdef PODS_DIAG
+// The launch-per-item grid form (r4; the persistent kernel replaced it in r5) and its
+// measurement-only variants (DIAG: wrong results): the diagnostic library only (tools/lib_variants.sh
+// diag), never libpodsgen.so.
 template <int NST, int DIAG = 0, int ILV = 0>
 __global__ __launch_bounds__(512, 1) void k_syrk_i8(const int8_t* __restrict__ R, int ns, int64_t ms, int64_t cs,
                                                     int kcs,
@@ -848,20 +572,22 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8(const int8_t* __restrict__ R
     syrk_tile<NST, DIAG, false, ILV>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
 }
 
+#endif  // PODS_DIAG
+
 // The persistent, XCD-paced form (r5): one 512-thread workgroup per CU, workgroup b on XCD b % 8
 // (dispatch deals blocks round-robin over the XCDs) as slot b / 8 of nslot.  XCD x's items (its
 // share of every modulus' lower tiles and K splits, host-ordered so that one round -- nslot
 // consecutive items -- is a compact block of tiles of one modulus and split) are taken in rounds,
-// slot s taking item r * nslot + s of round r, with a soft pacing point after every round and,
-// with pace_every > 0, every pace_every K steps inside a tile: the workgroups that share an L2
-// then stream the same K window of the same panels (the launch-per-item form let them drift apart
-// over the 17 rounds at C3, and the XCD's 4 MB L2 held the union of their windows: 54 % hits).
-template <int NST, int ILV, bool MID, bool WIDE = false, int LD = 0>
+// slot s taking item r * nslot + s of round r, with a soft pacing point after every round: the
+// workgroups that share an L2 then stream the same K window of the same panels (the
+// launch-per-item form let them drift apart over the 17 rounds at C3, and the XCD's 4 MB L2 held
+// the union of their windows: 54 % hits).  5-stage ring, the DMA pieces among the first MFMA rows
+// (ILV 1), one more stage in flight (LD 1).
+template <int NST, int ILV, int LD>
 __global__ __launch_bounds__(512, 1) void k_syrk_i8_paced(const int8_t* __restrict__ R, int ns, int64_t ms, int64_t cs,
                                                           int kcs, const int4* __restrict__ xitems, int per_xcd,
                                                           int nsplit, uint8_t* __restrict__ P, int64_t pslab, int ldp,
-                                                          int accumulate, unsigned* __restrict__ pace_ctr,
-                                                          int pace_every) {
+                                                          int accumulate, unsigned* __restrict__ pace_ctr) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int x = blockIdx.x & 7, slot = blockIdx.x >> 3;
   unsigned* const ctr = pace_ctr + x * 32;  // one 128-B line per XCD
@@ -877,16 +603,10 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8_paced(const int8_t* __restri
       const int8_t* base = R + (int64_t)l * ms + (int64_t)sp * kcs * cs;
       uint8_t* dst = P + (int64_t)(l * nsplit + sp) * pslab;
       const int m = modulus(l);
-      if (WIDE && bj >= 0x10000)
-        syrk_tile_wide<4>(base, cs, ns, kcs, bi * TB, (bj & 0xffff) * 128, m, smem, dst, ldp, accumulate);
-      else if (bi == bj)
-        syrk_tile<NST, 0, true, ILV, LD>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate, ctr,
-                                         nslot, MID ? pace_every : 0, &epoch);
+      if (bi == bj)
+        syrk_tile<NST, 0, true, ILV, LD>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
       else
-        syrk_tile<NST, 0, false, ILV, LD>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate, ctr,
-                                          nslot, MID ? pace_every : 0, &epoch);
-    } else if (MID && pace_every > 0) {  // an empty slot still keeps the tile's pacing points
-      for (int t = pace_every; t < kcs; t += pace_every) pace_xcd(ctr, epoch, nslot);
+        syrk_tile<NST, 0, false, ILV, LD>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
     }
     pace_xcd(ctr, epoch, nslot);
   }
@@ -1077,60 +797,40 @@ std::vector<int> corr_i8_items(int ns, const CorrI8Plan& p) {
     }
   std::sort(t.begin(), t.end());
   const int tiles = (int)t.size(), per = (tiles + 7) / 8;
-  // PODS_CORR_ORDER (A/B runs): "m" = plain Morton order, no XCD groups; "x" = plain Morton order
-  // with every XCD given a contiguous range of the whole grid (kernel-side remap)
-  const char* ord = std::getenv("PODS_CORR_ORDER");
-  if (!ord || ord[0] == 'g') {
-    // default: XCD lane x (grid position 8k + x; nitems is a multiple of 8) takes split x % S
-    // and Morton group x / S of the 8 / S groups, so an XCD's concurrent workgroups all read one
-    // K range of one modulus, on a compact block of tiles (S in {1, 2, 4, 8})
-    if (8 % p.nsplit == 0) {
-      const int ngrp = 8 / p.nsplit, gsz = (tiles + ngrp - 1) / ngrp;
-      std::vector<int> out;
-      out.reserve((size_t)8 * gsz * 4);
-      for (int k = 0; k < gsz; ++k)
-        for (int x = 0; x < 8; ++x) {
-          const int sp = x % p.nsplit, grp = x / p.nsplit, idx = grp * gsz + k;
-          if (idx < tiles && k < gsz) {
-            out.push_back(t[idx].second.first);
-            out.push_back(t[idx].second.second);
-          } else {
-            out.push_back(-1);
-            out.push_back(-1);
-          }
-          out.push_back(sp);
-          out.push_back(0);
-        }
-      return out;
-    }
-  }
-  if (ord && ord[0] == 's') {  // measurement only (wrong results): every item is tile (1, 0)
+  // XCD lane x (grid position 8k + x; nitems is a multiple of 8) takes split x % S and Morton group
+  // x / S of the 8 / S groups, so an XCD's concurrent workgroups all read one K range of one
+  // modulus, on a compact block of tiles (S in {1, 2, 4, 8}; L2-miss traffic 96.9 -> 65.0 GB per
+  // launch against interleaved Morton groups, r4).  (Measured and removed in r6 as A/B orders: plain
+  // Morton, XCD-contiguous ranges of it -- 0.3-0.7 ms slower.)
+#ifdef PODS_DIAG
+  if (const char* ord = std::getenv("PODS_CORR_ORDER"); ord && ord[0] == 's') {
+    // measurement only (wrong results): every item is tile (1, 0)
     std::vector<int> out;
     for (int s = 0; s < p.nsplit; ++s)
-      for (int k = 0; k < per * 8; ++k) {
-        out.push_back(nb > 1 ? 1 : 0);
-        out.push_back(0);
-        out.push_back(s);
-        out.push_back(0);
-      }
+      for (int k = 0; k < per * 8; ++k) out.insert(out.end(), {nb > 1 ? 1 : 0, 0, s, 0});
     return out;
   }
-  if (ord && (ord[0] == 'm' || ord[0] == 'x')) {
+#endif
+  if (8 % p.nsplit == 0) {
+    const int ngrp = 8 / p.nsplit, gsz = (tiles + ngrp - 1) / ngrp;
     std::vector<int> out;
-    for (int s = 0; s < p.nsplit; ++s)
-      for (int k = 0; k < per * 8; ++k) {
-        if (k < tiles) {
-          out.push_back(t[k].second.first);
-          out.push_back(t[k].second.second);
+    out.reserve((size_t)8 * gsz * 4);
+    for (int k = 0; k < gsz; ++k)
+      for (int x = 0; x < 8; ++x) {
+        const int sp = x % p.nsplit, grp = x / p.nsplit, idx = grp * gsz + k;
+        if (idx < tiles) {
+          out.push_back(t[idx].second.first);
+          out.push_back(t[idx].second.second);
         } else {
           out.push_back(-1);
           out.push_back(-1);
         }
-        out.push_back(s);
+        out.push_back(sp);
         out.push_back(0);
       }
     return out;
   }
+  // other split counts (a forced PODS_CORR_SPLITS): split-major, Morton groups interleaved over XCDs
   std::vector<int> out;
   out.reserve((size_t)p.nitems * 4);
   for (int s = 0; s < p.nsplit; ++s)
@@ -1178,97 +878,12 @@ std::vector<int> corr_i8_xcd_items(const std::vector<int>& items, int nitems, in
   return out;
 }
 
-// The 256 x 384 table: per row block bi, its diagonal 256 tile, and the 2 bi 128-column units left
-// of it as 256 x 384 tiles from column 0, with one or two 256 tiles next to the diagonal when 2 bi
-// mod 3 leaves 2 or 1 units (2 bi = 1 mod 3 only for bi >= 2).  The same MACs as the 256-tile
-// grid, 13.7 % fewer operand bytes at ns = 4096 (3,536 vs 4,096 KB per K step and modulus).  The
-// tiles in Morton order of (row, column start) are cut into 8 / S compact groups of equal cost
-// (MFMA rows: 1.5 for a wide tile, 1 for a 256 tile, 0.75 for a diagonal one); XCD x takes split x
-// mod S and group x / S, its items ordered wide tiles first, then 256 tiles, then diagonal ones
-// (each kind modulus by modulus), so a round of nslot items is one kind of one modulus.
-std::vector<int> corr_i8_xcd_items_wide(int ns, const CorrI8Plan& p, int* per_xcd) {
-  struct T {
-    uint64_t key;
-    int bi, code, kind;  // kind 0 wide, 1 square, 2 diagonal
-  };
-  std::vector<T> t;
-  const int nb = (ns + i8::TB - 1) / i8::TB;
-  auto morton = [](uint32_t r, uint32_t c) {
-    uint64_t k = 0;
-    for (int b = 0; b < 20; ++b) k |= ((uint64_t)((r >> b) & 1u) << (2 * b + 1)) | ((uint64_t)((c >> b) & 1u) << (2 * b));
-    return k;
-  };
-  for (int bi = 0; bi < nb; ++bi) {
-    const int u = 2 * bi, r = u % 3;
-    const int nsq = r == 0 ? 0 : (r == 2 ? 1 : 2);
-    const int nw = (u - 2 * nsq) / 3;
-    for (int w = 0; w < nw; ++w) t.push_back({morton(2 * bi, 3 * w), bi, 0x10000 | (3 * w), 0});
-    for (int q = 0; q < nsq; ++q) t.push_back({morton(2 * bi, 2 * (bi - 1 - q)), bi, bi - 1 - q, 1});
-    t.push_back({morton(2 * bi, 2 * bi), bi, bi, 2});
-  }
-  std::stable_sort(t.begin(), t.end(), [](const T& a, const T& b) { return a.key < b.key; });
-  static const double cost[3] = {1.5, 1.0, 0.75};
-  double total = 0.0;
-  for (const T& x : t) total += cost[x.kind];
-  const int S = (8 % p.nsplit == 0) ? p.nsplit : 1;
-  const int ngrp = 8 / S;
-  std::vector<int> grp(t.size());
-  double run = 0.0;
-  for (size_t k = 0; k < t.size(); ++k) {
-    grp[k] = std::min(ngrp - 1, (int)((run + 0.5 * cost[t[k].kind]) * ngrp / total));
-    run += cost[t[k].kind];
-  }
-  std::vector<std::vector<int>> per(8);
-  for (int x = 0; x < 8; ++x)
-    for (int sp = x % S; sp < p.nsplit; sp += S)  // S = 1 when 8 % nsplit != 0: every split on every XCD
-      for (int kind = 0; kind < 3; ++kind)
-        for (int l = 0; l < i8::NMOD; ++l)
-          for (size_t k = 0; k < t.size(); ++k)
-            if (grp[k] == x / S && t[k].kind == kind) per[x].insert(per[x].end(), {t[k].bi, t[k].code, sp, l});
-  int px = 0;
-  for (int x = 0; x < 8; ++x) px = std::max(px, (int)per[x].size() / 4);
-  std::vector<int> out((size_t)8 * px * 4, -1);
-  for (int x = 0; x < 8; ++x) std::copy(per[x].begin(), per[x].end(), out.begin() + (size_t)x * px * 4);
-  *per_xcd = px;
-  return out;
-}
-
 hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowpad, const double* mean,
                           const double* devmax, const CorrI8Plan& p, const int* items, int8_t* R, uint8_t* P,
                           double* C, int64_t ldc, int divide, hipStream_t st, hipEvent_t syrk_begin,
-                          hipEvent_t syrk_end, const int* xitems, int per_xcd, unsigned* pace_ctr, int pace_every,
-                          int wide) {
+                          hipEvent_t syrk_end, const int* xitems, int per_xcd, unsigned* pace_ctr) {
   using namespace i8;
-  // default: 5 ring stages, each wave's DMA pieces one after each of its first MFMA rows (ILV 1;
-  // 22.0-22.8 ms at C3 against 24.0 for the pieces back to back after the barrier,
-  // profiles/r4/corr_i8_ilv_ab.log).  PODS_SYRK_I8 (A/B runs): "4" / "5" ring stages with the
-  // pieces after the barrier; "i1" / "i2" / "i4": 4 stages, ILV 1 / 2 / 4; "i6" / "i7": 5 stages,
-  // ILV 2 / 4; "9m" / "9d" / "9w" / "9x" / "9y": measurement only (wrong results): no MFMAs / no
-  // operand traffic / an L2-resident K window / both / the window with ILV 1
-  int variant = 45;
-  if (const char* v = std::getenv("PODS_SYRK_I8")) {
-    if (v[0] == '4') variant = 4;
-    if (v[0] == '5') variant = 5;
-    if (v[0] == 'i') variant = 40 + (v[1] ? v[1] - '0' : 1);
-    if (v[0] == '9') variant = v[1] == 'm' ? 91 : v[1] == 'w' ? 93 : v[1] == 'x' ? 94 : v[1] == 'y' ? 95 : v[1] == 'b' ? 96 : 92;
-  }
-  const void* fn = variant == 5 ? reinterpret_cast<const void*>(&k_syrk_i8<5>)
-                 : variant == 91 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 1>)
-                 : variant == 92 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 2>)
-                 : variant == 93 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 3>)
-                 : variant == 94 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 4>)
-                 : variant == 41 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 0, 1>)
-                 : variant == 42 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 0, 2>)
-                 : variant == 44 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 0, 4>)
-                 : variant == 95 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 3, 1>)
-                 : variant == 96 ? reinterpret_cast<const void*>(&k_syrk_i8<5, 5, 1>)
-                 : variant == 45 ? reinterpret_cast<const void*>(&k_syrk_i8<5, 0, 1>)
-                 : variant == 46 ? reinterpret_cast<const void*>(&k_syrk_i8<5, 0, 2>)
-                 : variant == 47 ? reinterpret_cast<const void*>(&k_syrk_i8<5, 0, 4>)
-                                 : reinterpret_cast<const void*>(&k_syrk_i8<4>);
-  const size_t lds = (size_t)(variant == 5 || (variant >= 45 && variant <= 47) || variant == 96 ? 5 : 4) * 2 * PANEL;
-  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) return e;
+  if (!xitems || !pace_ctr) return hipErrorInvalidValue;
   // residue layout: modulus l's K chunk kc at R + l * ms + kc * cs, one matrix per modulus
   // ([NMOD][chunks][ns][64]); the moduli interleaved per chunk ([chunks][NMOD][ns][64], a residue
   // wave's 16 stores in one window) measured no faster (r5, profiles/r5/residue_layout_ab.log)
@@ -1276,50 +891,53 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
   const int64_t cs = (int64_t)ns * KC;
   const int ldp = (ns + 63) / 64 * 64;
   const int64_t pslab = (int64_t)ns * ldp;
-  // default (r5): the persistent XCD-paced kernel (k_syrk_i8_paced: 22.34 vs 22.89 ms at C3 for
-  // the launch-per-item grid, profiles/r5/pace_ab.log) when the caller passes the per-XCD item
-  // table; pace_every > 0 adds pacing points inside a tile (measured no better: 22.54 at 256 K
-  // steps, 22.59 at 96).  PODS_SYRK_PACE=0 (A/B) or no table: the grid form below
-  const bool paced = xitems != nullptr && pace_ctr != nullptr;
-  int nslot = 0;
-  if (paced) {
-    int dev = 0, cus = 0;
-    e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e != hipSuccess) return e;
-    nslot = std::max(1, cus / 8);
-    for (const void* f : {reinterpret_cast<const void*>(&k_syrk_i8_paced<5, 1, false>),
-                          reinterpret_cast<const void*>(&k_syrk_i8_paced<5, 1, true>),
-                          reinterpret_cast<const void*>(&k_syrk_i8_paced<5, 1, false, true>),
-                          reinterpret_cast<const void*>(&k_syrk_i8_paced<5, 1, false, false, 1>)}) {
-      e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(5 * 2 * PANEL));
-      if (e != hipSuccess) return e;
-    }
+  int dev = 0, cus = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) return e;
+  const int nslot = std::max(1, cus / 8);
+  // The SYRK: the persistent XCD-paced kernel (k_syrk_i8_paced: 22.34 vs 22.89 ms at C3 for the
+  // r4 launch-per-item grid, profiles/r5/pace_ab.log), 5 ring stages, each wave's DMA pieces one
+  // after each of its first MFMA rows (ILV 1: 22.0-22.8 ms against 24.0 for the pieces back to back
+  // after the barrier, profiles/r4/corr_i8_ilv_ab.log), one more stage in flight (LD 1: 21.89 vs
+  // 22.12 ms, profiles/r5/syrk_lead_wide_ab.log).  (A/B variants measured equal or slower and
+  // removed in r6: 4 stages, ILV 2 / 4, the r4 lead, 256 x 384 tiles, pacing points inside a tile.)
+  const void* syrk = reinterpret_cast<const void*>(&k_syrk_i8_paced<5, 1, 1>);
+#ifdef PODS_DIAG
+  // the diagnostic library only (tools/lib_variants.sh diag): PODS_SYRK_I8 selects the r4 grid form
+  // "g", or its measurement-only variants (wrong results) "9m" / "9d" / "9w" / "9x" / "9y" / "9b":
+  // no MFMAs / no operand traffic / an L2-resident K window / both / the window with ILV 1 / no
+  // per-step barrier
+  int variant = 0;
+  if (const char* v = std::getenv("PODS_SYRK_I8")) {
+    if (v[0] == 'g') variant = 45;
+    if (v[0] == '9') variant = v[1] == 'm' ? 91 : v[1] == 'w' ? 93 : v[1] == 'x' ? 94 : v[1] == 'y' ? 95 : v[1] == 'b' ? 96 : 92;
   }
+  const void* grid_fn = variant == 91 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 1>)
+                      : variant == 92 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 2>)
+                      : variant == 93 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 3>)
+                      : variant == 94 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 4>)
+                      : variant == 95 ? reinterpret_cast<const void*>(&k_syrk_i8<4, 3, 1>)
+                      : variant == 96 ? reinterpret_cast<const void*>(&k_syrk_i8<5, 5, 1>)
+                      : variant == 45 ? reinterpret_cast<const void*>(&k_syrk_i8<5, 0, 1>)
+                                      : nullptr;
+  const size_t grid_lds = (size_t)(variant == 45 || variant == 96 ? 5 : 4) * 2 * PANEL;
+  if (grid_fn) {
+    e = hipFuncSetAttribute(grid_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)grid_lds);
+    if (e != hipSuccess) return e;
+  }
+#endif
+  e = hipFuncSetAttribute(syrk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(5 * 2 * PANEL));
+  if (e != hipSuccess) return e;
   if (syrk_begin && p.nlaunch > 1) e = hipEventRecord(syrk_begin, st);
   if (e != hipSuccess) return e;
   for (int li = 0; li < p.nlaunch; ++li) {
     const int64_t kc0 = (int64_t)li * p.chunks;
-    // default (r5), ns % 16 == 0: k_residues<8> -- the wave's 64 mean values through LDS and the
-    // signed 14-bit limbs, 3.72 vs 4.37 ms at C3 (profiles/r5/residues_ab.log); otherwise <0>.
-    // PODS_RES_I8 (A/B runs): 0 / 1 the r4 kernel (unsigned 11-bit / signed 14-bit limbs), 7 the
-    // LDS mean with unsigned limbs (3.83); 2 / 3 measurement only (no loads / no stores: 3.1 / 4.5
-    // ms, the kernel is VALU-bound at ~3 ms plus its load stalls).  Measured slower and removed
-    // (DESIGN.md s3): record loads coalesced through an LDS transpose, software-pipelined
-    // grid-stride forms prefetching the next record (and its mean)
-    const char* rv = std::getenv("PODS_RES_I8");
+    // residues: k_residues<8> (the wave's 64 mean values through LDS, signed 14-bit limbs) when
+    // ns % 16 == 0 (a wave then covers one K chunk), else k_residues<0>
     const int64_t thr = p.chunks * ns * 4;
-    const bool r8 = ns % 16 == 0 && !(rv && rv[0] && rv[0] != '8');
-    const bool e8 = rv && rv[0] == 'e' && ns % 8 == 0;
-    const void* rk = r8                   ? reinterpret_cast<const void*>(&k_residues<8>)
-                     : rv && rv[0] == '1' ? reinterpret_cast<const void*>(&k_residues<1>)
-                     : rv && rv[0] == '2' ? reinterpret_cast<const void*>(&k_residues<2>)
-                     : rv && rv[0] == '3' ? reinterpret_cast<const void*>(&k_residues<3>)
-                     : rv && rv[0] == '7' && ns % 16 == 0 ? reinterpret_cast<const void*>(&k_residues<7>)
-                                          : reinterpret_cast<const void*>(&k_residues<0>);
-    const unsigned rlds = r8 || e8 || (rv && rv[0] == '7' && ns % 16 == 0) ? 4 * 512 : 0;
-    const unsigned rgrid = (unsigned)((thr * (e8 ? 2 : 1) + 255) / 256);
-    if (e8) rk = reinterpret_cast<const void*>(&k_residues_e8);
+    const bool r8 = ns % 16 == 0;
+    const void* rk = r8 ? reinterpret_cast<const void*>(&k_residues<8>) : reinterpret_cast<const void*>(&k_residues<0>);
     {
       const double* AT_ = AT;
       const double* mean_ = mean;
@@ -1329,52 +947,34 @@ hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowp
       int ns_ = ns;
       int8_t* R_ = R;
       void* rargs[] = {&AT_, &ns_, &rl_, &rp_, &mean_, &dm_, &bb_, &kc_, &nk_, &R_, &ms_, &cs_};
-      e = hipLaunchKernel(rk, dim3(rgrid), dim3(256), rargs, rlds, st);
+      e = hipLaunchKernel(rk, dim3((unsigned)((thr + 255) / 256)), dim3(256), rargs, r8 ? 4 * 512 : 0, st);
       if (e != hipSuccess) return e;
     }
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
     // the events bracket the SYRK launch (with several launches: the first residue pass to the last SYRK)
     if (syrk_begin && p.nlaunch == 1) e = hipEventRecord(syrk_begin, st);
     if (e != hipSuccess) return e;
-    if (paced) {
-      e = hipMemsetAsync(pace_ctr, 0, 8 * 32 * sizeof(unsigned), st);
-      if (e != hipSuccess) return e;
-      // default: one more ring stage in flight (LD = 1: 21.89 vs 22.12 ms at C3, 7 interleaved rounds,
-      // profiles/r5/syrk_lead_wide_ab.log); PODS_SYRK_LEAD=0 (A/B) the r4 lead.  PODS_SYRK_WIDE=1
-      // (A/B): 256 x 384 tiles, 22.08 ms (their B fragments are read during the step, so they cannot
-      // take the extra stage; with LD = 1 on their 256 tiles 22.23)
-      const char* lv = std::getenv("PODS_SYRK_LEAD");
-      const bool lead = !(lv && lv[0] == '0');
-      if (lead && !wide && pace_every <= 0)
-        hipLaunchKernelGGL((k_syrk_i8_paced<5, 1, false, false, 1>), dim3(8 * nslot), dim3(512), 5 * 2 * PANEL, st,
-                           (const int8_t*)R, ns, ms, cs, p.kcs, reinterpret_cast<const int4*>(xitems), per_xcd,
-                           p.nsplit, P, pslab, ldp, li > 0 ? 1 : 0, pace_ctr, 0);
-      else if (wide)
-        hipLaunchKernelGGL((k_syrk_i8_paced<5, 1, false, true>), dim3(8 * nslot), dim3(512), 5 * 2 * PANEL, st,
-                           (const int8_t*)R, ns, ms, cs, p.kcs, reinterpret_cast<const int4*>(xitems), per_xcd,
-                           p.nsplit, P, pslab, ldp, li > 0 ? 1 : 0, pace_ctr, 0);
-      else if (pace_every > 0)
-        hipLaunchKernelGGL((k_syrk_i8_paced<5, 1, true>), dim3(8 * nslot), dim3(512), 5 * 2 * PANEL, st,
-                           (const int8_t*)R, ns, ms, cs, p.kcs, reinterpret_cast<const int4*>(xitems), per_xcd,
-                           p.nsplit, P, pslab, ldp, li > 0 ? 1 : 0, pace_ctr, pace_every);
-      else
-        hipLaunchKernelGGL((k_syrk_i8_paced<5, 1, false>), dim3(8 * nslot), dim3(512), 5 * 2 * PANEL, st,
-                           (const int8_t*)R, ns, ms, cs, p.kcs, reinterpret_cast<const int4*>(xitems), per_xcd,
-                           p.nsplit, P, pslab, ldp, li > 0 ? 1 : 0, pace_ctr, 0);
-    } else {
+#ifdef PODS_DIAG
+    if (grid_fn) {
       const int ldp_ = ldp;
       const int acc_ = li > 0 ? 1 : 0;
-      const char* ord = std::getenv("PODS_CORR_ORDER");
-      int xr_ = ord && ord[0] == 'x' ? 1 : 0;
       const int4* it_ = reinterpret_cast<const int4*>(items);
       int64_t ms_ = ms, cs_ = cs;
+      int xr_ = 0;
       void* args[] = {&R, const_cast<int*>(&ns), &ms_, &cs_, const_cast<int*>(&p.kcs),
                       &it_, const_cast<int*>(&p.nitems), const_cast<int*>(&p.nsplit), &P,
                       const_cast<int64_t*>(&pslab), const_cast<int*>(&ldp_), const_cast<int*>(&acc_), &xr_};
-      e = hipLaunchKernel(fn, dim3((unsigned)(NMOD * p.nitems)), dim3(512), args, lds, st);
+      e = hipLaunchKernel(grid_fn, dim3((unsigned)(NMOD * p.nitems)), dim3(512), args, grid_lds, st);
       if (e != hipSuccess) return e;
+      continue;
     }
+#else
+    (void)items;
+#endif
+    e = hipMemsetAsync(pace_ctr, 0, 8 * 32 * sizeof(unsigned), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_syrk_i8_paced<5, 1, 1>), dim3(8 * nslot), dim3(512), 5 * 2 * PANEL, st,
+                       (const int8_t*)R, ns, ms, cs, p.kcs, reinterpret_cast<const int4*>(xitems), per_xcd,
+                       p.nsplit, P, pslab, ldp, li > 0 ? 1 : 0, pace_ctr);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

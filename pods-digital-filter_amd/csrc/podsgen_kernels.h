@@ -65,15 +65,11 @@ hipError_t launch_absdev(const double* AT, int ns, int64_t rowlen, int64_t rowpa
                          double* devmax, hipStream_t st);
 hipError_t launch_corr_i8(const double* AT, int ns, int64_t rowlen, int64_t rowpad, const double* mean,
                           const double* devmax, const CorrI8Plan& p, const int* items, int8_t* R, uint8_t* P,
-                          double* C, int64_t ldc, int divide, hipStream_t st, hipEvent_t syrk_begin = nullptr,
-                          hipEvent_t syrk_end = nullptr, const int* xitems = nullptr, int per_xcd = 0,
-                          unsigned* pace_ctr = nullptr, int pace_every = 0, int wide = 0);
+                          double* C, int64_t ldc, int divide, hipStream_t st, hipEvent_t syrk_begin,
+                          hipEvent_t syrk_end, const int* xitems, int per_xcd, unsigned* pace_ctr);
 // the persistent SYRK's per-XCD item table from the grid-order one (per_xcd: items per XCD)
 std::vector<int> corr_i8_xcd_items(const std::vector<int>& items, int nitems, int* per_xcd);
-// The persistent SYRK's table with 256 x 384 tiles (r5): {bi, code, split, modulus} per item, code
-// = bj for a 256 x 256 tile, 0x10000 | (first column / 128) for a 256 x 384 one
-std::vector<int> corr_i8_xcd_items_wide(int ns, const CorrI8Plan& p, int* per_xcd);
-// bytes past the residue buffer's end that the 256 x 384 tiles may read (row blocks past ns)
+// slack past the residue buffer's end (allocation padding)
 constexpr int64_t CORR_I8_RPAD = 1 << 16;
 // Split-K SYRK (k_syrk_g128 + k_syrk_reduce).  Plan: returns the number of K splits (work
 // slabs of ns*ns doubles).

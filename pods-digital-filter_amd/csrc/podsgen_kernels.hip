@@ -1472,17 +1472,9 @@ static hipError_t launch_fx(const double* R, const double* bx, int ns, int64_t S
     const int64_t nvb = bx_ * ncomp * nch;
     const int64_t grid = nvb;
     // nontemporal plane loads / T1 stores: 8.15 vs 8.22 ms of main-stream generation at C3
-    // (bench A/B, r4); PODS_X_NT=0 turns them off
-    static const bool nt = [] {
-      const char* v = std::getenv("PODS_X_NT");
-      return !(v && v[0] == '0');
-    }();
-    if (nt)
-      hipLaunchKernelGGL((k_filter_x2<NX, 8, true>), dim3((unsigned)grid), dim3(256), 0, st, R, bx, ns, Sl, chunk2,
-                         T1, (int)bx_, ncomp, nch, s0, s1);
-    else
-      hipLaunchKernelGGL((k_filter_x2<NX, 8>), dim3((unsigned)grid), dim3(256), 0, st, R, bx, ns, Sl, chunk2, T1,
-                         (int)bx_, ncomp, nch, s0, s1);
+    // (bench A/B, r4)
+    hipLaunchKernelGGL((k_filter_x2<NX, 8, true>), dim3((unsigned)grid), dim3(256), 0, st, R, bx, ns, Sl, chunk2,
+                       T1, (int)bx_, ncomp, nch, s0, s1);
     return hipGetLastError();
   }
   if (s0 != 0 || s1 != ns) return hipErrorInvalidValue;  // step ranges: the point-pair kernel only
@@ -1583,10 +1575,9 @@ hipError_t launch_mean(const double* AT, int64_t rowlen, int ns, const int* prog
     const hipError_t e = hipMemsetAsync(devmax, 0, sizeof(double), st);
     if (e != hipSuccess) return e;
   }
-  // default (r5): the leaves spread over threads when there are at least 2 (and <= 256);
-  // PODS_MEAN=row (A/B): one thread per row
-  const char* mv = std::getenv("PODS_MEAN");
-  if (nleaf >= 2 && nleaf <= 256 && !(mv && mv[0] == 'r')) {
+  // default (r5): the leaves spread over threads when there are at least 2 (and <= 256); else one
+  // thread per row (k_mean)
+  if (nleaf >= 2 && nleaf <= 256) {
     // 16 leaf lanes per row (1.12-1.14 ms at C3; 32 lanes in 512-thread blocks 1.20, one thread
     // per row 1.23: profiles/r5/mean_ab.log)
     constexpr int LN = 16;

@@ -1449,7 +1449,6 @@ hipError_t syevd2_chase(int n, double* ws, const SyevdPlan& p, uint32_t* flags, 
   uint32_t* prog = flags + 128;
   const int cus = std::max(1, stream_cus(st));  // a CU-masked stream offers only its CUs
   int P = std::max(1, std::min(q1 - q0, cus));
-  if (const char* cp = std::getenv("PODS_CHASE_P")) P = std::max(1, std::min(P, std::atoi(cp)));  // A/B runs
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sb::k_sbtrd_win<B, GW>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)SW::lds_bytes);
   if (e != hipSuccess) return e;

@@ -10,6 +10,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PODSGEN_LIB", os.path.join(_HERE, "libpodsgen.so"))
 
 PODS_OK = 0
+PODS_ERR_UNSUPPORTED = -6   # podsgen.h: no plan / no kernel for this shape
 PODS_LUND_1D = 0
 PODS_LUND_PRF = 1
 PODS_LUND_NONE = -1

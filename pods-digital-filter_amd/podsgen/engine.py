@@ -208,16 +208,23 @@ class Generator:
             exchange = world > 1 and dist is not None and os.environ.get("PODS_MT_EXCHANGE", "1") != "0"
         self._xch = None
         if exchange:
-            self.enable_exchange()
+            self.enable_exchange(required=False)
 
-    def enable_exchange(self):
+    def enable_exchange(self, required=True):
         """pods_df_set_exchange with every rank's slab; the send / receive buffers are torch
-        tensors on this device (pods_df_exchange_bind)."""
+        tensors on this device (pods_df_exchange_bind).  The library has no exchange plan for a
+        stream too short for it (planes shorter than one 312-word MT block, or fewer substreams
+        than ranks: tiny inlets such as 8 x 8 with nf = 2); with required=False every rank then
+        twists the whole stream instead (the r4 path, same bits) -- the decision depends only on
+        the job's shape, so all ranks take the same one."""
         lib, h = self.ctx.lib, self.ctx.h
         slabs = [row_slab(self.setup.jma, q, self.world) for q in range(self.world)]
         j0s = np.array([a for a, _ in slabs], dtype=np.int32)
         j1s = np.array([b for _, b in slabs], dtype=np.int32)
-        check(lib.pods_df_set_exchange(h, self.world, self.rank, ptr(j0s), ptr(j1s)), "pods_df_set_exchange")
+        rc = lib.pods_df_set_exchange(h, self.world, self.rank, ptr(j0s), ptr(j1s))
+        if rc == _lib.PODS_ERR_UNSUPPORTED and not required:
+            return False
+        check(rc, "pods_df_set_exchange")
         sb = np.zeros(self.world, dtype=np.int64)
         rb = np.zeros(self.world, dtype=np.int64)
         check(lib.pods_df_exchange_sizes(h, ptr(sb), ptr(rb)), "pods_df_exchange_sizes")
@@ -226,6 +233,7 @@ class Generator:
         self._recv = torch.empty(max(int(rb.sum()), 16), dtype=torch.uint8, device=dev)
         check(lib.pods_df_exchange_bind(h, ptr(self._send), ptr(self._recv)), "pods_df_exchange_bind")
         self._xch = ([int(x) for x in sb], [int(x) for x in rb])
+        return True
 
     _a2a = None   # finisher of an all_to_all issued ahead (prefetch_jump)
 
@@ -233,7 +241,12 @@ class Generator:
         """The all_to_all of the segment-start states (2.5 KB per rank and plane; every rank calls
         generate() / prefetch_jump() together).  RCCL moves device buffers, ordered after the
         current stream; with async_op the call returns a finisher that makes the current stream
-        wait for it.  gloo (CPU transport, e.g. several ranks on one GPU) goes through host copies."""
+        wait for it.  gloo (CPU transport, e.g. several ranks on one GPU) goes through host copies:
+        with async_op the device-to-host copy of the records is enqueued on the current stream (the
+        gen stream, behind them) into pinned memory and everything else is left to the finisher --
+        it waits for that copy only, runs the all_to_all and uploads the received states on the
+        stream current at that point (generate()'s), so the host never waits for the generation
+        the records were enqueued beside."""
         sb, rb = self._xch
         d = self.dist
         n_s, n_r = sum(sb), sum(rb)
@@ -241,19 +254,54 @@ class Generator:
             work = d.all_to_all_single(self._recv[:n_r], self._send[:n_s], output_split_sizes=rb,
                                        input_split_sizes=sb, async_op=async_op)
             return (lambda: work.wait()) if async_op else None
-        send = self._send[:n_s].cpu()
-        recv = torch.empty(n_r, dtype=torch.uint8)
-        d.all_to_all_single(recv, send, output_split_sizes=rb, input_split_sizes=sb)
-        self._recv[:n_r].copy_(recv, non_blocking=False)
-        return (lambda: None) if async_op else None
+        if not async_op:
+            send = self._send[:n_s].cpu()
+            recv = torch.empty(n_r, dtype=torch.uint8)
+            d.all_to_all_single(recv, send, output_split_sizes=rb, input_split_sizes=sb)
+            self._recv[:n_r].copy_(recv, non_blocking=False)
+            return None
+        if getattr(self, "_host_xch", None) is None or self._host_xch[0].numel() != n_s:
+            self._host_xch = (torch.empty(n_s, dtype=torch.uint8, pin_memory=True),
+                              torch.empty(n_r, dtype=torch.uint8, pin_memory=True))
+        send, recv = self._host_xch
+        send.copy_(self._send[:n_s], non_blocking=True)
+        copied = torch.cuda.Event()
+        copied.record()
+
+        def finish():
+            copied.synchronize()
+            d.all_to_all_single(recv, send, output_split_sizes=rb, input_split_sizes=sb)
+            self._recv[:n_r].copy_(recv, non_blocking=True)
+            # the pinned buffers are reused by the next exchange: keep the upload ordered before it
+            done = torch.cuda.Event()
+            done.record()
+            self._host_xch_done = done
+        prev = getattr(self, "_host_xch_done", None)
+        if prev is not None:   # the previous upload from `recv` finished before it is overwritten
+            prev.synchronize()
+        return finish
 
     _ahead = None      # event behind the next run's prefetched parts (prefetch_*)
     _ahead_parts = 0   # which parts: PODS_GEN_JUMP, + PODS_GEN_PLANES
 
-    def generate(self):
+    def generate(self, timer=None):
         """The whole generation on the current stream -- or, after prefetch_jump() (and
         prefetch_planes_beside_solver()), the parts not yet done, behind the event of those
-        already enqueued on the gen stream."""
+        already enqueued on the gen stream.  timer (one device, no exchange): each part is launched
+        on its own under timer("gen_<part>") -- the same kernels in the same order, one HIP-event
+        pair per kernel (bench.py --config c2)."""
+        if timer is not None and self._xch is None:
+            rest = _lib.PODS_GEN_ALL
+            if self._ahead is not None:
+                torch.cuda.current_stream(self.ctx.device).wait_event(self._ahead)
+                rest &= ~self._ahead_parts
+                self._ahead, self._ahead_parts = None, 0
+            for part, name in ((_lib.PODS_GEN_JUMP, "gen_jump"), (_lib.PODS_GEN_PLANES, "gen_planes"),
+                               (_lib.PODS_GEN_XPASS, "gen_xpass"), (_lib.PODS_GEN_YZPASS, "gen_yzpass")):
+                if rest & part:
+                    with timer(name):
+                        check(self.ctx.lib.pods_df_generate_parts(self.ctx.h, part), "pods_df_generate_parts")
+            return self.snapshots()
         if self._xch is not None:   # the state exchange: own substreams, all_to_all, own segments
             done = 0
             if self._ahead is not None:
@@ -859,9 +907,10 @@ def eigen_solve_speculative(ctx: Context, C, ns, nm, tol_CN, tm, beside=None):
     return T, lam_t, Y, verify
 
 
-def pod_head(snap: DeviceSnapshots, world=1, timer=None):
-    """The mean and the (partial, when world > 1) correlation of run_pod (PODFS.py:1451-1455 after
-    main() :1492-1495), enqueued on the current stream: returns (C, mean)."""
+def pod_head(snap: DeviceSnapshots, world=1, timer=None, partial=None):
+    """The mean and the (partial, when world > 1 or `partial`: not divided by ns, the all-reduce's
+    unpack divides) correlation of run_pod (PODFS.py:1451-1455 after main() :1492-1495), enqueued
+    on the current stream: returns (C, mean)."""
     ctx, lib = snap.ctx, snap.ctx.lib
     dev = torch.device("cuda", ctx.device)
     tm = timer or (lambda name: _NullCtx())
@@ -873,7 +922,7 @@ def pod_head(snap: DeviceSnapshots, world=1, timer=None):
             check(lib.pods_center(ctx.h), "pods_center")
     C = torch.empty((snap.ns, snap.ns), dtype=torch.float64, device=dev)
     with tm("corr"):
-        check(lib.pods_corr(ctx.h, ptr(C), 1 if world == 1 else 0), "pods_corr")
+        check(lib.pods_corr(ctx.h, ptr(C), 0 if (world > 1 if partial is None else partial) else 1), "pods_corr")
     return C, mean
 
 
@@ -1268,9 +1317,11 @@ class ShardedSteps:
     (the next step's generation runs beside it; the tail waits for it and unpacks C).  Every result is
     that of the unpipelined order bit for bit (same kernels on the same inputs); pipelined=False
     (PODS_PIPELINE=0) runs each step's tail right after its own all-reduce.  results[k] is step
-    k's PODResult once its tail has run; flush() runs the last tail."""
+    k's PODResult once its tail has run; flush() runs the last tail.  collectives=True runs the
+    all-reduce through the process group even at world 1 (a one-rank group: a sum of one, exactly
+    the divided SYRK's bits), so a single device exercises the backend's collective path (tests)."""
 
-    def __init__(self, setup: DFSetup, gen, dist, spectrum=None, backlog=None, pipelined=None):
+    def __init__(self, setup: DFSetup, gen, dist, spectrum=None, backlog=None, pipelined=None, collectives=None):
         self.setup, self.gen, self.dist = setup, gen, dist
         self.spectrum, self.backlog = spectrum, backlog
         if pipelined is None:
@@ -1281,6 +1332,8 @@ class ShardedSteps:
         self.results = []
         _, self.rank, self.world = _dist_info(dist)
         self._solve = None
+        self._spec_done = None
+        self.collectives = self.world > 1 if collectives is None else bool(collectives)
 
     def _solve_stream(self):
         if self._solve is None:
@@ -1302,13 +1355,14 @@ class ShardedSteps:
             snap = self.gen.generate()
         if prefetch_next:
             self.gen.prefetch_jump(timer)
-        C, mean = pod_head(snap, self.world, timer)
+        C, mean = pod_head(snap, self.world, timer, partial=self.collectives)
         if self.pending is not None:
             self._tail(timer)
         check(ctx.lib.pods_select_snapshots(ctx.h, bank), "pods_select_snapshots")
         finish = None
-        if self.world > 1:
-            ctx.detect_sharing(self.dist)
+        if self.collectives:
+            if self.world > 1:
+                ctx.detect_sharing(self.dist)
             # the packed partial C goes out now; with the pipeline the main stream does not wait for
             # it (the next step's generation runs beside the all-reduce) -- its tail unpacks it
             pack, unpack = device_triangle_ops(ctx)
@@ -1317,7 +1371,9 @@ class ShardedSteps:
                 work = self.dist.all_reduce(packed, async_op=True)
 
             def finish(packed=packed, work=work, unpack=unpack, C=C):
+                # on whatever stream is current (rank 0's tail: its solve stream)
                 work.wait()
+                packed.record_stream(torch.cuda.current_stream(ctx.device))
                 unpack(packed, C)
         self.pending = [bank, snap, C, mean, finish]
         self.k += 1
@@ -1328,10 +1384,29 @@ class ShardedSteps:
         bank, snap, C, mean, finish = self.pending
         self.pending = None
         ctx = self.gen.ctx
-        if finish is not None:
+        solve = self._solve_stream() if self.rank == 0 else None
+        ready = None
+        if solve is not None:
+            # rank 0: the leading-pair solve of step k-1 depends on step k-1's all-reduce only, so
+            # the finisher (RCCL: the solve stream waits for the collective) and the unpack go to
+            # the solve stream, which then runs beside step k's generation and correlation on the
+            # main stream (an event recorded on the main stream here used to order the
+            # solve behind step k's correlation).  Before it: the spectrum units this rank enqueued
+            # on the main stream in earlier tails (persistent k_trd grids: nothing may take their
+            # CUs while they run).  The solve's own kernels (subspace iteration) are not persistent:
+            # beside the generator and the paced SYRK they only share the CUs.
+            if self._spec_done is not None:
+                solve.wait_event(self._spec_done)
+            with ctx.on_stream(solve):
+                if finish is not None:
+                    finish()
+                C.record_stream(solve)
+                ready = torch.cuda.Event()
+                ready.record(solve)
+            # the main stream reads C later (this rank's spectrum units, after the solve)
+            torch.cuda.current_stream(ctx.device).wait_event(ready)
+        elif finish is not None:
             finish()   # the main stream waits for this step's all-reduce, then unpacks C
-        ready = torch.cuda.Event()
-        ready.record()
         s = self.setup
         self.gen.join_ahead()   # the persistent spectrum kernels must not find generator workgroups
         check(ctx.lib.pods_select_snapshots(ctx.h, bank), "pods_select_snapshots")
@@ -1342,8 +1417,11 @@ class ShardedSteps:
         if self.backlog is not None:
             self.backlog.finish_pending()
         pod = pod_tail(ctx, snap, C, mean, s.nm, 1.0e-15, self.dist, timer=timer, on_temporal=start_fourier,
-                       spectrum=self.spectrum, solve_stream=self._solve_stream() if self.rank == 0 else None,
-                       c_ready=ready)
+                       spectrum=self.spectrum, solve_stream=solve, c_ready=ready)
+        # everything pod_tail put on the main stream (this rank's spectrum units among it): the next
+        # tail's solve starts behind it
+        self._spec_done = torch.cuda.Event()
+        self._spec_done.record()
         self.results.append(pod)
         if self.backlog is not None:
             self.backlog.pending.append(fo[-1] if fo else None)

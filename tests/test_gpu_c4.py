@@ -5,8 +5,10 @@ centring, the split-K SYRK at ns = 8192, the two-stage eigensolver pods_syev2 (t
 ns > 4096 takes: PODFS.py:1309-1310), temporal scaling and the spatial modes.  Checked against
 the oracle and fp64 torch without ever copying the 51.5 GB snapshot matrix whole:
 
-  (i)   generation: steps 0, 1 and 8191 bit-exact against the oracle (one pass over the
-        reference's draw stream, oracle.generate_steps), every sampled block finite;
+  (i)   generation: steps 0, 1, 4095 and 8191 bit-exact against the oracle (one pass over the
+        reference's draw stream, oracle.generate_steps), every sampled block finite; and the
+        8-rank MT state exchange (the multi-GPU generator, emulated on this device) giving every
+        slab's rows of those steps bit for bit (last test: it reconfigures the context);
   (ii)  the mean bit-exact against numpy's pairwise np.mean on 2048 sampled rows (the pairwise
         sum is per row, so a row sample is exact), and the centred rows == raw - mean;
   (iii) C exactly symmetric; sampled 256 x 256 tiles within 1e-12 max|C| of torch A_c^T A_c/ns;
@@ -27,7 +29,7 @@ torch = pytest.importorskip("torch")
 from oracle import pods_oracle as O  # noqa: E402
 
 J, K, NS, SEED = 512, 512, 8192, 4242
-STEPS = [0, 1, NS - 1]
+STEPS = [0, 1, NS // 2 - 1, NS - 1]   # stream offsets up to 6.76 G doubles (13.5 G words, past 2^32)
 NROWS = 2048
 
 
@@ -168,3 +170,28 @@ def test_c4_fourier_and_ranking(c4):
     assert np.array_equal(fo.FC, ref["FC"])
     c_ind, c_count, FC = E.host_rank_and_count(fo.c, s.et)
     assert np.array_equal(fo.c_count, c_count) and np.array_equal(fo.c_ind, c_ind)
+
+
+@pytest.mark.timeout(900)
+def test_c4_mt_state_exchange_world8_bit_exact(c4):
+    """BASELINE config 4's 8-GPU generator -- each rank twists only its 1/8 of the
+    MT19937 stream, records every rank's segment-start states, one all_to_all (emulated on this
+    device: tests/exchange_emulation.py) and each rank regenerates its own rows -- at C4's full
+    shape, whose 6.76 G-double stream passes 2^32 words: every slab's rows at steps 0, 1, 4095 and
+    8191 equal the one-device generation's (pinned to the oracle above) bit for bit
+    (digitalfilters.py:1361-1367, :1454-1467).  Runs last: it reconfigures the module's context."""
+    from exchange_emulation import emulate_exchange
+    s, ctx = c4["s"], c4["gen"].ctx
+    P = J * K
+    seen = []
+
+    def visit(q, g):
+        rows = np.concatenate([np.arange(c * P + g.j0 * K, c * P + g.j1 * K) for c in range(3)])
+        for i in STEPS:
+            got = snap_block(g, i, i + 1)[0].cpu().numpy()
+            bad = np.nonzero(got != c4["cols"][i][rows])[0]
+            assert bad.size == 0, (q, i, bad[:8])
+        seen.append((g.j0, g.j1))
+
+    emulate_exchange(s, ctx, 8, visit)
+    assert [a for a, _ in seen] == [64 * q for q in range(8)] and seen[-1][1] == J

@@ -155,6 +155,30 @@ def test_c5_generation_every_slab_bit_exact_late_steps(c5):
 
 
 @pytest.mark.timeout(900)
+def test_c5_mt_state_exchange_every_slab_bit_exact(c5):
+    """the 8-GPU generator of BASELINE config 5 (nfx = 12, nfy = nfz = 6,
+    adapt2prf; a ~52.8 G-double stream) through the MT state exchange -- each rank twists only its
+    1/8 of the stream and regenerates its own rows from the states the one all_to_all brings
+    (emulated on this device and context: tests/exchange_emulation.py) -- equals the whole-stream
+    slab generator, itself pinned to the oracle above, bit for bit at steps 0, 1, 2047 and 16383
+    of every slab (digitalfilters.py:1361-1367, :1454-1467)."""
+    from exchange_emulation import emulate_exchange
+    s, ctx = c5["s"], c5["ctx"]
+    seen = []
+
+    def visit(q, g):
+        assert (g.j0, g.j1) == c5["slabs"][q]
+        got = snap_block(g, 0, 2).cpu().numpy()
+        assert np.array_equal(got, c5["early"][q]), q
+        for i in LATE:
+            assert np.array_equal(snap_block(g, i, i + 1)[0].cpu().numpy(), c5["late"][q][i]), (q, i)
+        seen.append(q)
+
+    emulate_exchange(s, ctx, WORLD, visit)
+    assert seen == list(range(WORLD))
+
+
+@pytest.mark.timeout(900)
 def test_c5_fourier_and_ranking(c5):
     """The DFT and ranking at ns = 16384 (PODFS.py:1560-1593) on C5's own temporal modes: c
     bit-exact against the oracle's reference expression for the first FOURIER_MODES modes, and

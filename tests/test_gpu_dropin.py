@@ -271,6 +271,129 @@ def test_jump_prefetch_early_bit_equal_two_ranks_one_device():
                 assert np.array_equal(got["spectra"][k], ref["spectra"][k]), (r, name, k)
 
 
+def _world1_worker(backend, port, out):
+    """One rank, three steps of ShardedSteps with the next step's jump prefetched (bench.py's
+    order): once through the collective path over a world-1 `backend` group (collectives=True: the
+    packed all-reduce issued asynchronously and finished on rank 0's solve stream; the MT state
+    exchange, whose all_to_all is issued asynchronously on the gen stream), once without any
+    collective or exchange (the reference)."""
+    import torch
+    import torch.distributed as dist
+    import podsgen
+    from podsgen import engine as E
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    s = podsgen.DFSetup(jma=48, kma=40, ns=1024, seed=23)
+    res = {"backend": dist.get_backend()}
+    for name, coll in (("coll", True), ("plain", False)):
+        d = dist if coll else None
+        gen = E.Generator(s, device=0, rank=0, world=1, dist=d, exchange=coll)
+        assert (gen._xch is not None) == coll
+        spectrum = E.SpectrumQueue(gen.ctx, s.ns, 0, 1)
+        backlog = E.FourierBacklog()
+        run = E.ShardedSteps(s, gen, d, spectrum, backlog, collectives=coll)
+        assert run.collectives == coll
+        for k in range(3):
+            run.step(prefetch_next=k < 2)
+        run.flush()
+        backlog.flush()
+        spectrum.drain()
+        torch.cuda.synchronize()
+        res[name] = dict(T=[p.T.cpu().numpy() for p in run.results], phi=[p.phi.cpu().numpy() for p in run.results],
+                         mean=[p.mean.cpu().numpy() for p in run.results], nm=[p.nm for p in run.results],
+                         spectra=spectrum.results(),
+                         fc=[None if f is None else (f.c, f.c_count, f.FC) for f in backlog.results])
+        gen.ctx.close()
+    out[backend] = res
+    dist.destroy_process_group()
+
+
+def test_world1_collective_paths_rccl_and_gloo_bit_equal():
+    """the RCCL branches of the multi-GPU path execute on this one device -- a
+    world-1 `nccl` (RCCL) process group drives ShardedSteps with its collectives forced: the MT
+    state exchange's all_to_all_single on device buffers (issued asynchronously on the gen stream,
+    Generator.exchange_states), the packed correlation's async all_reduce, finished and unpacked on
+    rank 0's solve stream (the solve waits for the all-reduce only).  Every step's mean,
+    T, Phi, spectrum and Fourier counts / FC rows are bit-equal to the same steps with no
+    collective at all, and to the same run over gloo (its host-copy exchange branch)."""
+    import multiprocessing as mp
+    mgr = mp.Manager()
+    out = mgr.dict()
+    ctx = mp.get_context("spawn")
+    for i, backend in enumerate(("nccl", "gloo")):
+        p = ctx.Process(target=_world1_worker, args=(backend, 29900 + os.getpid() % 80 + i, out))
+        p.start()
+        p.join(600)
+        assert p.exitcode == 0, backend
+    assert out["nccl"]["backend"] == "nccl" and out["gloo"]["backend"] == "gloo"
+    ref = out["gloo"]["plain"]
+    for run in (out["nccl"]["coll"], out["nccl"]["plain"], out["gloo"]["coll"]):
+        assert run["nm"] == ref["nm"]
+        for key in ("T", "phi", "mean"):
+            assert len(run[key]) == 3
+            for k in range(3):
+                assert np.array_equal(run[key][k], ref[key][k]), (key, k)
+        assert sorted(run["spectra"]) == sorted(ref["spectra"]) == [0, 1, 2]
+        for k in ref["spectra"]:
+            assert np.array_equal(run["spectra"][k], ref["spectra"][k]), k
+        assert len(run["fc"]) == len(ref["fc"]) == 3
+        for fa, fb in zip(run["fc"], ref["fc"]):
+            assert fa is not None and fb is not None
+            for x, y in zip(fa, fb):
+                assert np.array_equal(x, y)
+
+
+def _tiny_worker(rank, world, port, out):
+    import torch.distributed as dist
+    import podsgen
+    from podsgen import engine as E
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    s = podsgen.DFSetup(jma=8, kma=8, ns=16, seed=5, lengthscale=1.0, nm=4)
+    gen = E.Generator(s, device=0, rank=rank, world=world, dist=dist)
+    xch = gen._xch is not None
+    gen, pod, fo = E.pipeline(s, device=0, dist=dist, gen=gen)
+    out[rank] = dict(j0=gen.j0, j1=gen.j1, xch=xch, mean=pod.mean.cpu().numpy(), nm=pod.nm)
+    dist.destroy_process_group()
+
+
+def test_tiny_inlet_two_ranks_whole_stream_fallback():
+    """an inlet whose random planes are shorter than one 312-word MT19937 block (8 x 8,
+    nf = 2: S = 144) has no state-exchange plan (pods_df_set_exchange: PODS_ERR_UNSUPPORTED); a
+    multi-rank Generator then falls back to every rank twisting the whole stream instead of
+    failing -- 2 ranks (gloo, one GPU): the pipeline runs and every slab's mean equals the
+    single-rank run's rows bit for bit."""
+    import multiprocessing as mp
+    import podsgen
+    from podsgen import engine as E
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = 29150 + os.getpid() % 40
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_tiny_worker, args=(r, 2, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+        assert p.exitcode == 0
+    s = podsgen.DFSetup(jma=8, kma=8, ns=16, seed=5, lengthscale=1.0, nm=4)
+    assert s.nfy == 2 and (s.jma + 2 * s.nfy) * (s.kma + 2 * s.nfz) < 312
+    gen, pod, fo = E.pipeline(s, device=0)
+    mean = pod.mean.cpu().numpy()
+    P, K = s.P, s.kma
+    for r in range(2):
+        d = out[r]
+        assert not d["xch"]
+        pl = (d["j1"] - d["j0"]) * K
+        for comp in range(3):
+            rows = slice(comp * P + d["j0"] * K, comp * P + d["j1"] * K)
+            assert np.array_equal(d["mean"][comp * pl:(comp + 1) * pl], mean[rows])
+        assert d["nm"] == pod.nm
+
+
 def test_sharded_pipeline_two_ranks_one_device():
     """Row slabs on 2 ranks (gloo transport, one GPU) == the single-rank pipeline."""
     import multiprocessing as mp
@@ -447,7 +570,7 @@ def test_bench_launches_its_own_ranks():
     assert out["value"] > 0
 
 
-@pytest.mark.timeout(900)
+@pytest.mark.timeout(1500)
 def test_bench_c3_two_ranks_one_device_no_fallback():
     """`bench.py --gpus 2 --backend gloo` at C3 (ns = 4096: the split eigensolve, the spectrum
     units of engine.SpectrumQueue on both ranks) with both ranks on this one GPU.  The ranks'
@@ -470,3 +593,38 @@ def test_bench_c3_two_ranks_one_device_no_fallback():
     assert out["n_gpus"] == 2 and out["config"]["ns"] == 4096
     assert out["results"]["eigensolve"].startswith("split")
     assert out["results"]["num_valid"] is not None and out["results"]["nm"] == 20
+    assert out["config"]["mt_state_exchange"] and out["config"]["pipelined_tail"]
+    # the same job on one rank (fused eigensolve, no exchange, no pipeline) gives
+    # the same results: the valid-mode count of the full spectrum and every mode's Fourier count
+    r1 = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "1", "--config", "c3",
+                         "--steps", "2", "--warmup", "1", "--no-cpu"],
+                        capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    one = json.loads([l for l in r1.stdout.splitlines() if l.startswith("{")][-1])
+    assert one["results"]["eigensolve"].startswith("fused")
+    assert out["results"]["num_valid"] == one["results"]["num_valid"]
+    assert out["results"]["nm"] == one["results"]["nm"]
+    assert out["results"]["N_FC"] == one["results"]["N_FC"], (out["results"]["N_FC"], one["results"]["N_FC"])
+
+
+@pytest.mark.timeout(600)
+def test_bench_c2_generation_line():
+    """`bench.py --config c2` (BASELINE config 2: the digital filter + Lund transform only): one JSON
+    line with the generation-only metric, the per-kernel HIP-event times (jump, planes, x pass, y/z
+    pass) summing to about the step, and the y/z kernel's HBM roofline."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--config", "c2", "--steps", "3",
+                        "--warmup", "1", "--no-cpu"], capture_output=True, text=True, timeout=540, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert "generation only" in out["metric"] and out["config"]["ns"] == 4096
+    st = out["stages_ms"]
+    assert set(st) == {"gen_jump", "gen_planes", "gen_xpass", "gen_yzpass"}
+    assert 0.8 * out["ms_per_step"] <= sum(st.values()) <= 1.05 * out["ms_per_step"]
+    rl = out["roofline"]
+    assert rl["bound"] == "hbm" and 0.0 < rl["frac"] < 1.0 and rl["unit"] == "GB/s"
+    assert 0.0 < out["generation_roofline"]["frac"] < 1.0

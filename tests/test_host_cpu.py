@@ -26,6 +26,26 @@ def test_library_exports_every_header_symbol():
     assert _lib.load().pods_abi_version() == 1
 
 
+DIAG_SWITCHES = ("PODS_SYRK_I8", "PODS_RES_I8", "PODS_CORR_ORDER", "PODS_SYRK_WIDE", "PODS_SYRK_LEAD",
+                 "PODS_SYRK_PACE", "PODS_X_NT", "PODS_MEAN", "PODS_CHASE_P")
+
+
+def test_product_library_has_no_variant_switches():
+    """the measurement-only variants (wrong results: PODS_SYRK_I8=9*, the residue
+    pass without loads or stores, every item on one tile) and the A/B variants measured equal or
+    slower are not in libpodsgen.so -- the product library never reads those switches (no getenv
+    of their names: the names are not even in its string table), so setting them cannot change a
+    result.  The grid SYRK and its measurement variants build only into the diagnostic library
+    (`make -C pods-digital-filter_amd/csrc diag`, -DPODS_DIAG)."""
+    from podsgen import _lib
+    blob = open(_lib.LIB_PATH, "rb").read()
+    for name in DIAG_SWITCHES:
+        assert name.encode() + b"\0" not in blob, name
+    # the switches that select correct alternatives stay (fp64 SYRK, residue budget, K splits)
+    for name in ("PODS_CORR", "PODS_CORR_BUDGET_GB", "PODS_CORR_SPLITS"):
+        assert name.encode() + b"\0" in blob, name
+
+
 def test_persistent_grid_rule():
     """The co-residency rule every spin-waiting launch passes first (pods::check_persistent):
     a grid larger than blocks-per-CU x CUs is refused with PODS_ERR_UNSUPPORTED."""
