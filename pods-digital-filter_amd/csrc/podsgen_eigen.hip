@@ -155,6 +155,31 @@ __device__ __forceinline__ double pick(const double (&v)[S], int m) {
   return r;
 }
 
+// dst[i] = the lane-held vector v at row r = g + G i of this workgroup, i in [I0, R) (lane r % 512,
+// slot r / 512 holds it; k_trd's layout).  G = 256 (TT / 2): lane g has rows of even i at slot
+// i / 2, lane g + 256 those of odd i -- compile-time registers, two lanes store.
+template <int R, int S, int I0>
+__device__ __forceinline__ void share_rows(double* dst, const double (&v)[S], int g, int G, int t, int n) {
+  constexpr int TT_ = 512;
+  if (G == TT_ / 2) {
+    if (t == g) {
+#pragma unroll
+      for (int i = (I0 + 1) & ~1; i < R; i += 2)
+        if (g + G * i < n) dst[i] = v[i >> 1];
+    } else if (t == g + TT_ / 2) {
+#pragma unroll
+      for (int i = I0 | 1; i < R; i += 2)
+        if (g + G * i < n) dst[i] = v[i >> 1];
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = I0; i < R; ++i) {
+    const int r = g + G * i;
+    if (r < n && (r & (TT_ - 1)) == t) dst[i] = pick(v, r / TT_);
+  }
+}
+
 // ---- tagged 8-byte hand-off values: the two lowest mantissa bits carry the column parity
 // ---- tag (j mod 4).  One 8-B sc1 store publishes value and tag together; the consumer
 // ---- spins on its own loads until the tag matches -- no flag, no producer drain, one hop.
@@ -353,11 +378,12 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
       p[m] = tau_p * p[m];
       dot = __builtin_fma(p[m], vp[m], dot);
     }
-#pragma unroll
-    for (int i = I0; i < R; ++i) {
-      const int r = g + G * i;
-      if (r < n && (r & (TT - 1)) == t) rsv[i] = pick(vp, r / TT);
-    }
+    // v_{j-1} at this workgroup's rows, for the lanes that hold them (row r sits in lane r % 512,
+    // slot r / 512); with G = 256 workgroups (n > 4080) row g + 256 i is in lane g (i even) or
+    // g + 256 (i odd), slot i / 2 -- a register known at compile time, so only those two lanes
+    // store and nothing is selected (the general loop picks the slot with 2 S v_cndmasks per row
+    // in every lane: ~0.5 us per column at range 0, r6 trace)
+    share_rows<R, S, I0>(rsv, vp, g, G, t, n);
     dot = block_sum<TT / 64>(dot, red + 8 * (rk++ & 1));                       // B1
     if (trace) trace[j * 8 + 2] = (int64_t)__builtin_amdgcn_s_memrealtime();
     const double alpha = -0.5 * tau_p * dot;
@@ -373,11 +399,7 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
       x[m] = (c >= j && c < n) ? __builtin_fma(-p[m], vj, __builtin_fma(-vp[m], wj, x[m])) : 0.0;
     }
     if (t == ((j + 1) & (TT - 1))) bc[(j & 1) * 2] = pick(x, (j + 1) / TT);
-#pragma unroll
-    for (int i = I0; i < R; ++i) {
-      const int r = g + G * i;
-      if (r < n && (r & (TT - 1)) == t) rsw[i] = pick(p, r / TT);
-    }
+    share_rows<R, S, I0>(rsw, p, g, G, t, n);                                      // w_{j-1} likewise
     double ss = 0.0;
 #pragma unroll
     for (int m = 0; m < S; ++m) {
