@@ -1381,12 +1381,12 @@ int run_sytrd(pods_ctx* c, const double* C, int n, int* R_out, int64_t* trace = 
   if (pods::trd_plan(n, &R, &G, &slab) != 0)
     return fail(PODS_ERR_UNSUPPORTED, "pods_syev: n = " + std::to_string(n) + " > 4096");
   PODS_HIP(ensure(c->e_wm, (size_t)slab * sizeof(double)));
-  PODS_HIP(ensure(c->e_x, (size_t)32 * n * sizeof(double)));  // 2 vectors x 8 XCD copies x 2 parities x n
+  PODS_HIP(ensure(c->e_x, (size_t)32 * pods::TRD_HANDOFF * sizeof(double)));  // 2 vectors x 8 XCD copies x 2 parities x n
   PODS_HIP(ensure(c->e_flags, 64));
   PODS_HIP(ensure(c->e_det, ((size_t)4 * n + 8) * sizeof(double)));
   PODS_HIP(ensure(c->e_v, (size_t)std::max(n - 1, 1) * n * sizeof(double)));
   PODS_HIP(hipMemsetAsync(c->e_flags.p, 0, 64, c->stream));
-  PODS_HIP(hipMemsetAsync(c->e_x.p, 0, (size_t)32 * n * sizeof(double), c->stream));
+  PODS_HIP(hipMemsetAsync(c->e_x.p, 0, (size_t)32 * pods::TRD_HANDOFF * sizeof(double), c->stream));
   c->e_G = 0;
   double* det = c->e_det.as<double>();
   pods::TrdArgs a{};
@@ -1397,7 +1397,7 @@ int run_sytrd(pods_ctx* c, const double* C, int n, int* R_out, int64_t* trace = 
   a.klast = (n - 1) / 512;
   a.Wm = c->e_wm.as<double>();
   a.pbuf = c->e_x.as<double>();
-  a.rbuf = c->e_x.as<double>() + 16 * (int64_t)n;
+  a.rbuf = c->e_x.as<double>() + 16 * (int64_t)pods::TRD_HANDOFF;
   a.flags = c->e_flags.as<uint32_t>();
   a.D = det;
   a.E = det + n;
@@ -1523,14 +1523,14 @@ int pods_eigvals_begin(pods_ctx* c, int slot, const double* C, int n) {
     sl.flag_words = 0;
   }
   PODS_HIP(ensure(sl.wm, (size_t)slab * sizeof(double)));
-  PODS_HIP(ensure(sl.x, (size_t)32 * n * sizeof(double)));
+  PODS_HIP(ensure(sl.x, (size_t)32 * pods::TRD_HANDOFF * sizeof(double)));
   PODS_HIP(ensure(sl.flags, 64));
   PODS_HIP(ensure(sl.det, ((size_t)4 * n + 8) * sizeof(double)));
   PODS_HIP(ensure(sl.v, (size_t)std::max(n - 1, 1) * n * sizeof(double)));
   PODS_HIP(ensure(sl.cnt, pods::tri_grid_bytes()));
   PODS_HIP(ensure(sl.lam, (size_t)n * sizeof(double)));
   PODS_HIP(hipMemsetAsync(sl.flags.p, 0, 64, c->stream));
-  PODS_HIP(hipMemsetAsync(sl.x.p, 0, (size_t)32 * n * sizeof(double), c->stream));
+  PODS_HIP(hipMemsetAsync(sl.x.p, 0, (size_t)32 * pods::TRD_HANDOFF * sizeof(double), c->stream));
   double* det = sl.det.as<double>();
   pods::TrdArgs a{};
   a.C = C;
@@ -1540,7 +1540,7 @@ int pods_eigvals_begin(pods_ctx* c, int slot, const double* C, int n) {
   a.klast = (n - 1) / 512;
   a.Wm = sl.wm.as<double>();
   a.pbuf = sl.x.as<double>();
-  a.rbuf = sl.x.as<double>() + 16 * (int64_t)n;
+  a.rbuf = sl.x.as<double>() + 16 * (int64_t)pods::TRD_HANDOFF;
   a.flags = sl.flags.as<uint32_t>();
   a.D = det;
   a.E = det + n;

@@ -220,9 +220,26 @@ __device__ __forceinline__ int xcc_id() {
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
   return x & 15;
 }
-// buffer (p or column) for replica r, column parity q
-__device__ __forceinline__ double* hbuf(double* base, int r, int q, int n) {
-  return base + ((int64_t)r * 2 + q) * n;
+// buffer (p or column) for replica r, column parity q; hs doubles each (TRD_HANDOFF at most)
+__device__ __forceinline__ double* hbuf(double* base, int r, int q, int hs) {
+  return base + ((int64_t)r * 2 + q) * hs;
+}
+// Lane-major hand-off layout (r6): the granule of row/column c sits at (c % 512) S + c / 512, so a
+// consumer lane's S slots (columns t + 512 m) are S contiguous granules -- 16-B loads of slot pairs,
+// a wave's loads one contiguous 8 S x 64-byte run -- and a workgroup's 16 rows (g + 256 i with
+// G = 256) land in two runs of 8 contiguous granules per vector and copy, instead of 16 granules
+// 2 KB apart.
+template <int S>
+__device__ __forceinline__ int hslot(int c) {
+  return (c & 511) * S + (c >> 9);
+}
+__device__ __forceinline__ void gld2(__amdgpu_buffer_rsrc_t r, int idx, double& a, double& b) {
+  // volatile (bit 31) + sc1 (bit 4), like gld: two granules (16-B aligned: idx even)
+  const auto q = __builtin_amdgcn_raw_buffer_load_b128(r, idx * 8, 0, (1u << 31) | 16u);
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  const d2 v = __builtin_bit_cast(d2, q);
+  a = v.x;
+  b = v.y;
 }
 
 // -----------------------------------------------------------------------------------------
@@ -250,6 +267,8 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
   constexpr int I0 = (2 * K < R) ? 2 * K : R;  // first live row slot
   constexpr int RL = R - I0;                    // live rows
   constexpr int SR = S - K - SG - SL;           // register slots
+  constexpr int HS = TT * S;                    // doubles per hand-off buffer (<= TRD_HANDOFF)
+  static_assert(HS <= TRD_HANDOFF, "hand-off buffer");
   static_assert(SR >= 0 && RL > 0, "bad trd range configuration");
   extern __shared__ double lds[];
   double* Al = lds;                  // [SL][RL][TT]
@@ -311,6 +330,9 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
                        ? a.trace + (a.trace_wg < 0 ? (int64_t)g0 * n * 8 : 0)
                        : nullptr;
   for (int j = jb; j < je; ++j) {
+#ifdef PODS_TRD_DRAIN  // diagnostic variant builds only (tools/lib_variants.sh): the wave's stores done first
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     if (trace) trace[j * 8 + 0] = (int64_t)__builtin_amdgcn_s_memrealtime();
     // Re-materialise the lane/workgroup indices every column: without this the compiler
     // hoists ~100 loop-invariant addresses and masks out of the column loop and spills.
@@ -331,31 +353,44 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
         x[m] = c < n ? a.C[c] : 0.0;
       }
     } else {
-      const __amdgpu_buffer_rsrc_t rp = rsrc8(hbuf(a.pbuf, xrep, (j - 1) & 1, n), n);
-      const __amdgpu_buffer_rsrc_t rc = rsrc8(hbuf(a.rbuf, xrep, (j - 1) & 1, n), n);
+      const __amdgpu_buffer_rsrc_t rp = rsrc8(hbuf(a.pbuf, xrep, (j - 1) & 1, HS), HS);
+      const __amdgpu_buffer_rsrc_t rc = rsrc8(hbuf(a.rbuf, xrep, (j - 1) & 1, HS), HS);
       const uint32_t want = (uint32_t)j;
-      // Every spin re-reads all of this lane's granules (simple straight-line code keeps the
-      // register allocation flat); the wave leaves when all its lanes saw the tag.
+      // Every spin re-reads all of this lane's live granules (simple straight-line code keeps the
+      // register allocation flat); the wave leaves when all its lanes saw the tag.  Slots below
+      // ML hold only columns < j (slot K-1 reaches j = 512K-1 only in the range's first column):
+      // no loads for them; a granule whose column is dead or past n is loaded with its pair but
+      // not checked (nothing publishes it any more).
+      constexpr int PW = (S % 2 == 0) ? 2 : 1;
+      constexpr int ML = (K == 0 ? 0 : K - 1) / PW * PW;
+      const int lj = hslot<S>(j);
       for (int spin = 0;; ++spin) {
         bool ok = true;
 #pragma unroll
-        for (int m = 0; m < S; ++m) {
-          // slots below K hold only columns < j (slot K-1 reaches j = 512K-1 only in the
-          // range's first column): no loads for them
-          if (m < K && (m < K - 1 || j != jb)) {
-            p[m] = 0.0;
-            x[m] = 0.0;
-            continue;
-          }
-          const int c = t + TT * m;
-          const bool in = c >= j && c < n;
-          const double q1 = gld(rp, in ? c : j);
-          const double q2 = gld(rc, in ? c : j);
-          ok = ok && tag_ok(q1, want) && tag_ok(q2, want);
-          p[m] = in ? untag(q1) : 0.0;
-          x[m] = in ? untag(q2) : 0.0;
+        for (int m = 0; m < ML; ++m) {
+          p[m] = 0.0;
+          x[m] = 0.0;
         }
-        const double qj = gld(rp, j);
+#pragma unroll
+        for (int m = ML; m < S; m += PW) {
+          double q1[PW], q2[PW];
+          if constexpr (PW == 2) {
+            gld2(rp, t * S + m, q1[0], q1[1]);
+            gld2(rc, t * S + m, q2[0], q2[1]);
+          } else {
+            q1[0] = gld(rp, t * S + m);
+            q2[0] = gld(rc, t * S + m);
+          }
+#pragma unroll
+          for (int u = 0; u < PW; ++u) {
+            const int c = t + TT * (m + u);
+            const bool in = c >= j && c < n;
+            ok = ok && (!in || (tag_ok(q1[u], want) && tag_ok(q2[u], want)));
+            p[m + u] = in ? untag(q1[u]) : 0.0;
+            x[m + u] = in ? untag(q2[u]) : 0.0;
+          }
+        }
+        const double qj = gld(rp, lj);
         ok = ok && tag_ok(qj, want);
         pj = untag(qj);
         nspin = spin;
@@ -428,8 +463,8 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
     // ---- so the hand-off needs only a read of the stored rows; the rank-2 update of step
     // ---- j-1 is applied after the publish, overlapping the next column's hop.
     if (trace) trace[j * 8 + 4] = (int64_t)__builtin_amdgcn_s_memrealtime();
-    const __amdgpu_buffer_rsrc_t pw = rsrc8(hbuf(a.pbuf, 0, j & 1, n), 2 * NREP * n);
-    const __amdgpu_buffer_rsrc_t cw = rsrc8(hbuf(a.rbuf, 0, j & 1, n), 2 * NREP * n);
+    const __amdgpu_buffer_rsrc_t pw = rsrc8(hbuf(a.pbuf, 0, j & 1, HS), 2 * NREP * HS);
+    const __amdgpu_buffer_rsrc_t cw = rsrc8(hbuf(a.rbuf, 0, j & 1, HS), 2 * NREP * HS);
     const uint32_t tag = (uint32_t)(j + 1);
     const bool pubcol = t == ((j + 1) & (TT - 1));
     constexpr int RH = (SG > 0) ? 2 : ((RL % 4 == 0) ? 4 : ((RL % 2 == 0) ? 2 : 1));
@@ -528,8 +563,8 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
           d1 += rr[R * 8 + q];
           d2 += rr[(R + 1) * 8 + q];
         }
-        gst(pw, rep_ * 2 * n + r, __builtin_fma(-rsw[i], d2, __builtin_fma(-rsv[i], d1, sum)), tag);
-        gst(cw, rep_ * 2 * n + r, rcol[i], tag);
+        gst(pw, rep_ * 2 * HS + hslot<S>(r), __builtin_fma(-rsw[i], d2, __builtin_fma(-rsv[i], d1, sum)), tag);
+        gst(cw, rep_ * 2 * HS + hslot<S>(r), rcol[i], tag);
       }
     }
     // the writer's outputs leave after the hand-off so they never delay it
@@ -538,11 +573,21 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
         a.E[j] = beta;
         a.tau[j] = tau_j;
       }
+#if defined(PODS_TRD_NOV)  // diagnostic variant builds only (tools/lib_variants.sh): no V stores (wrong vectors)
+      if (x[0] == 12345.678) a.V[j] = x[1];
+#elif defined(PODS_TRD_VNT)  // diagnostic variant: V through nontemporal stores
+#pragma unroll
+      for (int m = 0; m < S; ++m) {
+        const int c = t + TT * m;
+        if (c < n) __builtin_nontemporal_store(x[m], a.V + (int64_t)j * a.ldv + c);
+      }
+#else
 #pragma unroll
       for (int m = 0; m < S; ++m) {
         const int c = t + TT * m;
         if (c < n) st_sc1(a.V + (int64_t)j * a.ldv + c, x[m]);  // sc1: keep V out of L2
       }
+#endif
     }
     // ---- rank-2 update of step j-1 on rows >= j+1 (dead rows: zero multipliers, exact
     // ---- no-op arithmetic, so no branch touches the matrix registers) --------------------
@@ -619,17 +664,18 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
     // tau_{n-2} = 0 (nothing below row n-1), v_{n-2} = e_{n-1}: d = a - 2 w[n-1]
     const int j = n - 1;
     if (t0 == (j & (TT - 1))) {
-      const __amdgpu_buffer_rsrc_t rp = rsrc8(hbuf(a.pbuf, 0, (j - 1) & 1, n), n);
-      const __amdgpu_buffer_rsrc_t rc = rsrc8(hbuf(a.rbuf, 0, (j - 1) & 1, n), n);
+      const __amdgpu_buffer_rsrc_t rp = rsrc8(hbuf(a.pbuf, 0, (j - 1) & 1, HS), HS);
+      const __amdgpu_buffer_rsrc_t rc = rsrc8(hbuf(a.rbuf, 0, (j - 1) & 1, HS), HS);
+      const int lj = hslot<S>(j);
       double pv = 0.0, cv = 0.0;
       bool np = true, nc = true;
       for (int spin = 0; (np || nc) && spin <= SPIN_LIMIT; ++spin) {
         if (np) {
-          const double q = gld(rp, j);
+          const double q = gld(rp, lj);
           if (tag_ok(q, (uint32_t)j)) { pv = untag(q); np = false; }
         }
         if (nc) {
-          const double q = gld(rc, j);
+          const double q = gld(rc, lj);
           if (tag_ok(q, (uint32_t)j)) { cv = untag(q); nc = false; }
         }
       }

@@ -98,6 +98,9 @@ hipError_t launch_rank(const float* c, int ns, int nm, double et, const int* pro
                        int32_t* c_ind, int64_t* c_count, hipStream_t st);
 
 // ---- symmetric eigensolver (podsgen_eigen.hip) ----------------------------------------
+// doubles per k_trd hand-off buffer (one vector, one XCD copy, one column parity): 512 lanes x 8
+// slots; the workspace holds 2 vectors x 8 copies x 2 parities of them
+constexpr int TRD_HANDOFF = 4096;
 struct TrdArgs {
   const double* C;   // n x n row-major symmetric input (read only)
   int64_t ldc;
