@@ -255,6 +255,10 @@ __device__ __forceinline__ void gld2(__amdgpu_buffer_rsrc_t r, int idx, double& 
 // pending reflector v_{j-1} is re-read from V and tau from the tau array.
 // Storage inside a launch: slots [K, K+SG) stay in Wm (L2-resident), the next SL slots in
 // LDS, the rest in VGPRs.
+// H = 1 (r6, with K = 0): the second half of range 0, columns [256, 511), run as a launch of its
+// own: there row slot i = 0 (rows g < 256) and the lanes t < 256 of slot 0 hold nothing live any
+// more, so the 15 live rows' slot 0 fits in LDS beside the SL = 2 slots (lanes 256..511 only,
+// "Ah") and the L2 slab slot of the first half (H = 0: columns [0, 256)) is gone.
 //
 // Column j (dsytd2 'L'): every workgroup reads p_{j-1} = A^{(j-1)} v_{j-1} and column j of
 // A^{(j-1)} (both published in column j-1 as tagged granules by the owners of the rows),
@@ -262,17 +266,20 @@ __device__ __forceinline__ void gld2(__amdgpu_buffer_rsrc_t r, int idx, double& 
 // reductions), applies the pending rank-2 update to its rows fused with p_j = A^{(j)} v_j,
 // and publishes p_j and column j+1 of its rows.  Three workgroup barriers, one cross-CU hop.
 // -----------------------------------------------------------------------------------------
-template <int R, int S, int K, int SG, int SL>
+template <int R, int S, int K, int SG, int SL, int H = 0>
 __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
-  constexpr int I0 = (2 * K < R) ? 2 * K : R;  // first live row slot
+  static_assert(H == 0 || (K == 0 && SG == 0 && R == 16), "the half launch splits range 0 of the 16-row plan");
+  constexpr int I0 = H ? 1 : ((2 * K < R) ? 2 * K : R);  // first live row slot
   constexpr int RL = R - I0;                    // live rows
-  constexpr int SR = S - K - SG - SL;           // register slots
+  constexpr int SGH = SG + H;                   // slots before the LDS ones: slab (SG) or half (H)
+  constexpr int SR = S - K - SGH - SL;          // register slots
   constexpr int HS = TT * S;                    // doubles per hand-off buffer (<= TRD_HANDOFF)
   static_assert(HS <= TRD_HANDOFF, "hand-off buffer");
   static_assert(SR >= 0 && RL > 0, "bad trd range configuration");
   extern __shared__ double lds[];
   double* Al = lds;                  // [SL][RL][TT]
-  double* red = lds + SL * RL * TT;  // 2 x 8 reduction slots
+  double* Ah = lds + SL * RL * TT;   // H: [RL][256] slot K's lanes 256..511
+  double* red = Ah + H * RL * 256;   // 2 x 8 reduction slots
   double* bc = red + 16;             // 4: alpha0 (double-buffered by column parity)
   double* rsv0 = bc + 4;             // 2 x R: v_{j-1}[r_i]   (double-buffered by column parity:
   double* rsw0 = rsv0 + 2 * R;       // 2 x R: w_{j-1}[r_i]    the update reads them after B3)
@@ -290,8 +297,11 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
   // Ranges K > klast = (n-1)/512 hold no column and are not launched; klast runs the tail.
   const bool last = K == a.klast;
   const int jend = min(lastrow + 1, n - 1);
-  const int jb = K == 0 ? 0 : TT * K - 1;
-  const int je = last ? jend : min(jend, TT * (K + 1) - 1);
+  // the 16-row plan runs range 0 as two halves: [0, 256) with the slab slot, [256, 511) with
+  // slot 0 in LDS (H); every other plan runs [0, 511)
+  constexpr bool SPLIT0 = K == 0 && R == 16;
+  const int jb = K == 0 ? (H ? TT / 2 : 0) : TT * K - 1;
+  const int je = last ? jend : min(jend, (SPLIT0 && !H) ? TT / 2 : TT * (K + 1) - 1);
 
   // ---- load the live block -----------------------------------------------------------------
 #pragma unroll
@@ -302,16 +312,20 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
     for (int m = K; m < S; ++m) {
       const int c = t0 + TT * m;
       double v;
-      if (K == 0)
+      if (K == 0 && !H)
         v = (r < n && c < n) ? a.C[(int64_t)r * a.ldc + c] : 0.0;
       else
         v = wm(m, i, t0);
-      if (m < K + SG) {
-        if (K == 0) wm(m, i, t0) = v;
-      } else if (m < K + SG + SL) {
-        Al[((m - K - SG) * RL + ii) * TT + t0] = v;
+      if (m < K + SGH) {
+        if (H) {
+          if (t0 >= TT / 2) Ah[ii * (TT / 2) + t0 - TT / 2] = v;
+        } else if (K == 0) {
+          wm(m, i, t0) = v;
+        }
+      } else if (m < K + SGH + SL) {
+        Al[((m - K - SGH) * RL + ii) * TT + t0] = v;
       } else {
-        Ar[ii][m - K - SG - SL] = v;
+        Ar[ii][m - K - SGH - SL] = v;
       }
     }
   }
@@ -467,7 +481,9 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
     const __amdgpu_buffer_rsrc_t cw = rsrc8(hbuf(a.rbuf, 0, j & 1, HS), 2 * NREP * HS);
     const uint32_t tag = (uint32_t)(j + 1);
     const bool pubcol = t == ((j + 1) & (TT - 1));
-    constexpr int RH = (SG > 0) ? 2 : ((RL % 4 == 0) ? 4 : ((RL % 2 == 0) ? 2 : 1));
+    // rows per reduction group; H (15 rows): groups of 4, the last one padded with a zero row
+    constexpr int RH = (SG > 0) ? 2 : ((RL % 4 == 0 || H) ? 4 : ((RL % 2 == 0) ? 2 : 1));
+    constexpr int NG = (RL + RH - 1) / RH;
     {
       double dd[2] = {0.0, 0.0};
 #pragma unroll
@@ -512,7 +528,7 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
 #pragma unroll
       for (int m = K; m < K + SG; ++m) slab[ii][m - K] = slab_ld(m, I0 + ii);
 #pragma unroll
-    for (int h = 0; h < RL / RH; ++h) {
+    for (int h = 0; h < NG; ++h) {
 #pragma unroll
       for (int ii = (h + SPF) * RH; ii < (SG > 0 ? (h + SPF + 1) * RH : 0); ++ii)
         if (ii < RL)
@@ -526,13 +542,22 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
 #pragma unroll
         for (int q = 0; q < RH; ++q) {
           const int ii = h * RH + q;
+          if (ii >= RL) {  // H: the zero row padding the last group
+            if (m == K) colv[q] = 0.0;
+            continue;
+          }
           double val;
-          if (m < K + SG) {
-            val = slab[ii][m - K];
-          } else if (m < K + SG + SL) {
-            val = Al[((m - K - SG) * RL + ii) * TT + t];
+          if (m < K + SGH) {
+            if constexpr (H) {  // lanes < 256 hold nothing live in slot K (their columns are < j)
+              const double hv = Ah[ii * (TT / 2) + (t & (TT / 2 - 1))];
+              val = t >= TT / 2 ? hv : 0.0;
+            } else {
+              val = slab[ii][m - K];
+            }
+          } else if (m < K + SGH + SL) {
+            val = Al[((m - K - SGH) * RL + ii) * TT + t];
           } else {
-            val = Ar[ii][m - K - SG - SL];
+            val = Ar[ii][m - K - SGH - SL];
           }
           acc[q] = __builtin_fma(val, x[m], acc[q]);
           if (m == K) colv[q] = val;
@@ -542,11 +567,12 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
 #pragma unroll
         for (int q = 0; q < RH; ++q) {
           const int i = I0 + h * RH + q;
-          rcol[i] = __builtin_fma(-rsv[i], p[K], __builtin_fma(-rsw[i], vp[K], colv[q]));
+          if (i < R) rcol[i] = __builtin_fma(-rsv[i], p[K], __builtin_fma(-rsw[i], vp[K], colv[q]));
         }
       }
       const double sum = rows_wave_sum(acc);
-      if ((lane & (64 / RH - 1)) == 0) rr[(I0 + h * RH + lane / (64 / RH)) * 8 + wv] = sum;
+      const int ir = I0 + h * RH + lane / (64 / RH);
+      if ((lane & (64 / RH - 1)) == 0 && ir < R) rr[ir * 8 + wv] = sum;
     }
     if (trace) trace[j * 8 + 5] = (int64_t)__builtin_amdgcn_s_memrealtime();
     __syncthreads();                                                               // B3
@@ -592,7 +618,7 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
     // ---- rank-2 update of step j-1 on rows >= j+1 (dead rows: zero multipliers, exact
     // ---- no-op arithmetic, so no branch touches the matrix registers) --------------------
 #pragma unroll
-    for (int h = 0; h < RL / RH; ++h) {
+    for (int h = 0; h < NG; ++h) {
       double vr[RH], wr[RH];
       // The group's multipliers and LDS slot values are read back to back before any use or
       // write (r5): read one by one -- each behind its row's liveness branch, or after the
@@ -600,14 +626,19 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
       double rv[RH], rw[RH];
 #pragma unroll
       for (int q = 0; q < RH; ++q) {
-        rv[q] = rsv[I0 + h * RH + q];
-        rw[q] = rsw[I0 + h * RH + q];
+        rv[q] = h * RH + q < RL ? rsv[I0 + h * RH + q] : 0.0;
+        rw[q] = h * RH + q < RL ? rsw[I0 + h * RH + q] : 0.0;
       }
       double lv[RH][SL > 0 ? SL : 1];
 #pragma unroll
       for (int q = 0; q < RH; ++q)
 #pragma unroll
-        for (int m = 0; m < SL; ++m) lv[q][m] = Al[(m * RL + h * RH + q) * TT + t];
+        for (int m = 0; m < SL; ++m) lv[q][m] = h * RH + q < RL ? Al[(m * RL + h * RH + q) * TT + t] : 0.0;
+      // H: slot K's values of the group (lanes 256..511; the waves of lanes < 256 hold none)
+      double hv[RH];
+#pragma unroll
+      for (int q = 0; q < RH; ++q)
+        hv[q] = (H && h * RH + q < RL && wv >= 4) ? Ah[(h * RH + q) * (TT / 2) + (t & (TT / 2 - 1))] : 0.0;
 #pragma unroll
       for (int q = 0; q < RH; ++q) {
         const int i = I0 + h * RH + q;
@@ -621,25 +652,31 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
 #pragma unroll
         for (int q = 0; q < RH; ++q) {
           const int ii = h * RH + q;
-          if (m < K + SG) {
+          if (ii >= RL) continue;
+          if (m < K + SGH && H) {
+            hv[q] = __builtin_fma(-vr[q], p[m], __builtin_fma(-wr[q], vp[m], hv[q]));
+          } else if (m < K + SGH) {
             const int so = (m * R + I0 + ii) * TT * 8;
             const double ref = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rwm, soff[m - K], so, 0));
             const double nv = __builtin_fma(-vr[q], p[m], __builtin_fma(-wr[q], vp[m], ref));
             __builtin_amdgcn_raw_buffer_store_b64(
                 __builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(rwm, 0, 0, 0)), nv), rwm, soff[m - K], so, 0);
-          } else if (m < K + SG + SL) {
-            double& ref = lv[q][m - K - SG];
+          } else if (m < K + SGH + SL) {
+            double& ref = lv[q][m - K - SGH];
             ref = __builtin_fma(-vr[q], p[m], __builtin_fma(-wr[q], vp[m], ref));
           } else {
-            double& ref = Ar[ii][m - K - SG - SL];
+            double& ref = Ar[ii][m - K - SGH - SL];
             ref = __builtin_fma(-vr[q], p[m], __builtin_fma(-wr[q], vp[m], ref));
           }
         }
       }
 #pragma unroll
       for (int q = 0; q < RH; ++q)
+        if (h * RH + q < RL) {
 #pragma unroll
-        for (int m = 0; m < SL; ++m) Al[(m * RL + h * RH + q) * TT + t] = lv[q][m];
+          for (int m = 0; m < SL; ++m) Al[(m * RL + h * RH + q) * TT + t] = lv[q][m];
+          if (H && wv >= 4) Ah[(h * RH + q) * (TT / 2) + (t & (TT / 2 - 1))] = hv[q];
+        }
     }
     if (trace) trace[j * 8 + 7] = (int64_t)__builtin_amdgcn_s_memrealtime();
 #pragma unroll
@@ -653,10 +690,13 @@ __global__ __launch_bounds__(TT, 1) void k_trd(TrdArgs a) {
     for (int ii = 0; ii < RL; ++ii) {
 #pragma unroll
       for (int m = K + SG; m < S; ++m) {
-        if (m < K + SG + SL)
-          wm(m, I0 + ii, t0) = Al[((m - K - SG) * RL + ii) * TT + t0];
-        else
-          wm(m, I0 + ii, t0) = Ar[ii][m - K - SG - SL];
+        if (m < K + SGH) {  // H: slot K's live lanes (range 1 no longer reads slot K)
+          if (t0 >= TT / 2) wm(m, I0 + ii, t0) = Ah[ii * (TT / 2) + t0 - TT / 2];
+        } else if (m < K + SGH + SL) {
+          wm(m, I0 + ii, t0) = Al[((m - K - SGH) * RL + ii) * TT + t0];
+        } else {
+          wm(m, I0 + ii, t0) = Ar[ii][m - K - SGH - SL];
+        }
       }
     }
   } else if (lastrow == n - 1 && n > 1) {
@@ -1416,16 +1456,17 @@ __global__ __launch_bounds__(256, 1) void k_bt_fused(const double* __restrict__ 
   }
 }
 
-template <int R, int S, int K, int SG, int SL>
+template <int R, int S, int K, int SG, int SL, int H = 0>
 static hipError_t launch_trd_t(const TrdArgs& a, hipStream_t st) {
-  constexpr int I0 = (2 * K < R) ? 2 * K : R;
-  const size_t lds = ((size_t)SL * (R - I0) * TT + 16 + 4 + 4 * R + 8 * (R + 2) + R) * sizeof(double);
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_trd<R, S, K, SG, SL>),
+  constexpr int I0 = H ? 1 : ((2 * K < R) ? 2 * K : R);
+  const size_t lds = ((size_t)SL * (R - I0) * TT + (size_t)H * (R - I0) * (TT / 2) + 16 + 4 + 4 * R + 8 * (R + 2) + R) *
+                     sizeof(double);
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_trd<R, S, K, SG, SL, H>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  e = check_persistent(reinterpret_cast<const void*>(&k_trd<R, S, K, SG, SL>), TT, lds, a.G, st);
+  e = check_persistent(reinterpret_cast<const void*>(&k_trd<R, S, K, SG, SL, H>), TT, lds, a.G, st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_trd<R, S, K, SG, SL>), dim3(a.G), dim3(TT), lds, st, a);
+  hipLaunchKernelGGL((k_trd<R, S, K, SG, SL, H>), dim3(a.G), dim3(TT), lds, st, a);
   return hipGetLastError();
 }
 
@@ -1534,7 +1575,10 @@ hipError_t launch_trd_ranges(const TrdArgs& a, int R, int kb, int ke, hipStream_
       PODS_TRD(8, 4, 3, 0, 0);
       break;
     case 16:
+      // range 0 in two launches: columns [0, 256) with slot 0 in the L2 slab, [256, 511) with
+      // the live half of slot 0 in LDS (r6)
       PODS_TRD(16, 8, 0, 1, 2);
+      if (e == hipSuccess && 0 <= a.klast && kb <= 0 && 0 <= ke) e = launch_trd_t<16, 8, 0, 0, 2, 1>(a, st);
       PODS_TRD(16, 8, 1, 0, 2);
       PODS_TRD(16, 8, 2, 0, 2);
       PODS_TRD(16, 8, 3, 0, 1);
