@@ -558,9 +558,10 @@ class SpectrumQueue:
     stage-1 groups, 1024-sweep chase ranges and the bisection: 17 units at ns = 8192), so the
     spectrum spreads over ranks 1..N-1 instead of one owner solving a whole step at once."""
 
-    # per-unit time (ms) of k_trd column ranges 0..7 and the bisection at ns = 4096
-    # (profiles/r3/c3_kernel_stats.csv); used only to even out the per-step load
-    UNIT_MS = [7.8, 5.5, 4.6, 4.0, 3.0, 2.9, 2.5, 2.2, 1.6]
+    # per-unit time (ms) of k_trd column ranges 0..7 and the bisection at ns = 4096 (r6: 512
+    # columns x the per-column times of profiles/r6/trd_trace_range0_split.log; r3's were 7.8, 5.5,
+    # 4.6, 4.0, 3.0, 2.9, 2.5, 2.2); used only to even out the per-step load
+    UNIT_MS = [5.5, 4.1, 3.5, 3.4, 3.0, 2.65, 2.6, 2.4, 1.6]
     # rank 0's own extra work per step at ns = 4096 (leading pairs 5.0, DFT + ranking ~1 ms)
     LEAD_MS = 6.0
 
