@@ -51,6 +51,8 @@ for r in range(rounds):
             elif not torch.equal(C, ref):
                 print("config %s: C differs from the first configuration" % v, flush=True)
     print("round %d: %s" % (r, "  ".join("%s %.2f" % (v, res[v][-1]) for v in configs)), flush=True)
+import hashlib  # noqa: E402
+print("C sha1 %s (lib %s)" % (hashlib.sha1(C.cpu().numpy().tobytes()).hexdigest()[:16], os.environ.get("PODSGEN_LIB", "product")), flush=True)
 for v in configs:
     x = sorted(res[v])
     med = x[len(x) // 2]
