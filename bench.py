@@ -432,13 +432,17 @@ def main():
         return
     # several ranks: the nm leading eigenpairs on the critical path (subspace iteration), the
     # rest of the spectrum spread over the ranks' following steps (engine.SpectrumQueue)
-    split = (world > 1 or os.environ.get("PODS_EIGEN") == "split") and ns >= E.SPLIT_MIN_N
+    # PODS_N1_PIPELINE=1 (measurement): one GPU through the same pipelined runner as N > 1 (the
+    # leading-pair solve of step k-1 beside step k's generation and correlation, the spectrum
+    # units behind them) instead of the fused per-step solver
+    n1pipe = world == 1 and os.environ.get("PODS_N1_PIPELINE") == "1"
+    split = (world > 1 or n1pipe or os.environ.get("PODS_EIGEN") == "split") and ns >= E.SPLIT_MIN_N
     spectrum = E.SpectrumQueue(gen.ctx, ns, rank, world) if split else None
 
     # several ranks: step k-1's POD tail (rank 0's leading-pair solve, broadcasts, spatial modes)
     # runs while the device has step k's generation and correlation (engine.ShardedSteps, two
     # snapshot banks; PODS_PIPELINE=0 runs each tail right after its own all-reduce)
-    runner = E.ShardedSteps(setup, gen, d, spectrum) if world > 1 else None
+    runner = E.ShardedSteps(setup, gen, d, spectrum) if world > 1 or n1pipe else None
 
     def step(timer=None, backlog=None, ahead=False):
         if runner is not None:

@@ -543,152 +543,6 @@ __device__ __forceinline__ void syrk_tile(const int8_t* __restrict__ base, int64
       }
 }
 
-// Register-staged form (r6 A/B, PODS_SYRK_RS): the same tile, ring and fragment layout, but past
-// the prologue each wave moves its pieces of the ring as global_load_dwordx4 into registers (one
-// K step ahead) + ds_write_b128 into the slot freed at this step's barrier, instead of LDS-DMA
-// pieces (60-185 cycles of issue each, MI355X_MICROARCH.md).  The A fragments of step t+1 are read
-// row by row into the registers step t's row just used (one A set instead of two) to pay for the
-// staging registers.
-template <int NST, bool SAME>
-__device__ __forceinline__ void syrk_tile_rs(const int8_t* __restrict__ base, int64_t cstride, int ns, int nt, int i0,
-                                             int j0, int m, char* smem, uint8_t* __restrict__ dst, int ldp,
-                                             int accumulate) {
-  constexpr int STG = 2 * PANEL;
-  constexpr int Q = SAME ? 2 : 4;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  int xo[2], yo[2];  // < ns * 64 bytes
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int rw = (wave * 2 + q) * 16 + (lane >> 2);
-    const int ls = (lane & 3) ^ swz((rw >> 2) & 3);
-    xo[q] = min(i0 + rw, ns - 1) * KC + ls * 16;
-    yo[q] = min(j0 + rw, ns - 1) * KC + ls * 16;
-  }
-  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
-  auto src = [&](int t, int q) {
-    return base + (int64_t)t * cstride + (q < 2 ? xo[q] : yo[q - 2]);
-  };
-  auto dsto = [&](int q) { return q < 2 ? (wave * 2 + q) * 1024 : PANEL + (wave * 2 + q - 2) * 1024; };
-  i32x4 sv[Q];
-  auto gload = [&](int t) {
-#pragma unroll
-    for (int q = 0; q < Q; ++q) sv[q] = *reinterpret_cast<const i32x4*>(src(t, q));
-  };
-  auto swrite = [&](int t) {
-    char* sb = smem + (t % NST) * STG + lane * 16;
-#pragma unroll
-    for (int q = 0; q < Q; ++q) *reinterpret_cast<i32x4*>(sb + dsto(q)) = sv[q];
-  };
-  i32x4 acc[8][4];
-#pragma unroll
-  for (int a = 0; a < 8; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = (i32x4){0, 0, 0, 0};
-  const int wr = wave >> 2, wc = wave & 3;
-  const bool idle = SAME && wr == 0 && wc >= 2;
-  const int fo = (lane & 15) * KC + (((lane >> 4) ^ swz((lane >> 2) & 3)) * 16);
-  auto arow = [&](int t, int a) {
-    return *reinterpret_cast<const i32x4*>(smem + (t % NST) * STG + wr * 128 * KC + fo + a * 16 * KC);
-  };
-  auto bread = [&](int t, i32x4 (&bv)[4]) {
-    const char* Y = smem + (t % NST) * STG + (SAME ? 0 : PANEL) + wc * 64 * KC + fo;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) bv[b] = *reinterpret_cast<const i32x4*>(Y + b * 16 * KC);
-  };
-  // prologue: stages 0 .. NST-1 by LDS-DMA, stage NST into registers
-  for (int t = 0; t < NST && t < nt; ++t) {
-    const uint32_t sb = lds0 + (uint32_t)((t % NST) * STG);
-#pragma unroll
-    for (int q = 0; q < Q; ++q) dma16(src(t, q), sb + dsto(q));
-  }
-  if (NST < nt) {
-    gload(NST);
-    wait_vm<Q>();
-  } else {
-    wait_vm<0>();
-  }
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-  i32x4 av[8], b0[4], b1[4];
-  if (!idle) {
-#pragma unroll
-    for (int a = 0; a < 8; ++a) av[a] = arow(0, a);
-    bread(0, b0);
-  }
-  auto fold = [&](int t) {
-    if ((t + 1) % FOLD == 0 && t + 1 < nt) {
-#pragma unroll
-      for (int a = 0; a < 8; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[a][b][r] %= m;
-    }
-  };
-  // step t: this wave's reads of stage t+1 done (lgkmcnt 0), one barrier (every wave's reads of
-  // slot t % NST -- stage t -- are then done), rows 0-3 of step t's MFMAs with stage t+1's A rows
-  // read behind them, the staged stage t + NST written into slot t % NST and stage t + NST + 1
-  // loaded, rows 4-7
-  auto step = [&](int t, const i32x4 (&bc)[4], i32x4 (&bn)[4]) {
-    if (t + 1 < nt) {
-      __builtin_amdgcn_s_waitcnt(0xC07F);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (!idle) {
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-#pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[a], bc[b], acc[a][b], 0, 0, 0);
-        av[a] = arow(t + 1, a);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    if (!idle) bread(t + 1, bn);  // (past the last step: a stale slot, never used)
-    if (t + NST < nt) {
-      swrite(t + NST);
-      if (t + NST + 1 < nt) gload(t + NST + 1);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (!idle) {
-#pragma unroll
-      for (int a = 4; a < 8; ++a) {
-#pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[a], bc[b], acc[a][b], 0, 0, 0);
-        av[a] = arow(t + 1, a);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      fold(t);
-    }
-  };
-  int t = 0;
-  for (; t + 1 < nt; t += 2) {
-    step(t, b0, b1);
-    step(t + 1, b1, b0);
-  }
-  if (t < nt) step(t, b0, b1);
-  const int fr = lane & 15, fq = lane >> 4;
-#pragma unroll
-  for (int a = 0; a < 8; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gi = i0 + wr * 128 + a * 16 + 4 * fq + r;
-        const int gj = j0 + wc * 64 + b * 16 + fr;
-        if (gi < ns && gj <= gi) {
-          int v = acc[a][b][r] % m;
-          if (v < 0) v += m;
-          uint8_t* p = dst + (int64_t)gi * ldp + gj;
-          if (accumulate) {
-            v += *p;
-            if (v >= m) v -= m;
-          }
-          *p = (uint8_t)v;
-        }
-      }
-}
-
 #ifdef PODS_DIAG
 // The launch-per-item grid form (r4; the persistent kernel replaced it in r5) and its
 // measurement-only variants (DIAG: wrong results): the diagnostic library only (tools/lib_variants.sh
@@ -729,9 +583,6 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8(const int8_t* __restrict__ R
 // launch-per-item form let them drift apart over the 17 rounds at C3, and the XCD's 4 MB L2 held
 // the union of their windows: 54 % hits).  5-stage ring, the DMA pieces among the first MFMA rows
 // (ILV 1), one more stage in flight (LD 1).
-#ifndef PODS_SYRK_RS
-#define PODS_SYRK_RS 0
-#endif
 template <int NST, int ILV, int LD>
 __global__ __launch_bounds__(512, 1) void k_syrk_i8_paced(const int8_t* __restrict__ R, int ns, int64_t ms, int64_t cs,
                                                           int kcs, const int4* __restrict__ xitems, int per_xcd,
@@ -752,17 +603,10 @@ __global__ __launch_bounds__(512, 1) void k_syrk_i8_paced(const int8_t* __restri
       const int8_t* base = R + (int64_t)l * ms + (int64_t)sp * kcs * cs;
       uint8_t* dst = P + (int64_t)(l * nsplit + sp) * pslab;
       const int m = modulus(l);
-      if constexpr (PODS_SYRK_RS) {
-        if (bi == bj)
-          syrk_tile_rs<NST, true>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
-        else
-          syrk_tile_rs<NST, false>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
-      } else {
-        if (bi == bj)
-          syrk_tile<NST, 0, true, ILV, LD>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
-        else
-          syrk_tile<NST, 0, false, ILV, LD>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
-      }
+      if (bi == bj)
+        syrk_tile<NST, 0, true, ILV, LD>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
+      else
+        syrk_tile<NST, 0, false, ILV, LD>(base, cs, ns, kcs, bi * TB, bj * TB, m, smem, dst, ldp, accumulate);
     }
     pace_xcd(ctr, epoch, nslot);
   }

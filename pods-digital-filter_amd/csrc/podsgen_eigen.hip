@@ -1555,6 +1555,22 @@ hipError_t launch_trd(const TrdArgs& a, int R, hipStream_t st) { return launch_t
 // its own launch and leaves the live block parked in a.Wm, so a caller may run the ranges of
 // one matrix in separate calls (with other work on the stream between them) as long as the
 // workspace of TrdArgs is left alone in between.
+// LDS slots of ranges 2-5 of the 16-row plan (variant builds: -DPODS_TRD_SL3=...).  r6: range 3
+// with none (204 VGPRs, no spill) instead of one -- pods_syev 31.09 -> 30.83 ms, the C3 step
+// 69.02 -> 68.78 ms; range 2 with 3 slots and ranges 4-5 with one measured slower
+// (profiles/r6/trd_range_slots_ab.log)
+#ifndef PODS_TRD_SL2
+#define PODS_TRD_SL2 2
+#endif
+#ifndef PODS_TRD_SL3
+#define PODS_TRD_SL3 0
+#endif
+#ifndef PODS_TRD_SL4
+#define PODS_TRD_SL4 0
+#endif
+#ifndef PODS_TRD_SL5
+#define PODS_TRD_SL5 0
+#endif
 hipError_t launch_trd_ranges(const TrdArgs& a, int R, int kb, int ke, hipStream_t st) {
   using namespace eig;
   hipError_t e = hipSuccess;
@@ -1580,10 +1596,10 @@ hipError_t launch_trd_ranges(const TrdArgs& a, int R, int kb, int ke, hipStream_
       PODS_TRD(16, 8, 0, 1, 2);
       if (e == hipSuccess && 0 <= a.klast && kb <= 0 && 0 <= ke) e = launch_trd_t<16, 8, 0, 0, 2, 1>(a, st);
       PODS_TRD(16, 8, 1, 0, 2);
-      PODS_TRD(16, 8, 2, 0, 2);
-      PODS_TRD(16, 8, 3, 0, 1);
-      PODS_TRD(16, 8, 4, 0, 0);
-      PODS_TRD(16, 8, 5, 0, 0);
+      PODS_TRD(16, 8, 2, 0, PODS_TRD_SL2);
+      PODS_TRD(16, 8, 3, 0, PODS_TRD_SL3);
+      PODS_TRD(16, 8, 4, 0, PODS_TRD_SL4);
+      PODS_TRD(16, 8, 5, 0, PODS_TRD_SL5);
       PODS_TRD(16, 8, 6, 0, 0);
       PODS_TRD(16, 8, 7, 0, 0);
       break;

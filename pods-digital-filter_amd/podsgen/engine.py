@@ -391,7 +391,7 @@ class Generator:
     def prefetch_planes_beside_solver(self, timer=None):
         """Enqueue the NEXT run's random planes on the gen stream behind the marker the current
         pods_syev records after tridiagonalisation range 2 (pods_syev_marker): from range 3 on
-        the k_trd workgroups hold at most 192 VGPRs per wave (2 waves per SIMD) and <= 42 KB of
+        the k_trd workgroups hold at most 204 VGPRs per wave (2 waves per SIMD) and <= 42 KB of
         LDS, so the MT generator (16 VGPRs; LDS padded to 55 KB so at most 2 of its workgroups
         share a CU, PODS_GEN_BESIDE_SOLVER) runs beside them and every later range still finds
         room on every CU whatever the dispatch order.  Measured against a marker after range 3
@@ -1357,6 +1357,11 @@ class ShardedSteps:
         if prefetch_next:
             self.gen.prefetch_jump(timer)
         C, mean = pod_head(snap, self.world, timer, partial=self.collectives)
+        # without a collective nothing else orders rank 0's solve stream behind this correlation
+        c_done = None
+        if not self.collectives:
+            c_done = torch.cuda.Event()
+            c_done.record()
         if self.pending is not None:
             self._tail(timer)
         check(ctx.lib.pods_select_snapshots(ctx.h, bank), "pods_select_snapshots")
@@ -1376,13 +1381,13 @@ class ShardedSteps:
                 work.wait()
                 packed.record_stream(torch.cuda.current_stream(ctx.device))
                 unpack(packed, C)
-        self.pending = [bank, snap, C, mean, finish]
+        self.pending = [bank, snap, C, mean, finish, c_done]
         self.k += 1
         if not self.pipelined:
             self._tail(timer)
 
     def _tail(self, timer):
-        bank, snap, C, mean, finish = self.pending
+        bank, snap, C, mean, finish, c_done = self.pending
         self.pending = None
         ctx = self.gen.ctx
         solve = self._solve_stream() if self.rank == 0 else None
@@ -1398,6 +1403,8 @@ class ShardedSteps:
             # beside the generator and the paced SYRK they only share the CUs.
             if self._spec_done is not None:
                 solve.wait_event(self._spec_done)
+            if c_done is not None:   # no collective: the correlation itself, on the main stream
+                solve.wait_event(c_done)
             with ctx.on_stream(solve):
                 if finish is not None:
                     finish()

@@ -346,6 +346,52 @@ def test_world1_collective_paths_rccl_and_gloo_bit_equal():
                 assert np.array_equal(x, y)
 
 
+def test_one_gpu_pipelined_steps_bit_equal():
+    """on ONE device (no process group) the pipelined runner -- step k's
+    generation into snapshot bank k % 2, mean and correlation enqueued before step k-1's tail (the
+    leading-pair solve on its own stream beside them, the spectrum units and spatial modes of
+    step k-1 from the other bank, the Fourier stage) -- gives every step's mean, T, Phi, nm,
+    spectrum and Fourier counts / FC rows bit-equal to the same steps run one after the other
+    (pipelined=False, bank 0), over three seeds whose results differ."""
+    import podsgen
+    from podsgen import engine as E
+    s = podsgen.DFSetup(jma=48, kma=40, ns=1024, seed=PIPE_SEEDS[0])
+    res = {}
+    for pipelined in (True, False):
+        gen = E.Generator(s, device=0)
+        spectrum = E.SpectrumQueue(gen.ctx, s.ns, 0, 1)
+        backlog = E.FourierBacklog()
+        run = E.ShardedSteps(s, gen, None, spectrum, backlog, pipelined=pipelined)
+        assert run.world == 1 and not run.collectives
+        for seed in PIPE_SEEDS:
+            run.step(seed=seed)
+        run.flush()
+        backlog.flush()
+        spectrum.drain()
+        torch.cuda.synchronize()
+        res[pipelined] = dict(
+            T=[p.T.cpu().numpy() for p in run.results], phi=[p.phi.cpu().numpy() for p in run.results],
+            mean=[p.mean.cpu().numpy() for p in run.results], nm=[p.nm for p in run.results],
+            spectra=spectrum.results(),
+            fc=[None if f is None else (f.c, f.c_count, f.FC) for f in backlog.results])
+        gen.ctx.close()
+    a, b = res[True], res[False]
+    assert a["nm"] == b["nm"]
+    for key in ("T", "phi", "mean"):
+        assert len(a[key]) == len(PIPE_SEEDS)
+        for k in range(len(PIPE_SEEDS)):
+            assert np.array_equal(a[key][k], b[key][k]), (key, k)
+        assert not np.array_equal(a[key][0], a[key][1]), key
+    assert sorted(a["spectra"]) == sorted(b["spectra"]) == list(range(len(PIPE_SEEDS)))
+    for k in a["spectra"]:
+        assert np.array_equal(a["spectra"][k], b["spectra"][k]), k
+    assert len(a["fc"]) == len(b["fc"]) == len(PIPE_SEEDS)
+    for fa, fb in zip(a["fc"], b["fc"]):
+        assert fa is not None and fb is not None
+        for x, y in zip(fa, fb):
+            assert np.array_equal(x, y)
+
+
 def _tiny_worker(rank, world, port, out):
     import torch.distributed as dist
     import podsgen
