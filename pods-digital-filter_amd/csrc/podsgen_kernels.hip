@@ -1293,14 +1293,27 @@ __global__ void k_temporal_scale(const double* __restrict__ V, int64_t v_rs, int
 // group ahead of the FMAs.  T is staged through LDS (broadcast reads).  KS > 1 writes
 // partial sums part[ks][r][m] that k_spatial_reduce folds in a fixed order.
 // -----------------------------------------------------------------------------------------
+// r6: 4 snapshots per load group (142 VGPRs, 3 waves per SIMD) instead of 8 (210, 2 waves): 1.28 vs
+// 1.31 ms for pods_spatial_modes at C3, Phi bit-identical; 128- or 256-snapshot T chunks, 16 per
+// group, 3 waves forced at 8, and the next chunk's first group loaded across the chunk barriers
+// measured equal or slower (profiles/r6/spatial_variants_ab.log; variant builds: -DPODS_SPATIAL_*)
+#ifndef PODS_SPATIAL_U
+#define PODS_SPATIAL_U 4
+#endif
+#ifndef PODS_SPATIAL_CH
+#define PODS_SPATIAL_CH 64
+#endif
+#ifndef PODS_SPATIAL_WPE
+#define PODS_SPATIAL_WPE 1
+#endif
 template <int NMB>
-__global__ __launch_bounds__(256) void k_spatial_modes(const double* __restrict__ AT, int64_t rowlen,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PODS_SPATIAL_WPE))) void k_spatial_modes(const double* __restrict__ AT, int64_t rowlen,
                                                        int ns, const double* __restrict__ mean,
                                                        const double* __restrict__ T, int ldT, int col0,
                                                        int nm, const double* __restrict__ inv_lam,
                                                        double* __restrict__ phi, int ldphi, int chunk,
                                                        double* __restrict__ part) {
-  constexpr int CH = 64, U = 8;
+  constexpr int CH = PODS_SPATIAL_CH, U = PODS_SPATIAL_U;
   __shared__ __attribute__((aligned(16))) double Ts[CH][NMB];
   const int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
   const int64_t rowpad = (rowlen + 15) & ~(int64_t)15;
