@@ -1080,13 +1080,16 @@ __global__ __launch_bounds__(256) void k_twisted(const double* __restrict__ D,
         for (int w = 1; w < 4; ++w)
           if (rv[w] < rv[best] || (rv[w] == rv[best] && ri[w] < ri[best])) best = w;
         scr[8] = ri[best];
-        g[(int)ri[best]] = DBL_MAX;  // excluded from later rounds
+        const int ib = (int)ri[best];
+        if (ib >= 0 && ib < n) g[ib] = DBL_MAX;  // excluded from later rounds
       }
       __syncthreads();
     }
   }
   __syncthreads();
-  const int r = (int)scr[8];
+  // (no finite |gamma| -- a NaN input -- leaves the argmin at -1 or n: clamped, so garbage in
+  // gives garbage out, never an access outside the vectors)
+  const int r = min(max((int)scr[8], 0), n - 1);
   // multipliers in place: L+_i = e_i / D+_i at dp[i], U-_i = e_i / D-_{i+1} at dm[i+1]
   for (int i = t; i < n - 1; i += 256) {
     dp[i] = se[i] / dp[i];
