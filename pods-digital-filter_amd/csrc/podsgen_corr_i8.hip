@@ -336,8 +336,11 @@ __device__ __forceinline__ void residues_body(const double* __restrict__ AT, int
     const double* __restrict__ mean, const double* __restrict__ devmax, int bbits, int64_t kc0, int64_t nkc, \
     int8_t* __restrict__ R, int64_t ms, int64_t cs
 #define PODS_RES_PASS AT, ns, rowlen, rowpad, mean, devmax, bbits, kc0, nkc, R, ms, cs
+#ifndef PODS_RES_WPE
+#define PODS_RES_WPE 3
+#endif
 template <int V>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) void k_residues(PODS_RES_ARGS) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, PODS_RES_WPE))) void k_residues(PODS_RES_ARGS) {
   residues_body<V>(PODS_RES_PASS);
 }
 #undef PODS_RES_ARGS
