@@ -336,6 +336,8 @@ __device__ __forceinline__ void residues_body(const double* __restrict__ AT, int
     const double* __restrict__ mean, const double* __restrict__ devmax, int bbits, int64_t kc0, int64_t nkc, \
     int8_t* __restrict__ R, int64_t ms, int64_t cs
 #define PODS_RES_PASS AT, ns, rowlen, rowpad, mean, devmax, bbits, kc0, nkc, R, ms, cs
+// (r6: a cap of 4, 5 or 8 waves per SIMD instead of 3 -- 90-102 VGPRs -- left the whole pods_corr
+// at 26.0-26.2 ms either way, profiles/r6/residues_occupancy_ab.log: the pass is VALU-bound)
 #ifndef PODS_RES_WPE
 #define PODS_RES_WPE 3
 #endif
