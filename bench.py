@@ -545,9 +545,12 @@ def main():
                                                 "%.1f TFLOP/s fp64 MFMA peak by construction" % FP64_MFMA_PEAK_TFLOPS),
                     "bound_note": ("the int8 pipe is fed by LDS-DMA: 214 GB L2->LDS per launch at C3; measured "
                                    "(DESIGN.md s3): MFMAs alone 16.9 ms (the chip holds ~1.7-1.94 GHz under "
-                                   "this load), the kernel with an L2-resident K window 19.3 ms; MFMA pipe "
-                                   "busy 66 % of the r4 kernel; r5: one persistent workgroup per CU, the 32 "
-                                   "of an XCD paced round by round over the same panels")}
+                                   "this load), the kernel with an L2-resident K window 19.3 ms; r6: "
+                                   "SQ_VALU_MFMA_BUSY_CYCLES = 16 x the MFMA count, pipe busy 0.645 at the "
+                                   "1.66 GHz held under the profiler; MFMAs + fragment reads alone 17.3 ms, "
+                                   "operand traffic alone 20.6 ms (profiles/r6/syrk_mfma_calibration.json, "
+                                   "syrk_diag_ab.log); one persistent workgroup per CU, the 32 of an XCD paced "
+                                   "round by round over the same panels")}
     else:
         achieved = flops / (corr_ms * 1e-3) / 1e12
         roofline = {"kernel": "pods_corr (k_syrk_g128 + k_syrk_reduce), rank 0",
