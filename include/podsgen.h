@@ -257,6 +257,12 @@ int pods_syev_flags_async(pods_ctx* ctx, uint32_t* flags_host);
  * leave registers and LDS free (PODS_GEN_BESIDE_SOLVER). */
 int pods_syev_marker(pods_ctx* ctx, int after_range);
 int pods_stream_wait_marker(pods_ctx* ctx, void* stream);
+/* The same behind the whole tridiagonalisation of the next pods_syev (where = 0: before its
+ * bisection, eigenvectors and back-transformation) or behind its eigenvalues (where = 1: before
+ * the eigenvectors and back-transformation): the next run's x pass can start there (scheduling
+ * plumbing, no reference counterpart). */
+int pods_syev_marker_tail(pods_ctx* ctx, int where);
+int pods_stream_wait_marker_tail(pods_ctx* ctx, void* stream);
 
 /* All n eigenvalues of C alone (the full spectrum POD.eigenvalues.dat and the valid-mode count
  * consume, PODFS.py:1309-1320, :1339), as a sequence of stream-ordered units that a caller can

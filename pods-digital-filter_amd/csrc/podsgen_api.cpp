@@ -312,6 +312,10 @@ struct pods_ctx {
   hipEvent_t marker = nullptr;
   int marker_after = -1;
   bool marker_recorded = false;
+  // the same behind the whole tridiagonalisation (pods_syev_marker_tail)
+  hipEvent_t marker_tail = nullptr;
+  bool marker_tail_req = false, marker_tail_recorded = false;
+  int marker_tail_where = 0;  // 0: behind the tridiagonalisation, 1: behind the eigenvalues
   // pods_set_shared_device: the per-device lock file persistent launches hold (-1: not shared)
   int lock_fd = -1;
   // pods_corr: 1 = exact int8-MFMA modular products + CRT (podsgen_corr_i8.hip), 0 = fp64 MFMA
@@ -525,6 +529,7 @@ int pods_destroy(pods_ctx* c) {
     (void)hipHostFree(c->pin);
   }
   if (c->marker) (void)hipEventDestroy(c->marker);
+  if (c->marker_tail) (void)hipEventDestroy(c->marker_tail);
   if (c->lock_fd >= 0) (void)close(c->lock_fd);
   delete c;
   return PODS_OK;
@@ -874,8 +879,13 @@ int pods_df_generate_parts(pods_ctx* c, int parts) {
     int64_t nch = (256LL * 2048 + pts - 1) / pts;
     nch = std::max<int64_t>(1, std::min<int64_t>(nch, std::max(1, p.ns / 16)));
     const int chunk = (int)((p.ns + nch - 1) / nch);
+    // beside the eigensolver's tail (PODS_GEN_BESIDE_SOLVER): 2 workgroups per CU, so the
+    // latency-bound bisection / eigenvector / back-transformation kernels keep room on every CU
+    int cus = 0, dev = 0;
+    if ((parts & PODS_GEN_BESIDE_SOLVER) && hipGetDevice(&dev) == hipSuccess)
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     PODS_HIP(pods::launch_filter_x(c->NX, c->R.as<double>(), taps, p.ns, c->Sl, 3, chunk,
-                                   c->T1.as<double>(), c->stream));
+                                   c->T1.as<double>(), c->stream, 0, -1, 2 * cus));
   }
   if (parts & PODS_GEN_YZPASS) {
     PODS_HIP(pods::launch_filter_yz(c->NY, c->T1.as<double>(), taps + c->NX, taps + c->NX + c->NY,
@@ -1418,6 +1428,12 @@ int run_sytrd(pods_ctx* c, const double* C, int n, int* R_out, int64_t* trace = 
   } else {
     PODS_HIP(pods::launch_trd(a, R, c->stream));
   }
+  c->marker_tail_recorded = false;
+  if (c->marker_tail_req && c->marker_tail && c->marker_tail_where == 0) {
+    PODS_HIP(hipEventRecord(c->marker_tail, c->stream));
+    c->marker_tail_recorded = true;
+    c->marker_tail_req = false;
+  }
   *R_out = R;
   return PODS_OK;
 }
@@ -1661,6 +1677,11 @@ int pods_syev(pods_ctx* c, const double* C, int n, int nvec, double* lam_desc, d
   PODS_HIP(ensure(c->e_cnt, pods::tri_grid_bytes()));
   int* gcnt = c->e_cnt.as<int>();
   PODS_HIP(pods::launch_tri_eigvals(D, E, n, bounds, lam_desc, gcnt, c->stream));
+  if (c->marker_tail_req && c->marker_tail) {  // pods_syev_marker_tail(ctx, 1): behind the eigenvalues
+    PODS_HIP(hipEventRecord(c->marker_tail, c->stream));
+    c->marker_tail_recorded = true;
+  }
+  c->marker_tail_req = false;
   if (nvec > 0) {
     const int nblk = std::max((n - 1 + 63) / 64, 1);
     PODS_HIP(ensure(c->e_inv, (size_t)nvec * n * sizeof(double)));
@@ -1786,6 +1807,26 @@ int pods_syev_marker(pods_ctx* c, int after_range) {
   if (int e = check_ctx(c)) return e;
   if (!c->marker) PODS_HIP(hipEventCreateWithFlags(&c->marker, hipEventDisableTiming));
   c->marker_after = after_range;
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_syev_marker_tail(pods_ctx* c, int where) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (where != 0 && where != 1) return fail(PODS_ERR_ARG, "pods_syev_marker_tail: where must be 0 or 1");
+  if (!c->marker_tail) PODS_HIP(hipEventCreateWithFlags(&c->marker_tail, hipEventDisableTiming));
+  c->marker_tail_req = true;
+  c->marker_tail_where = where;
+  return PODS_OK;
+  PODS_CATCH
+}
+
+int pods_stream_wait_marker_tail(pods_ctx* c, void* stream) {
+  PODS_TRY
+  if (int e = check_ctx(c)) return e;
+  if (!c->marker_tail_recorded) return fail(PODS_ERR_STATE, "the last pods_syev recorded no tail marker");
+  PODS_HIP(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), c->marker_tail, 0));
   return PODS_OK;
   PODS_CATCH
 }

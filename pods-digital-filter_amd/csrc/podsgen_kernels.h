@@ -27,8 +27,10 @@ hipError_t launch_mt_chains(int mode, const uint32_t* st0, const int64_t* b0, co
                             const int64_t* rec_block, const int* rec_slot, const int* rec_first, uint32_t* rec_out,
                             int64_t ntot, int64_t S, int Kp, int rlo, int rhi, int64_t Sl, double low, double range,
                             double* out, hipStream_t st);
+// max_grid > 0: at most that many workgroups (each then takes several virtual blocks): the x pass
+// beside the eigensolver's tail keeps to a few waves per CU
 hipError_t launch_filter_x(int NX, const double* R, const double* bx, int ns, int64_t Sl, int ncomp,
-                           int chunk, double* T1, hipStream_t st, int s0 = 0, int s1 = -1);
+                           int chunk, double* T1, hipStream_t st, int s0 = 0, int s1 = -1, int max_grid = 0);
 // lund_sj: 0 = one row of 9 x K parameters for every j (plain layout lund[e * Pl + k]);
 // otherwise the table is j-varying and in the chunk-major layout below
 inline int64_t lund_chunk_index(int64_t j, int e, int k, int K) {

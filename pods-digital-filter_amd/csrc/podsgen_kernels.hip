@@ -1469,7 +1469,7 @@ hipError_t launch_mt_generate(const uint32_t* states, int G, int64_t Bs, int64_t
 
 template <int NX>
 static hipError_t launch_fx(const double* R, const double* bx, int ns, int64_t Sl, int ncomp,
-                            int chunk, double* T1, hipStream_t st, int s0, int s1) {
+                            int chunk, double* T1, hipStream_t st, int s0, int s1, int max_grid) {
   if (Sl % 2 == 0 && ((uintptr_t)R & 15) == 0 && ((uintptr_t)T1 & 15) == 0) {
     const int nsr = s1 - s0;  // steps of this launch
     // point pairs: half the threads, so twice the step chunks keep the same parallelism
@@ -1483,7 +1483,7 @@ static hipError_t launch_fx(const double* R, const double* bx, int ns, int64_t S
     const int chunk2 = (int)((nsr + nch0 - 1) / nch0);
     const int nch = (nsr + chunk2 - 1) / chunk2;
     const int64_t nvb = bx_ * ncomp * nch;
-    const int64_t grid = nvb;
+    const int64_t grid = max_grid > 0 ? std::min<int64_t>(nvb, max_grid) : nvb;  // grid-stride over nvb
     // nontemporal plane loads / T1 stores: 8.15 vs 8.22 ms of main-stream generation at C3
     // (bench A/B, r4)
     hipLaunchKernelGGL((k_filter_x2<NX, 8, true>), dim3((unsigned)grid), dim3(256), 0, st, R, bx, ns, Sl, chunk2,
@@ -1498,12 +1498,12 @@ static hipError_t launch_fx(const double* R, const double* bx, int ns, int64_t S
 }
 
 hipError_t launch_filter_x(int NX, const double* R, const double* bx, int ns, int64_t Sl, int ncomp,
-                           int chunk, double* T1, hipStream_t st, int s0, int s1) {
+                           int chunk, double* T1, hipStream_t st, int s0, int s1, int max_grid) {
   if (s1 < 0) s1 = ns;
   switch (NX) {
 #define PODS_FX(n) \
   case n:          \
-    return launch_fx<n>(R, bx, ns, Sl, ncomp, chunk, T1, st, s0, s1);
+    return launch_fx<n>(R, bx, ns, Sl, ncomp, chunk, T1, st, s0, s1, max_grid);
     PODS_FX(1) PODS_FX(3) PODS_FX(5) PODS_FX(7) PODS_FX(9) PODS_FX(11) PODS_FX(13) PODS_FX(15)
     PODS_FX(17) PODS_FX(19) PODS_FX(21) PODS_FX(23) PODS_FX(25) PODS_FX(27) PODS_FX(29)
     PODS_FX(31) PODS_FX(33) PODS_FX(35) PODS_FX(37) PODS_FX(39) PODS_FX(41) PODS_FX(43)

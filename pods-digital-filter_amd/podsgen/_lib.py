@@ -77,6 +77,8 @@ SIGNATURES = {
     "pods_syev_flags_async": (c_int, [c_void_p, c_void_p]),
     "pods_syev_marker": (c_int, [c_void_p, c_int]),
     "pods_stream_wait_marker": (c_int, [c_void_p, c_void_p]),
+    "pods_syev_marker_tail": (c_int, [c_void_p, c_int]),
+    "pods_stream_wait_marker_tail": (c_int, [c_void_p, c_void_p]),
     "pods_cheb_prepare": (c_int, [c_void_p, c_void_p, c_int]),
     "pods_cheb_step": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_dbl, c_dbl, c_dbl,
                                c_void_p]),

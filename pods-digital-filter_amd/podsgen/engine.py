@@ -407,6 +407,14 @@ class Generator:
         # -2.2 ms on the main stream, the solver +2.5 ms and the DFT beside it twice as long)
         self._on_gen_stream(_lib.PODS_GEN_PLANES | _lib.PODS_GEN_BESIDE_SOLVER, timer, "gen_planes_ahead",
                             wait_main=False)
+        # and the next run's x pass, behind the solver's eigenvalues (pods_syev_marker_tail) with
+        # 2 workgroups per CU: beside the eigenvectors of T (20 workgroups), the back-transformation
+        # (64) and this run's modes, which leave most CUs idle -- the next generation on the main
+        # stream is then its y/z pass alone (PODS_XPASS_BESIDE, above)
+        if XPASS_BESIDE and self.ctx.lib.pods_stream_wait_marker_tail(
+                self.ctx.h, ctypes.c_void_p(gs.cuda_stream)) == _lib.PODS_OK:
+            self._on_gen_stream(_lib.PODS_GEN_XPASS | (_lib.PODS_GEN_BESIDE_SOLVER if XPASS_CAP else 0), timer,
+                                "gen_xpass_ahead", wait_main=False)
 
     def join_ahead(self):
         """Make the current stream wait for the prefetched jump-ahead (if any): called before the
@@ -478,6 +486,16 @@ SYEV_MAX_N = 4096   # pods_syev's on-chip limit (trd_plan)
 SYEV2_MAX_N = 16384  # pods_syev2 (two-stage): 64 panel workgroups x 256 rows
 SYEV_MAX_VEC = 64
 SPLIT_MIN_N = 1024   # below this the fused solve is cheaper than a 64-vector subspace iteration
+# the next run's x pass beside this run's eigensolver tail (see prefetch_planes_beside_solver):
+# PODS_XPASS_BESIDE = 4 (default): behind the eigenvalues, 2 workgroups per CU; 0: on the main
+# stream in the next generation; A/B values 1 / 2: behind the tridiagonalisation / the
+# eigenvalues with the full grid, 3: behind the tridiagonalisation with 2 workgroups per CU
+# (C3, profiles/r6/xpass_beside_ab.log: 69.1-69.4 / 69.1-69.3 / 68.8 / 68.6-68.7 / 68.05-68.1 ms
+# per step for 0 / 1 / 2 / 3 / 4)
+_XPB = os.environ.get("PODS_XPASS_BESIDE", "4")
+XPASS_BESIDE = _XPB in ("1", "2", "3", "4")
+XPASS_WHERE = 1 if _XPB in ("2", "4") else 0
+XPASS_CAP = _XPB in ("3", "4")
 SPLIT_MAX_VEC = 40   # leading pairs a 64-vector block resolves (nm <= 40; beyond, the fused solve)
 
 
@@ -879,6 +897,8 @@ def eigen_solve_speculative(ctx: Context, C, ns, nm, tol_CN, tm, beside=None):
     Y = torch.empty((ns, nm), dtype=torch.float64, device=dev)
     if beside is not None:   # a marker behind tridiagonalisation range 2 for beside()
         check(lib.pods_syev_marker(ctx.h, 2), "pods_syev_marker")
+        if XPASS_BESIDE:     # and one behind the whole tridiagonalisation (or its eigenvalues)
+            check(lib.pods_syev_marker_tail(ctx.h, XPASS_WHERE), "pods_syev_marker_tail")
     with tm("eigh"):
         check(lib.pods_syev(ctx.h, ptr(C), ns, nm, ptr(lam_t), ptr(Y)), "pods_syev")
     if beside is not None:

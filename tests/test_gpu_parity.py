@@ -266,15 +266,18 @@ def test_prefetched_generation_matches(ctx):
 def test_planes_prefetched_beside_solver(ctx):
     """ns > 2048: the next run's random planes start on the gen stream behind the marker of
     tridiagonalisation range 3 (Generator.prefetch_planes_beside_solver) while the solver's
-    late ranges run.  The next step's snapshot matrix and POD equal a plain run's bit for bit,
-    and no persistent kernel aborted (no fallback warning)."""
+    late ranges run, and (by default, engine.XPASS_BESIDE) its x pass behind the solver's
+    eigenvalues, beside the eigenvectors and back-transformation.  The next step's snapshot
+    matrix and POD equal a plain run's bit for bit, and no persistent kernel aborted (no
+    fallback warning)."""
     import warnings
     s = podsgen.DFSetup(jma=24, kma=20, ns=2560, seed=31)
     g1 = E.Generator(s, ctx=ctx)
     with warnings.catch_warnings(record=True) as w:
         warnings.simplefilter("always")
         E.pipeline(s, gen=g1, prefetch_next=True)
-        assert g1._ahead_parts == _lib.PODS_GEN_JUMP | _lib.PODS_GEN_PLANES
+        assert g1._ahead_parts == (_lib.PODS_GEN_JUMP | _lib.PODS_GEN_PLANES
+                                   | (_lib.PODS_GEN_XPASS if E.XPASS_BESIDE else 0))
         _, p2, f2 = E.pipeline(s, gen=g1)
         A2 = g1.snapshots().to_host()
     assert not [x for x in w if "podsgen" in str(x.message)], [str(x.message) for x in w]
