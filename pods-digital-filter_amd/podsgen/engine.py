@@ -355,7 +355,12 @@ class Generator:
         # prefetch_jump_early only the records (the jump is already on the gen stream)
         parts = _lib.PODS_GEN_JUMP | (_lib.PODS_GEN_RECORD if self._xch is not None else 0)
         if self._early:
-            self._on_gen_stream(_lib.PODS_GEN_RECORD, timer, "gen_jump_ahead")
+            if self._xch is not None:
+                self._on_gen_stream(_lib.PODS_GEN_RECORD, timer, "gen_jump_ahead")
+            else:   # one device: the jump is already on the gen stream; mark its end
+                ev = torch.cuda.Event()
+                ev.record(self.ctx.gen_stream())
+                self._ahead = ev
             self._ahead_parts |= _lib.PODS_GEN_JUMP
             self._early = False
         else:
@@ -376,7 +381,10 @@ class Generator:
         workgroups then held CUs the persistent SYRK's one-per-CU grid waited for (corr +0.5 ms,
         profiles/r5/rank_probe_c3_final.log).  Does nothing unless this run's jump and records
         were prefetched (its generation would otherwise run them on the main stream)."""
-        if self._xch is None or self._early or not (self._ahead_parts & _lib.PODS_GEN_RECORD):
+        # with the exchange: after the records prefetched one step earlier; on one device
+        # (JUMP_EARLY_N1): after the planes prefetched one step earlier consumed the jump states
+        ready = _lib.PODS_GEN_RECORD if self._xch is not None else _lib.PODS_GEN_PLANES
+        if self._early or not (self._ahead_parts & ready) or (self._xch is None and not JUMP_EARLY_N1):
             return
         tm = timer or (lambda name: _NullCtx())
         gs = self.ctx.gen_stream()
@@ -496,6 +504,9 @@ _XPB = os.environ.get("PODS_XPASS_BESIDE", "4")
 XPASS_BESIDE = _XPB in ("1", "2", "3", "4")
 XPASS_WHERE = 1 if _XPB in ("2", "4") else 0
 XPASS_CAP = _XPB in ("3", "4")
+# A/B: one device, the next run's jump-ahead beside this run's y/z pass instead of beside its mean
+# and residues (Generator.prefetch_jump_early)
+JUMP_EARLY_N1 = os.environ.get("PODS_JUMP_EARLY_N1", "0") == "1"
 SPLIT_MAX_VEC = 40   # leading pairs a 64-vector block resolves (nm <= 40; beyond, the fused solve)
 
 
@@ -1300,6 +1311,8 @@ def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=Non
     dist_, rank, world = _dist_info(dist)
     tm = timer or (lambda name: _NullCtx())
     gen = gen or Generator(setup, device=device, rank=rank, world=world, dist=dist_)
+    if prefetch_next and JUMP_EARLY_N1:
+        gen.prefetch_jump_early(timer)   # A/B: the next jump beside this generation's y/z pass
     with tm("generate"):
         snap = gen.generate()
     if prefetch_next:
