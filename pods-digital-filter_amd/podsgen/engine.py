@@ -398,7 +398,8 @@ class Generator:
 
     def prefetch_planes_beside_solver(self, timer=None):
         """Enqueue the NEXT run's random planes on the gen stream behind the marker the current
-        pods_syev records after tridiagonalisation range 2 (pods_syev_marker): from range 3 on
+        pods_syev records after tridiagonalisation range 4 (r6; range 2 until then:
+        pods_syev_marker, PLANES_AFTER): from range 3 on
         the k_trd workgroups hold at most 204 VGPRs per wave (2 waves per SIMD) and <= 42 KB of
         LDS, so the MT generator (16 VGPRs; LDS padded to 55 KB so at most 2 of its workgroups
         share a CU, PODS_GEN_BESIDE_SOLVER) runs beside them and every later range still finds
@@ -507,6 +508,10 @@ XPASS_CAP = _XPB in ("3", "4")
 # A/B: one device, the next run's jump-ahead beside this run's y/z pass instead of beside its mean
 # and residues (Generator.prefetch_jump_early)
 JUMP_EARLY_N1 = os.environ.get("PODS_JUMP_EARLY_N1", "0") == "1"
+# the tridiagonalisation range after which the next run's random planes start: 4 (r6; C3
+# 67.62-67.66 / 67.27-67.34 / 67.24-67.28 ms per step after range 2 / 3 / 4 with the x pass
+# beside the tail, profiles/r6/planes_marker_ab.log); PODS_PLANES_AFTER overrides
+PLANES_AFTER = int(os.environ.get("PODS_PLANES_AFTER", "4"))
 SPLIT_MAX_VEC = 40   # leading pairs a 64-vector block resolves (nm <= 40; beyond, the fused solve)
 
 
@@ -906,8 +911,10 @@ def eigen_solve_speculative(ctx: Context, C, ns, nm, tol_CN, tm, beside=None):
     lib, dev = ctx.lib, C.device
     lam_t = torch.empty(ns, dtype=torch.float64, device=dev)
     Y = torch.empty((ns, nm), dtype=torch.float64, device=dev)
-    if beside is not None:   # a marker behind tridiagonalisation range 2 for beside()
-        check(lib.pods_syev_marker(ctx.h, 2), "pods_syev_marker")
+    if beside is not None:   # a marker behind a tridiagonalisation range for beside()
+        # after range min(4, last - 1) (ranges of 512 columns; none for ns <= 1536, as before)
+        klast = (ns - 1) // 512
+        check(lib.pods_syev_marker(ctx.h, min(PLANES_AFTER, klast - 1) if klast > 2 else 2), "pods_syev_marker")
         if XPASS_BESIDE:     # and one behind the whole tridiagonalisation (or its eigenvalues)
             check(lib.pods_syev_marker_tail(ctx.h, XPASS_WHERE), "pods_syev_marker_tail")
     with tm("eigh"):
