@@ -820,6 +820,10 @@ int pods_df_exchange_bind(pods_ctx* c, void* send_dev, void* recv_dev) {
   return PODS_OK;
 }
 
+// workgroups per CU of the x pass beside the solver's tail, in halves (variant builds: -DPODS_XPASS_CAP=)
+#ifndef PODS_XPASS_CAP
+#define PODS_XPASS_CAP 4
+#endif
 int pods_df_generate_parts(pods_ctx* c, int parts) {
   PODS_TRY
   if (int e = check_ctx(c)) return e;
@@ -885,7 +889,7 @@ int pods_df_generate_parts(pods_ctx* c, int parts) {
     if ((parts & PODS_GEN_BESIDE_SOLVER) && hipGetDevice(&dev) == hipSuccess)
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     PODS_HIP(pods::launch_filter_x(c->NX, c->R.as<double>(), taps, p.ns, c->Sl, 3, chunk,
-                                   c->T1.as<double>(), c->stream, 0, -1, 2 * cus));
+                                   c->T1.as<double>(), c->stream, 0, -1, PODS_XPASS_CAP * cus / 2));
   }
   if (parts & PODS_GEN_YZPASS) {
     PODS_HIP(pods::launch_filter_yz(c->NY, c->T1.as<double>(), taps + c->NX, taps + c->NX + c->NY,
