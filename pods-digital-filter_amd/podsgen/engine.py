@@ -508,6 +508,11 @@ XPASS_CAP = _XPB in ("3", "4")
 # A/B: one device, the next run's jump-ahead beside this run's y/z pass instead of beside its mean
 # and residues (Generator.prefetch_jump_early)
 JUMP_EARLY_N1 = os.environ.get("PODS_JUMP_EARLY_N1", "0") == "1"
+# the speculative Fourier stage waits for T only, so it runs beside the spatial pass (r6; it had
+# waited for the spatial pass too and then ran beside the next step's y/z pass): C3 dft 4.9 -> 1.4
+# ms, main-stream generation 5.64 -> 5.22 ms, spatial 1.24 -> 1.47 ms, step 67.9-68.2 -> 67.9-68.0
+# (profiles/r6/dft_beside_spatial_ab.log); PODS_DFT_EARLY=0 restores the old order
+DFT_EARLY = os.environ.get("PODS_DFT_EARLY", "1") == "1"
 # the tridiagonalisation range after which the next run's random planes start: 4 (r6; C3
 # 67.62-67.66 / 67.27-67.34 / 67.24-67.28 ms per step after range 2 / 3 / 4 with the x pass
 # beside the tail, profiles/r6/planes_marker_ab.log); PODS_PLANES_AFTER overrides
@@ -1005,11 +1010,16 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
         # the device computes them (no idle gap for a round trip), then checks the truncation
         T, lam_t, Y, verify = eigen_solve_speculative(ctx, C, ns, nm, tol_CN, tm, beside=beside_solve)
         phi = torch.empty((snap.rowlen, nm), dtype=torch.float64, device=dev)
+        t_ready = None
+        if DFT_EARLY:   # T is complete here: the Fourier stage may start beside the spatial pass
+            t_ready = torch.cuda.Event()
+            t_ready.record()
         with tm("spatial"):
             check(lib.pods_spatial_modes_dev(ctx.h, ptr(T), nm, ptr(lam_t), nm, ptr(phi)), "pods_spatial_modes_dev")
-        t_ready = torch.cuda.Event()
-        t_ready.record()
-        if on_temporal is not None:   # the Fourier stage beside the spatial pass (redone on a miss)
+        if t_ready is None:
+            t_ready = torch.cuda.Event()
+            t_ready.record()
+        if on_temporal is not None:   # the Fourier stage (redone on a miss)
             on_temporal(T, nm, t_ready)
         try:
             lam_desc, nvalid = verify()
