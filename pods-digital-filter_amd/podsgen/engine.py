@@ -407,15 +407,18 @@ class Generator:
         / 4 with up to 3 or 6 generator workgroups per CU: the solver grows least this way
         (36.5 -> 36.9 ms against 37.1-37.2).  Called right after pods_syev is enqueued (after
         prefetch_jump); does nothing when no marker was recorded (ns <= 1536)."""
-        if self._ahead_parts != _lib.PODS_GEN_JUMP or self._xch is not None:
+        # (JUMP_WITH_PLANES, the default on one device: the next jump, not prefetched beside this
+        # run's mean and residues, goes here, ahead of the planes)
+        jump = JUMP_WITH_PLANES and self._ahead_parts == 0
+        if (self._ahead_parts != _lib.PODS_GEN_JUMP and not jump) or self._xch is not None:
             return
         gs = self.ctx.gen_stream()
         if self.ctx.lib.pods_stream_wait_marker(self.ctx.h, ctypes.c_void_p(gs.cuda_stream)) != _lib.PODS_OK:
             return
-        # (the x pass as well, capped at 2 workgroups per CU, measured no faster: generation
-        # -2.2 ms on the main stream, the solver +2.5 ms and the DFT beside it twice as long)
-        self._on_gen_stream(_lib.PODS_GEN_PLANES | _lib.PODS_GEN_BESIDE_SOLVER, timer, "gen_planes_ahead",
-                            wait_main=False)
+        # (the x pass beside ranges 3-7 as well, capped at 2 workgroups per CU, measured no faster
+        # in r3: generation -2.2 ms on the main stream, the solver +2.5 ms)
+        self._on_gen_stream((_lib.PODS_GEN_JUMP if jump else 0) | _lib.PODS_GEN_PLANES | _lib.PODS_GEN_BESIDE_SOLVER,
+                            timer, "gen_planes_ahead", wait_main=False)
         # and the next run's x pass, behind the solver's eigenvalues (pods_syev_marker_tail) with
         # 2 workgroups per CU: beside the eigenvectors of T (20 workgroups), the back-transformation
         # (64) and this run's modes, which leave most CUs idle -- the next generation on the main
@@ -508,6 +511,11 @@ XPASS_CAP = _XPB in ("3", "4")
 # A/B: one device, the next run's jump-ahead beside this run's y/z pass instead of beside its mean
 # and residues (Generator.prefetch_jump_early)
 JUMP_EARLY_N1 = os.environ.get("PODS_JUMP_EARLY_N1", "0") == "1"
+# one device: the next run's jump-ahead beside the late tridiagonalisation ranges, ahead of its
+# planes, instead of beside this run's mean and residues (r6: C3 67.10-67.11 -> 66.54-66.55 ms per
+# step, the correlation 0.65 ms faster, profiles/r6/jump_with_planes_ab.log);
+# PODS_JUMP_WITH_PLANES=0 restores the old place
+JUMP_WITH_PLANES = os.environ.get("PODS_JUMP_WITH_PLANES", "1") == "1"
 # the speculative Fourier stage waits for T only, so it runs beside the spatial pass (r6; it had
 # waited for the spatial pass too and then ran beside the next step's y/z pass): C3 dft 4.9 -> 1.4
 # ms, main-stream generation 5.64 -> 5.22 ms, spatial 1.24 -> 1.47 ms, step 67.9-68.2 -> 67.9-68.0
@@ -1332,7 +1340,7 @@ def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=Non
         gen.prefetch_jump_early(timer)   # A/B: the next jump beside this generation's y/z pass
     with tm("generate"):
         snap = gen.generate()
-    if prefetch_next:
+    if prefetch_next and not (JUMP_WITH_PLANES and gen._xch is None):
         gen.prefetch_jump(timer)
     pending = []
 
