@@ -1340,7 +1340,8 @@ def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=Non
         gen.prefetch_jump_early(timer)   # A/B: the next jump beside this generation's y/z pass
     with tm("generate"):
         snap = gen.generate()
-    if prefetch_next and not (JUMP_WITH_PLANES and gen._xch is None):
+    # (with the planes beside the solver -- ns > 1536, one device -- the jump goes there too)
+    if prefetch_next and not (JUMP_WITH_PLANES and gen._xch is None and (setup.ns - 1) // 512 > 2):
         gen.prefetch_jump(timer)
     pending = []
 
