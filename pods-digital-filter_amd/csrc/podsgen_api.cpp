@@ -315,6 +315,9 @@ struct pods_ctx {
   // the same behind the whole tridiagonalisation (pods_syev_marker_tail)
   hipEvent_t marker_tail = nullptr;
   bool marker_tail_req = false, marker_tail_recorded = false;
+  // pods_syev: k_larft on a second stream beside the bisection and eigenvectors of T
+  hipStream_t aux = nullptr;
+  hipEvent_t aux_fork = nullptr, aux_join = nullptr;
   int marker_tail_where = 0;  // 0: behind the tridiagonalisation, 1: behind the eigenvalues
   // pods_set_shared_device: the per-device lock file persistent launches hold (-1: not shared)
   int lock_fd = -1;
@@ -530,6 +533,9 @@ int pods_destroy(pods_ctx* c) {
   }
   if (c->marker) (void)hipEventDestroy(c->marker);
   if (c->marker_tail) (void)hipEventDestroy(c->marker_tail);
+  if (c->aux_fork) (void)hipEventDestroy(c->aux_fork);
+  if (c->aux_join) (void)hipEventDestroy(c->aux_join);
+  if (c->aux) (void)hipStreamDestroy(c->aux);
   if (c->lock_fd >= 0) (void)close(c->lock_fd);
   delete c;
   return PODS_OK;
@@ -1680,6 +1686,20 @@ int pods_syev(pods_ctx* c, const double* C, int n, int nvec, double* lam_desc, d
   // back-transformation kernels it shared CUs with.)
   PODS_HIP(ensure(c->e_cnt, pods::tri_grid_bytes()));
   int* gcnt = c->e_cnt.as<int>();
+  // the compact-WY blocks of the back-transformation (k_larft) need V and tau only: on a second
+  // stream beside the bisection and the eigenvectors of T, joined before k_bt_fused
+  const bool fork = nvec > 0 && n > 1;
+  if (fork) {
+    const int nblk = std::max((n - 1 + 63) / 64, 1);
+    PODS_HIP(ensure(c->e_t, (size_t)nblk * 64 * 64 * sizeof(double)));
+    if (!c->aux) PODS_HIP(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+    if (!c->aux_fork) PODS_HIP(hipEventCreateWithFlags(&c->aux_fork, hipEventDisableTiming));
+    if (!c->aux_join) PODS_HIP(hipEventCreateWithFlags(&c->aux_join, hipEventDisableTiming));
+    PODS_HIP(hipEventRecord(c->aux_fork, c->stream));
+    PODS_HIP(hipStreamWaitEvent(c->aux, c->aux_fork, 0));
+    PODS_HIP(pods::launch_larft(c->e_v.as<double>(), n, tau, n, c->e_t.as<double>(), c->aux));
+    PODS_HIP(hipEventRecord(c->aux_join, c->aux));
+  }
   PODS_HIP(pods::launch_tri_eigvals(D, E, n, bounds, lam_desc, gcnt, c->stream));
   if (c->marker_tail_req && c->marker_tail) {  // pods_syev_marker_tail(ctx, 1): behind the eigenvalues
     PODS_HIP(hipEventRecord(c->marker_tail, c->stream));
@@ -1694,10 +1714,11 @@ int pods_syev(pods_ctx* c, const double* C, int n, int nvec, double* lam_desc, d
     PODS_HIP(ensure(c->e_w2, pods::bt_w2_bytes(nvec)));
     PODS_HIP(pods::launch_tri_eigvecs(D, E, n, lam_desc, bounds, nvec, c->e_inv.as<double>(), vec,
                                       c->stream));
+    if (fork) PODS_HIP(hipStreamWaitEvent(c->stream, c->aux_join, 0));
     PODS_HIP(pods::launch_back_transform(c->e_v.as<double>(), n, tau, n, nvec, c->e_t.as<double>(),
                                          c->e_part.as<double>(), c->e_w2.as<double>(),
                                          c->e_flags.as<uint32_t>() + 1, vec,
-                                         c->stream));
+                                         c->stream, /*skip_larft=*/fork));
   }
   return lk.release();
   PODS_CATCH

@@ -1688,11 +1688,11 @@ hipError_t launch_orth(const double* lam_desc, const double* bounds, int n, int 
 
 hipError_t launch_back_transform(const double* V, int64_t ldv, const double* tau, int n, int nvec,
                                  double* Tg, double* part, double* W2, uint32_t* abortw, double* Z,
-                                 hipStream_t st) {
+                                 hipStream_t st, bool skip_larft) {
   const int nref = n - 1;
   if (nref <= 0 || nvec <= 0) return hipSuccess;
   const int nblk = (nref + eig::WB - 1) / eig::WB;
-  hipLaunchKernelGGL(eig::k_larft, dim3(nblk), dim3(256), 0, st, V, ldv, tau, n, Tg);
+  if (!skip_larft) hipLaunchKernelGGL(eig::k_larft, dim3(nblk), dim3(256), 0, st, V, ldv, tau, n, Tg);
   int CR = 0, G = 0;
   bt_plan(n, nvec, &CR, &G);
   hipError_t e = hipMemsetAsync(part, 0, bt_part_bytes(n, nvec), st);
@@ -1715,6 +1715,14 @@ hipError_t launch_back_transform(const double* V, int64_t ldv, const double* tau
   else
     hipLaunchKernelGGL(eig::k_bt_fused<64>, dim3(G), dim3(256), lds, st, V, ldv, (const double*)Tg, n,
                        nvec, nblk, Z, nvec, part, W2, abortw);
+  return hipGetLastError();
+}
+
+hipError_t launch_larft(const double* V, int64_t ldv, const double* tau, int n, double* Tg, hipStream_t st) {
+  const int nref = n - 1;
+  if (nref <= 0) return hipSuccess;
+  const int nblk = (nref + eig::WB - 1) / eig::WB;
+  hipLaunchKernelGGL(eig::k_larft, dim3(nblk), dim3(256), 0, st, V, ldv, tau, n, Tg);
   return hipGetLastError();
 }
 

@@ -142,9 +142,12 @@ hipError_t launch_tri_eigvecs(const double* D, const double* E, int n, const dou
                               const double* bounds, int nvec, double* X, double* Z, hipStream_t st);
 // Z <- Q Z with Q = H_0 ... H_{n-2} (one k_larft launch + one persistent k_bt_fused launch);
 // Tg: ceil((n-1)/64) x 64 x 64, part: bt_part_bytes, W2: bt_w2_bytes, abortw: 0 on entry
+// larft_st: the stream for k_larft (it needs V and tau only); the caller orders `st` behind it
+// (null: k_larft on `st` too)
 hipError_t launch_back_transform(const double* V, int64_t ldv, const double* tau, int n, int nvec,
                                  double* Tg, double* part, double* W2, uint32_t* abortw, double* Z,
-                                 hipStream_t st);
+                                 hipStream_t st, bool skip_larft = false);
+hipError_t launch_larft(const double* V, int64_t ldv, const double* tau, int n, double* Tg, hipStream_t st);
 void bt_plan(int n, int nvec, int* CR, int* G);
 // cluster modified Gram-Schmidt of the nvec eigenvector columns of Z (k_orth)
 hipError_t launch_orth(const double* lam_desc, const double* bounds, int n, int nvec, double* Z, int ldz,
