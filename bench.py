@@ -54,6 +54,9 @@ CONFIGS = {
 }
 
 
+# A/B: one device, the spatial-mode pass beside the next step's generation (engine.pipeline overlap_spatial)
+OVERLAP_SPATIAL = os.environ.get("PODS_OVERLAP_SPATIAL", "0") == "1"
+
 def c5_profile(J, K):
     """a deterministic inhomogeneous SPD stress field on a tanh jet,
     uu = vv = ww = (0.02 U)^2 scaled, uv/uw/vw = rho sqrt(..) with a smooth rho in (-0.4, 0.4),
@@ -450,7 +453,7 @@ def main():
             runner.step(timer=timer, prefetch_next=ahead)
             return None, None, None
         return E.pipeline(setup, device=device, dist=d, gen=gen, timer=timer, spectrum=spectrum, backlog=backlog,
-                          prefetch_next=ahead)
+                          prefetch_next=ahead, overlap_spatial=OVERLAP_SPATIAL)
 
     # ahead: the next step's MT19937 jump-ahead runs on a second stream beside this step's mean
     # and centring (Generator.prefetch_jump).  The last warm-up step and the last timed step do

@@ -108,6 +108,13 @@ class Context:
             self._side = torch.cuda.Stream(device=self.device)
         return self._side
 
+    def spatial_stream(self):
+        """The stream one device's spatial-mode pass goes to when it may overlap the next run's
+        generation (pipeline(overlap_spatial=True))."""
+        if getattr(self, "_spatial", None) is None:
+            self._spatial = torch.cuda.Stream(device=self.device)
+        return self._spatial
+
     def gen_stream(self):
         """The stream the next run's random planes and x pass go to (Generator.prefetch_next)."""
         if getattr(self, "_gen", None) is None:
@@ -457,6 +464,7 @@ class PODResult:
     phi: "torch.Tensor"           # (3P_local, nm) spatial modes
     C: Optional["torch.Tensor"] = None
     timings: dict = field(default_factory=dict)
+    phi_ready: Optional["torch.cuda.Event"] = None   # set when phi is computed on another stream
 
 
 def _dist_info(dist):
@@ -979,7 +987,8 @@ def pod_head(snap: DeviceSnapshots, world=1, timer=None, partial=None):
 
 
 def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=False,
-            keep_C=False, timer=None, on_temporal=None, spectrum=None, before_eigen=None, beside_solve=None):
+            keep_C=False, timer=None, on_temporal=None, spectrum=None, before_eigen=None, beside_solve=None,
+            spatial_stream=None):
     """PODFS.POD (PODFS.py:1294-1393) with correct_for_cell_volumes='false'.
 
     spectrum: a SpectrumQueue -- the eigenvalues past the nm leading ones are then computed by
@@ -1019,11 +1028,23 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
         T, lam_t, Y, verify = eigen_solve_speculative(ctx, C, ns, nm, tol_CN, tm, beside=beside_solve)
         phi = torch.empty((snap.rowlen, nm), dtype=torch.float64, device=dev)
         t_ready = None
-        if DFT_EARLY:   # T is complete here: the Fourier stage may start beside the spatial pass
-            t_ready = torch.cuda.Event()
+        if DFT_EARLY or spatial_stream is not None:   # T is complete here: the Fourier stage (and
+            t_ready = torch.cuda.Event()                # with spatial_stream the spatial pass) may start
             t_ready.record()
-        with tm("spatial"):
-            check(lib.pods_spatial_modes_dev(ctx.h, ptr(T), nm, ptr(lam_t), nm, ptr(phi)), "pods_spatial_modes_dev")
+        phi_ready = None
+        if spatial_stream is not None:   # the spatial pass off the main stream (the caller joins it)
+            spatial_stream.wait_event(t_ready)
+            for x in (T, lam_t, phi):
+                x.record_stream(spatial_stream)
+            with ctx.on_stream(spatial_stream):
+                with tm("spatial"):
+                    check(lib.pods_spatial_modes_dev(ctx.h, ptr(T), nm, ptr(lam_t), nm, ptr(phi)),
+                          "pods_spatial_modes_dev")
+                phi_ready = torch.cuda.Event()
+                phi_ready.record(spatial_stream)
+        else:
+            with tm("spatial"):
+                check(lib.pods_spatial_modes_dev(ctx.h, ptr(T), nm, ptr(lam_t), nm, ptr(phi)), "pods_spatial_modes_dev")
         if t_ready is None:
             t_ready = torch.cuda.Event()
             t_ready.record()
@@ -1037,6 +1058,9 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
         if lam_desc is not None and nvalid >= nm:
             nmt = nm
         else:   # fewer valid modes than nm (or no spectrum): the host path
+            if phi_ready is not None:   # the speculative spatial pass is superseded
+                torch.cuda.current_stream(dev).wait_event(phi_ready)
+                phi_ready = None
             if lam_desc is not None:
                 nmt = nvalid
                 ncols = max(nmt, 1)
@@ -1060,7 +1084,7 @@ def run_pod(snap: DeviceSnapshots, nm, tol_CN=1.0e-15, dist=None, full_temporal=
             if on_temporal is not None:   # supersedes the speculative launch
                 on_temporal(T, nmt, t_ready)
         return PODResult(energy=lam_desc, num_valid=nvalid, nm=nmt, mean=mean, T=T, phi=phi[:, :nmt],
-                         C=C if keep_C else None)
+                         C=C if keep_C else None, phi_ready=phi_ready)
     return pod_tail(ctx, snap, C, mean, nm, tol_CN, dist, full_temporal, keep_C, timer, on_temporal, spectrum)
 
 
@@ -1325,17 +1349,34 @@ class FourierBacklog:
 
 
 def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=None, gen=None, spectrum=None,
-             backlog=None, prefetch_next=False):
+             backlog=None, prefetch_next=False, overlap_spatial=False):
     """The whole hot path; returns (Generator, PODResult, FourierResult | None).
     spectrum: a SpectrumQueue for multi-step runs (see run_pod).  backlog: a FourierBacklog --
     this step's Fourier result is then finished during the next step (or by backlog.flush())
     and the returned FourierResult is None.  prefetch_next: a next run follows on this
     generator; its random planes and x pass are enqueued on the gen stream right after this
     run's generation: the MT19937 jump-ahead, beside this run's mean and centring
-    (Generator.prefetch_jump)."""
+    (Generator.prefetch_jump).
+
+    overlap_spatial (one device, multi-step runs): consecutive runs alternate between the two
+    snapshot banks (pods_select_snapshots) and this run's spatial-mode pass goes to its own stream
+    behind the temporal modes, so the next run's generation (into the other bank) starts beside
+    it; pod.phi is then complete once pod.phi_ready has passed (the main stream waits for it
+    before the bank is generated into again, and at once when no next run follows)."""
     dist_, rank, world = _dist_info(dist)
     tm = timer or (lambda name: _NullCtx())
     gen = gen or Generator(setup, device=device, rank=rank, world=world, dist=dist_)
+    overlap = overlap_spatial and world == 1
+    if overlap:
+        bank = getattr(gen, "_sp_bank", 0)
+        gen._sp_bank = bank ^ 1
+        check(gen.ctx.lib.pods_select_snapshots(gen.ctx.h, bank), "pods_select_snapshots")
+        waits = getattr(gen, "_sp_wait", None)
+        if waits is None:
+            waits = gen._sp_wait = {}
+        ev = waits.pop(bank, None)
+        if ev is not None:   # the spatial pass that read this bank two runs ago
+            torch.cuda.current_stream(gen.ctx.device).wait_event(ev)
     if prefetch_next and JUMP_EARLY_N1:
         gen.prefetch_jump_early(timer)   # A/B: the next jump beside this generation's y/z pass
     with tm("generate"):
@@ -1354,7 +1395,13 @@ def pipeline(setup: DFSetup, device=0, dist=None, full_temporal=False, timer=Non
             backlog.finish_pending()
     beside = (lambda: gen.prefetch_planes_beside_solver(timer)) if prefetch_next else None
     pod = run_pod(snap, setup.nm, dist=dist_, full_temporal=full_temporal, timer=timer,
-                  on_temporal=start_fourier, spectrum=spectrum, before_eigen=before_eigen, beside_solve=beside)
+                  on_temporal=start_fourier, spectrum=spectrum, before_eigen=before_eigen, beside_solve=beside,
+                  spatial_stream=gen.ctx.spatial_stream() if overlap else None)
+    if pod.phi_ready is not None:
+        if prefetch_next:
+            gen._sp_wait[bank] = pod.phi_ready
+        else:
+            torch.cuda.current_stream(gen.ctx.device).wait_event(pod.phi_ready)
     # the last launch counts (a speculative Fourier launch is superseded when the truncation
     # check redoes the modes)
     if backlog is not None:

@@ -290,6 +290,43 @@ def test_planes_prefetched_beside_solver(ctx):
     c2.close()
 
 
+def test_spatial_pass_overlapping_next_generation(ctx):
+    """One device, three runs with overlap_spatial (engine.pipeline): the runs alternate between
+    the two snapshot banks and each run's spatial-mode pass runs on its own stream beside the next
+    run's generation.  Every run's Phi (read after pod.phi_ready), mean, energy and Fourier
+    coefficients equal the plain runs' bit for bit, and consecutive runs of different seeds differ
+    (so a bank mix-up would show)."""
+    s = podsgen.DFSetup(jma=24, kma=20, ns=2560, seed=41)
+    g1 = E.Generator(s, ctx=ctx)
+    got = []
+    for k, seed in enumerate((41, 42, 43)):
+        podsgen.check(ctx.lib.pods_df_set_seed(ctx.h, seed), "pods_df_set_seed")
+        _, p, f = E.pipeline(s, gen=g1, prefetch_next=False, overlap_spatial=True)
+        assert p.phi_ready is not None
+        p.phi_ready.synchronize()
+        got.append((p.phi.cpu().numpy(), p.mean.cpu().numpy(), p.energy, f.c))
+    c2 = E.Context(0)
+    g2 = E.Generator(s, ctx=c2)
+    for k, seed in enumerate((41, 42, 43)):
+        podsgen.check(c2.lib.pods_df_set_seed(c2.h, seed), "pods_df_set_seed")
+        _, p, f = E.pipeline(s, gen=g2)
+        assert p.phi_ready is None
+        phi, mean, energy, c = got[k]
+        assert np.array_equal(phi, p.phi.cpu().numpy()), k
+        assert np.array_equal(mean, p.mean.cpu().numpy()) and np.array_equal(energy, p.energy), k
+        assert np.array_equal(c, f.c), k
+    assert not np.array_equal(got[0][0], got[1][0])
+    # one seed, the next runs prefetched (the deferred join: a run's Phi completes beside the
+    # next run's generation)
+    podsgen.check(ctx.lib.pods_df_set_seed(ctx.h, 41), "pods_df_set_seed")
+    for k in range(3):
+        _, p, f = E.pipeline(s, gen=g1, prefetch_next=k < 2, overlap_spatial=True)
+        p.phi_ready.synchronize()
+        assert np.array_equal(p.phi.cpu().numpy(), got[0][0]), k
+        assert np.array_equal(f.c, got[0][3]), k
+    c2.close()
+
+
 def test_speculative_modes_fallback(ctx):
     """One device: the temporal/spatial modes are enqueued behind pods_syev for nm_trunc = nm
     before the host reads the spectrum.  With fewer valid modes than nm (a rank-6 correlation,
